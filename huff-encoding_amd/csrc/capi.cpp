@@ -1,0 +1,434 @@
+// capi.cpp — the extern "C" boundary (include/huffgpu.h).
+//
+// Each entry point converts huff::Status into an int code plus the
+// thread-local last-error message; nothing throws across the ABI.
+#include <cstring>
+#include <exception>
+#include <new>
+#include <string>
+
+#include "runtime/runtime.hpp"
+
+namespace {
+
+thread_local std::string t_last_error;
+thread_local uint8_t t_missing = 0;
+
+int report(const huff::Status& s) {
+    if (s.code != HUFF_OK) {
+        t_last_error = s.msg;
+        if (s.code == HUFF_E_MISSING_LETTER) t_missing = s.missing_letter;
+    }
+    return s.code;
+}
+
+int fail(int code, const char* msg) {
+    t_last_error = msg;
+    return code;
+}
+
+template <class F>
+int guarded(F&& f) {
+    try {
+        return report(f());
+    } catch (const std::bad_alloc&) {
+        return fail(HUFF_E_INVALID_ARG, "host allocation failed");
+    } catch (const std::exception& e) {
+        return fail(HUFF_E_INVALID_ARG, e.what());
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* huff_last_error(void) { return t_last_error.c_str(); }
+uint8_t huff_last_missing_letter(void) { return t_missing; }
+const char* huff_version(void) { return "huffgpu 0.1 (gfx950)"; }
+
+// --------------------------------------------------------------------------
+int huff_ctx_create(int device, huff_ctx** out) {
+    if (!out) return fail(HUFF_E_INVALID_ARG, "null output");
+    *out = nullptr;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count == 0)
+        return fail(HUFF_E_NO_DEVICE, "no HIP device available (the GPU codec has no CPU fallback)");
+    if (device < 0 || device >= count) return fail(HUFF_E_INVALID_ARG, "device index out of range");
+    return guarded([&]() -> huff::Status {
+        auto* c = new huff_ctx();
+        c->device = device;
+        huff::Status st = c->activate();
+        if (!st && hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess)
+            st = huff::Status::err(HUFF_E_HIP, "hipStreamCreate failed");
+        if (st) {
+            delete c;
+            return st;
+        }
+        c->stream = c->own;
+        *out = c;
+        return huff::Status::ok();
+    });
+}
+
+int huff_ctx_destroy(huff_ctx* ctx) {
+    if (!ctx) return HUFF_OK;
+    hipSetDevice(ctx->device);
+    hipStreamSynchronize(ctx->stream);
+    for (auto& p : ctx->pending) {
+        hipEventDestroy(p.a);
+        hipEventDestroy(p.b);
+    }
+    for (auto e : ctx->free_events) hipEventDestroy(e);
+    if (ctx->own) hipStreamDestroy(ctx->own);
+    delete ctx;
+    return HUFF_OK;
+}
+
+int huff_ctx_set_stream(huff_ctx* ctx, void* hip_stream) {
+    if (!ctx) return fail(HUFF_E_INVALID_ARG, "null context");
+    ctx->stream = hip_stream ? static_cast<hipStream_t>(hip_stream) : ctx->own;
+    return HUFF_OK;
+}
+
+int huff_ctx_synchronize(huff_ctx* ctx) {
+    if (!ctx) return fail(HUFF_E_INVALID_ARG, "null context");
+    return guarded([&] {
+        HUFF_TRY(ctx->activate());
+        return ctx->sync();
+    });
+}
+
+int huff_ctx_device(const huff_ctx* ctx) { return ctx ? ctx->device : -1; }
+
+int huff_ctx_set_timing(huff_ctx* ctx, int on) {
+    if (!ctx) return fail(HUFF_E_INVALID_ARG, "null context");
+    ctx->timing = on != 0;
+    return HUFF_OK;
+}
+
+int huff_ctx_kernel_time(huff_ctx* ctx, const char* name, double* total_ms, uint64_t* launches) {
+    if (!ctx || !name || !total_ms || !launches) return fail(HUFF_E_INVALID_ARG, "null argument");
+    return guarded([&] {
+        HUFF_TRY(ctx->activate());
+        HUFF_TRY(ctx->collect_timing());
+        auto it = ctx->kstats.find(name);
+        *total_ms = it == ctx->kstats.end() ? 0.0 : it->second.first;
+        *launches = it == ctx->kstats.end() ? 0 : it->second.second;
+        return huff::Status::ok();
+    });
+}
+
+int huff_ctx_reset_timing(huff_ctx* ctx) {
+    if (!ctx) return fail(HUFF_E_INVALID_ARG, "null context");
+    return guarded([&] {
+        HUFF_TRY(ctx->activate());
+        HUFF_TRY(ctx->collect_timing());
+        ctx->kstats.clear();
+        return huff::Status::ok();
+    });
+}
+
+// --------------------------------------------------------------------------
+void huff_weights_new(huff_byte_weights* out) {
+    if (out) std::memset(out, 0, sizeof(*out));
+}
+
+static void to_c(const huff::ByteWeights& w, huff_byte_weights* out) {
+    for (int b = 0; b < 256; ++b) out->weights[b] = w.weights[b];
+    out->len = w.len;
+}
+
+static huff::ByteWeights from_c(const huff_byte_weights* in) {
+    huff::ByteWeights w;
+    for (int b = 0; b < 256; ++b) w.weights[b] = in->weights[b];
+    w.len = in->len;
+    return w;
+}
+
+int huff_weights_from_bytes(huff_ctx* ctx, const uint8_t* bytes, size_t n, huff_byte_weights* out) {
+    if (!ctx || !out || (!bytes && n)) return fail(HUFF_E_INVALID_ARG, "null argument");
+    return guarded([&] {
+        huff::ByteWeights w;
+        HUFF_TRY(huff::weights_from_host(ctx, bytes, n, w));
+        to_c(w, out);
+        return huff::Status::ok();
+    });
+}
+
+int huff_weights_threaded_from_bytes(huff_ctx* ctx, const uint8_t* bytes, size_t n, size_t thread_num,
+                                     huff_byte_weights* out) {
+    if (!ctx || !out || (!bytes && n)) return fail(HUFF_E_INVALID_ARG, "null argument");
+    return guarded([&] {
+        huff::ByteWeights w;
+        HUFF_TRY(huff::weights_threaded_from_host(ctx, bytes, n, thread_num, w));
+        to_c(w, out);
+        return huff::Status::ok();
+    });
+}
+
+void huff_weights_add(huff_byte_weights* self, const huff_byte_weights* other) {
+    if (!self || !other) return;
+    huff::ByteWeights a = from_c(self);
+    a.add(from_c(other));
+    to_c(a, self);
+}
+
+size_t huff_weights_iter(const huff_byte_weights* w, uint8_t letters[257], uint64_t weights[257]) {
+    if (!w || !letters || !weights) return 0;
+    return from_c(w).iter(letters, weights);
+}
+
+// --------------------------------------------------------------------------
+int huff_tree_from_weights(const huff_byte_weights* w, huff_tree** out) {
+    if (!w || !out) return fail(HUFF_E_INVALID_ARG, "null argument");
+    *out = nullptr;
+    return guarded([&] {
+        auto t = std::make_unique<huff_tree>();
+        HUFF_TRY(huff::HuffTree::from_weights(from_c(w), t->t));
+        *out = t.release();
+        return huff::Status::ok();
+    });
+}
+
+int huff_tree_clone(const huff_tree* t, huff_tree** out) {
+    if (!t || !out) return fail(HUFF_E_INVALID_ARG, "null argument");
+    return guarded([&] {
+        auto c = std::make_unique<huff_tree>();
+        c->t = t->t;
+        *out = c.release();
+        return huff::Status::ok();
+    });
+}
+
+void huff_tree_free(huff_tree* t) { delete t; }
+
+size_t huff_tree_num_leaves(const huff_tree* t) { return t ? t->t.num_leaves() : 0; }
+uint64_t huff_tree_root_weight(const huff_tree* t) { return t ? t->t.root_weight() : 0; }
+
+int huff_tree_read_codes(const huff_tree* t, uint64_t code[256], uint8_t len[256]) {
+    if (!t || !code || !len) return fail(HUFF_E_INVALID_ARG, "null argument");
+    const huff::EncTables& e = t->enc_tables();
+    std::memcpy(code, e.code, sizeof(e.code));
+    std::memcpy(len, e.len, sizeof(e.len));
+    if (!e.fits64) return fail(HUFF_E_CODE_TOO_LONG, "a code is longer than 64 bits; use huff_tree_code_bits");
+    return HUFF_OK;
+}
+
+int huff_tree_code_bits(const huff_tree* t, uint8_t letter, uint8_t* bits, size_t cap, size_t* nbits) {
+    if (!t || !nbits) return fail(HUFF_E_INVALID_ARG, "null argument");
+    std::array<std::vector<uint8_t>, 256> codes;
+    t->t.read_codes(codes);
+    const auto& c = codes[letter];
+    *nbits = c.size();
+    if (cap < c.size()) return fail(HUFF_E_BUFFER_TOO_SMALL, "bit buffer too small");
+    if (bits && !c.empty()) std::memcpy(bits, c.data(), c.size());
+    return HUFF_OK;
+}
+
+int huff_tree_as_bin(const huff_tree* t, uint8_t* out, size_t cap, size_t* nbits) {
+    if (!t || !nbits) return fail(HUFF_E_INVALID_ARG, "null argument");
+    std::vector<uint8_t> bits = t->t.as_bin();
+    *nbits = bits.size();
+    std::vector<uint8_t> packed = huff::pack_msb0(bits);
+    if (cap < packed.size()) return fail(HUFF_E_BUFFER_TOO_SMALL, "output buffer too small");
+    if (out) std::memcpy(out, packed.data(), packed.size());
+    return HUFF_OK;
+}
+
+int huff_tree_try_from_bin(const uint8_t* bits, size_t nbits, huff_tree** out) {
+    if ((!bits && nbits) || !out) return fail(HUFF_E_INVALID_ARG, "null argument");
+    *out = nullptr;
+    return guarded([&] {
+        auto t = std::make_unique<huff_tree>();
+        HUFF_TRY(huff::HuffTree::try_from_bin(huff::unpack_msb0(bits, nbits), t->t));
+        *out = t.release();
+        return huff::Status::ok();
+    });
+}
+
+// --------------------------------------------------------------------------
+int huff_cd_new(const uint8_t* comp, size_t len, uint8_t padding, const huff_tree* t, huff_compress_data** out) {
+    if (!t || !out || (!comp && len)) return fail(HUFF_E_INVALID_ARG, "null argument");
+    *out = nullptr;
+    if (len == 0) return fail(HUFF_E_EMPTY_COMP, "provided comp_bytes are empty");       // comp.rs:56-58
+    if (padding > 7) return fail(HUFF_E_PADDING, "padding bits cannot be larger than 7");  // comp.rs:59-61
+    return guarded([&] {
+        auto cd = std::make_unique<huff_compress_data>();
+        cd->comp.assign(comp, comp + len);
+        cd->padding = padding;
+        cd->tree = new huff_tree();
+        cd->tree->t = t->t;
+        *out = cd.release();
+        return huff::Status::ok();
+    });
+}
+
+void huff_cd_free(huff_compress_data* cd) { delete cd; }
+
+int huff_cd_comp_bytes(const huff_compress_data* cd, const uint8_t** ptr, size_t* len) {
+    if (!cd || !ptr || !len) return fail(HUFF_E_INVALID_ARG, "null argument");
+    *ptr = cd->comp.data();
+    *len = cd->comp.size();
+    return HUFF_OK;
+}
+
+uint8_t huff_cd_padding(const huff_compress_data* cd) { return cd ? cd->padding : 0; }
+const huff_tree* huff_cd_tree(const huff_compress_data* cd) { return cd ? cd->tree : nullptr; }
+int huff_cd_has_index(const huff_compress_data* cd) { return cd && cd->index ? 1 : 0; }
+
+int huff_cd_to_bytes(const huff_compress_data* cd, uint8_t* out, size_t cap, size_t* out_len) {
+    if (!cd || !out_len) return fail(HUFF_E_INVALID_ARG, "null argument");
+    return guarded([&] {
+        std::vector<uint8_t> v;
+        HUFF_TRY(huff::container_to_bytes(cd->tree->t, cd->comp.data(), cd->comp.size(), cd->padding, v));
+        *out_len = v.size();
+        if (cap < v.size()) return huff::Status::err(HUFF_E_BUFFER_TOO_SMALL, "output buffer too small");
+        if (out) std::memcpy(out, v.data(), v.size());
+        return huff::Status::ok();
+    });
+}
+
+int huff_cd_try_from_bytes(const uint8_t* bytes, size_t n, huff_compress_data** out) {
+    if ((!bytes && n) || !out) return fail(HUFF_E_INVALID_ARG, "null argument");
+    *out = nullptr;
+    return guarded([&] {
+        auto cd = std::make_unique<huff_compress_data>();
+        cd->tree = new huff_tree();
+        size_t off = 0, len = 0;
+        HUFF_TRY(huff::container_from_bytes(bytes, n, cd->tree->t, cd->padding, off, len));
+        cd->comp.assign(bytes + off, bytes + off + len);
+        *out = cd.release();
+        return huff::Status::ok();
+    });
+}
+
+int huff_compress_with_tree(huff_ctx* ctx, const uint8_t* bytes, size_t n, const huff_tree* t,
+                            huff_compress_data** out) {
+    if (!ctx || !t || !out || (!bytes && n)) return fail(HUFF_E_INVALID_ARG, "null argument");
+    return guarded([&] { return huff::compress_host(ctx, bytes, n, t, out); });
+}
+
+int huff_compress_bytes(huff_ctx* ctx, const uint8_t* bytes, size_t n, huff_compress_data** out) {
+    if (!ctx || !out || (!bytes && n)) return fail(HUFF_E_INVALID_ARG, "null argument");
+    if (n == 0) return fail(HUFF_E_EMPTY_WEIGHTS, "provided empty weights");  // from_weights panics first
+    return guarded([&] { return huff::compress_host(ctx, bytes, n, nullptr, out); });
+}
+
+int huff_decompress(huff_ctx* ctx, const huff_compress_data* cd, uint8_t* out, size_t cap, size_t* out_len) {
+    if (!ctx || !cd || !out_len || (!out && cap)) return fail(HUFF_E_INVALID_ARG, "null argument");
+    return guarded([&] { return huff::decompress_host(ctx, cd, out, cap, out_len); });
+}
+
+// --------------------------------------------------------------------------
+int huff_enc_create(huff_ctx* ctx, const uint8_t* d_in, size_t n, huff_enc** out) {
+    if (!ctx || !out || (!d_in && n)) return fail(HUFF_E_INVALID_ARG, "null argument");
+    *out = nullptr;
+    return guarded([&] {
+        HUFF_TRY(ctx->activate());
+        auto e = std::make_unique<huff_enc>();
+        HUFF_TRY(e->init(ctx, d_in, n));
+        *out = e.release();
+        return huff::Status::ok();
+    });
+}
+
+void huff_enc_free(huff_enc* e) {
+    if (!e) return;
+    if (e->ctx) hipSetDevice(e->ctx->device);
+    delete e;
+}
+
+int huff_enc_hist(huff_enc* e, uint64_t weights[256]) {
+    if (!e) return fail(HUFF_E_INVALID_ARG, "null argument");
+    return guarded([&] {
+        HUFF_TRY(e->hist());
+        if (weights) std::memcpy(weights, e->w, sizeof(e->w));
+        return huff::Status::ok();
+    });
+}
+
+int huff_enc_bits(huff_enc* e, const huff_tree* t, uint64_t* total_bits) {
+    if (!e || !t || !total_bits) return fail(HUFF_E_INVALID_ARG, "null argument");
+    return guarded([&] { return e->bits(t, total_bits); });
+}
+
+int huff_enc_pack(huff_enc* e, const huff_tree* t, uint64_t bit_base, const uint8_t* prev_tail, size_t prev_tail_len,
+                  uint8_t* d_out, size_t out_cap, uint64_t* total_bits) {
+    if (!e || !t || !d_out || (!prev_tail && prev_tail_len)) return fail(HUFF_E_INVALID_ARG, "null argument");
+    if (reinterpret_cast<uintptr_t>(d_out) & 15) return fail(HUFF_E_INVALID_ARG, "d_out must be 16-byte aligned");
+    return guarded([&] { return e->pack(t, bit_base, prev_tail, prev_tail_len, d_out, out_cap, total_bits); });
+}
+
+int huff_enc_decode(huff_enc* e, const huff_tree* t, const uint8_t* d_comp, uint8_t* d_out) {
+    if (!e || !t || !d_comp || (!d_out && e->n)) return fail(HUFF_E_INVALID_ARG, "null argument");
+    return guarded([&] {
+        const uint64_t bytes = ((e->bit_base & 7) + e->total_bits + 7) / 8;
+        return e->decode(t, d_comp, bytes, d_out);
+    });
+}
+
+int huff_dev_generate(huff_ctx* ctx, int kind, uint64_t seed, uint64_t offset, const uint64_t* cdf, uint8_t* d_out,
+                      size_t n) {
+    if (!ctx || (!d_out && n) || (kind == 1 && !cdf)) return fail(HUFF_E_INVALID_ARG, "null argument");
+    return guarded([&]() -> huff::Status {
+        HUFF_TRY(ctx->activate());
+        void* d_cdf = nullptr;
+        if (kind == 1) {
+            if (hipMalloc(&d_cdf, 2048) != hipSuccess) return huff::Status::err(HUFF_E_HIP, "hipMalloc failed");
+            hipMemcpy(d_cdf, cdf, 2048, hipMemcpyHostToDevice);
+        }
+        hipError_t er = huff::dev::launch_generate(kind, seed, offset, static_cast<const uint64_t*>(d_cdf), d_out, n,
+                                                   ctx->stream);
+        hipStreamSynchronize(ctx->stream);
+        if (d_cdf) hipFree(d_cdf);
+        if (er != hipSuccess) return huff::Status::err(HUFF_E_HIP, hipGetErrorString(er));
+        return huff::Status::ok();
+    });
+}
+
+int huff_dev_alloc(huff_ctx* ctx, size_t bytes, void** d_ptr) {
+    if (!ctx || !d_ptr) return fail(HUFF_E_INVALID_ARG, "null argument");
+    hipSetDevice(ctx->device);
+    hipError_t e = hipMalloc(d_ptr, bytes ? bytes : 1);
+    return e == hipSuccess ? HUFF_OK : fail(HUFF_E_HIP, hipGetErrorString(e));
+}
+
+int huff_dev_free(huff_ctx* ctx, void* d_ptr) {
+    if (!ctx) return fail(HUFF_E_INVALID_ARG, "null argument");
+    hipSetDevice(ctx->device);
+    hipError_t e = hipFree(d_ptr);
+    return e == hipSuccess ? HUFF_OK : fail(HUFF_E_HIP, hipGetErrorString(e));
+}
+
+int huff_memcpy_htod(huff_ctx* ctx, void* d_dst, const void* src, size_t bytes) {
+    if (!ctx) return fail(HUFF_E_INVALID_ARG, "null argument");
+    hipSetDevice(ctx->device);
+    hipError_t e = hipMemcpy(d_dst, src, bytes, hipMemcpyHostToDevice);
+    return e == hipSuccess ? HUFF_OK : fail(HUFF_E_HIP, hipGetErrorString(e));
+}
+
+int huff_memcpy_dtoh(huff_ctx* ctx, void* dst, const void* d_src, size_t bytes) {
+    if (!ctx) return fail(HUFF_E_INVALID_ARG, "null argument");
+    hipSetDevice(ctx->device);
+    hipStreamSynchronize(ctx->stream);
+    hipError_t e = hipMemcpy(dst, d_src, bytes, hipMemcpyDeviceToHost);
+    return e == hipSuccess ? HUFF_OK : fail(HUFF_E_HIP, hipGetErrorString(e));
+}
+
+// --------------------------------------------------------------------------
+int huff_file_compress(huff_ctx* ctx, const char* src_path, const char* dst_path, size_t block_size) {
+    if (!ctx || !src_path || !dst_path) return fail(HUFF_E_INVALID_ARG, "null argument");
+    return guarded([&] { return huff::file_compress(ctx, src_path, dst_path, block_size); });
+}
+
+int huff_file_decompress(huff_ctx* ctx, const char* src_path, const char* dst_path, size_t block_size) {
+    if (!ctx || !src_path || !dst_path) return fail(HUFF_E_INVALID_ARG, "null argument");
+    return guarded([&] { return huff::file_decompress(ctx, src_path, dst_path, block_size); });
+}
+
+int huff_parse_block_size(const char* s, size_t* out) {
+    if (!out) return fail(HUFF_E_INVALID_ARG, "null argument");
+    return report(huff::parse_block_size(s, out));
+}
+
+}  // extern "C"

@@ -1,0 +1,93 @@
+// bitreader.hpp — MSB-first bit reader + table lookup shared by the decoders.
+//
+// The stream is the reference's byte layout (bit i -> byte i/8, mask
+// 0x80 >> (i%8)); it is read as big-endian 32-bit words into a 64-bit
+// left-aligned window. A code is looked up with the top K bits in the
+// primary table (LDS); longer codes follow 8-bit secondary tables in global
+// memory on a freshly loaded window. Table entries: leaf = (len << 8) | letter,
+// pointer = kLutPtr | index of the secondary table.
+#pragma once
+
+#include "kernels.hpp"
+
+namespace huff::dev {
+
+struct BitSrc {
+    const uint32_t* w;
+    const uint8_t* b;
+    uint64_t nbytes;
+
+    __device__ __forceinline__ uint32_t word(uint64_t i) const {
+        const uint64_t byte = i * 4;
+        if (byte + 4 <= nbytes) return __builtin_bswap32(w[i]);
+        uint32_t v = 0;
+        for (int k = 0; k < 4; ++k) {
+            v <<= 8;
+            if (byte + k < nbytes) v |= b[byte + k];
+        }
+        return v;
+    }
+    // 64 bits starting at bit pos, left-aligned
+    __device__ __forceinline__ uint64_t window(uint64_t pos) const {
+        const uint64_t wi = pos >> 5;
+        const uint32_t sh = static_cast<uint32_t>(pos & 31);
+        const uint64_t hi = (static_cast<uint64_t>(word(wi)) << 32) | word(wi + 1);
+        if (sh == 0) return hi;
+        return (hi << sh) | (word(wi + 2) >> (32 - sh));
+    }
+};
+
+struct Lut {
+    const uint32_t* prim;  // LDS copy of the primary table
+    const uint32_t* glob;  // full table in global memory (secondaries)
+    uint32_t K;
+};
+
+// slow path: the code at an arbitrary bit position
+__device__ __forceinline__ uint32_t lut_lookup_at(const BitSrc& src, const Lut& t, uint64_t pos) {
+    const uint64_t win = src.window(pos);
+    uint32_t e = t.prim[win >> (64 - t.K)];
+    uint32_t d = t.K;
+    while (e & kLutPtr) {
+        const uint32_t idx = static_cast<uint32_t>((win >> (56 - d)) & 0xFFu);
+        e = t.glob[(e & ~kLutPtr) + idx];
+        d += 8;
+    }
+    return e;
+}
+
+struct BitReader {
+    uint64_t pos, buf, wi;
+    uint32_t nb;
+
+    __device__ __forceinline__ void seek(const BitSrc& src, uint64_t p) {
+        pos = p;
+        wi = p >> 5;
+        const uint32_t sh = static_cast<uint32_t>(p & 31);
+        buf = ((static_cast<uint64_t>(src.word(wi)) << 32) | src.word(wi + 1)) << sh;
+        nb = 64 - sh;
+        wi += 2;
+    }
+    // entry of the code at pos (does not advance)
+    __device__ __forceinline__ uint32_t peek(const BitSrc& src, const Lut& t) {
+        if (nb < 32) {
+            buf |= static_cast<uint64_t>(src.word(wi)) << (32 - nb);
+            ++wi;
+            nb += 32;
+        }
+        const uint32_t e = t.prim[buf >> (64 - t.K)];
+        if ((e & kLutPtr) || ((e >> 8) & 0xFFu) > nb) return lut_lookup_at(src, t, pos);
+        return e;
+    }
+    __device__ __forceinline__ void advance(const BitSrc& src, uint32_t len) {
+        if (len <= nb) {
+            buf <<= len;
+            nb -= len;
+            pos += len;
+        } else {
+            seek(src, pos + len);
+        }
+    }
+};
+
+}  // namespace huff::dev

@@ -1,0 +1,204 @@
+// hist.hip — hist256: ByteWeights::from_bytes on the GPU
+// (huff_coding/src/weights.rs:265-279: one increment per byte).
+//
+// Roofline: HBM-bound, 1 byte read per input byte. Each workgroup owns whole
+// 64 KiB chunks (grid-stride), reads them with 16-B coalesced loads and counts
+// into an LDS histogram replicated 32x as [bin][copy]: lane l increments copy
+// l % 32, so the ds_add_u32 address of every lane of a 32-lane LDS group sits
+// in its own bank whatever the data (no bank conflicts on skewed inputs, the
+// two 32-lane halves of a wave are serviced in separate LDS cycles). After a
+// chunk the 32 copies are summed (rotated reads, conflict-free) into the
+// per-chunk histogram row; the workgroup's totals go to one of 8 XCD-group
+// copies of the global weights with one atomic per bin.
+#include "kernels.hpp"
+
+namespace huff::dev {
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kCopies = 32;
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint4 ld_nt(const uint4* p) {
+    u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+__device__ __forceinline__ void count_word(uint32_t* h, uint32_t w, uint32_t lane32) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        uint32_t b = (w >> (8 * k)) & 0xFFu;
+        __hip_atomic_fetch_add(&h[(b << 5) | lane32], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+}
+
+__device__ __forceinline__ void count_masked(uint32_t* h, uint4 v, uint64_t off, uint64_t lo, uint64_t hi,
+                                             uint32_t lane32) {
+    uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        uint64_t g = off + k;
+        if (g >= lo && g < hi) {
+            uint32_t b = (w[k >> 2] >> (8 * (k & 3))) & 0xFFu;
+            __hip_atomic_fetch_add(&h[(b << 5) | lane32], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+    }
+}
+
+// bytes [lo, hi) of `base` (base 16-B aligned); chunk c = base bytes
+// [c*kChunk, (c+1)*kChunk).
+__global__ __launch_bounds__(kThreads) void k_hist(const uint8_t* __restrict__ base, uint64_t lo, uint64_t hi,
+                                                   uint32_t nchunks, uint32_t* __restrict__ chunk_hist,
+                                                   unsigned long long* __restrict__ gw) {
+    __shared__ __attribute__((aligned(16))) uint32_t h[256 * kCopies];
+    const uint32_t t = threadIdx.x;
+    const uint32_t lane32 = t & 31;
+    for (uint32_t i = t; i < 256 * kCopies; i += kThreads) h[i] = 0;
+    uint64_t total = 0;
+    __syncthreads();
+
+    for (uint32_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
+        const uint64_t cbeg = static_cast<uint64_t>(c) * kChunk;
+        const bool full = cbeg >= lo && cbeg + kChunk <= hi;
+        if (full) {
+            const uint4* p = reinterpret_cast<const uint4*>(base + cbeg) + t;
+            // 16 rounds of 4 KiB; 4 loads in flight per lane
+#pragma unroll 1
+            for (int r = 0; r < 16; r += 4) {
+                uint4 v0 = ld_nt(p + (r + 0) * kThreads);
+                uint4 v1 = ld_nt(p + (r + 1) * kThreads);
+                uint4 v2 = ld_nt(p + (r + 2) * kThreads);
+                uint4 v3 = ld_nt(p + (r + 3) * kThreads);
+                count_word(h, v0.x, lane32); count_word(h, v0.y, lane32);
+                count_word(h, v0.z, lane32); count_word(h, v0.w, lane32);
+                count_word(h, v1.x, lane32); count_word(h, v1.y, lane32);
+                count_word(h, v1.z, lane32); count_word(h, v1.w, lane32);
+                count_word(h, v2.x, lane32); count_word(h, v2.y, lane32);
+                count_word(h, v2.z, lane32); count_word(h, v2.w, lane32);
+                count_word(h, v3.x, lane32); count_word(h, v3.y, lane32);
+                count_word(h, v3.z, lane32); count_word(h, v3.w, lane32);
+            }
+        } else {
+            for (int r = 0; r < 16; ++r) {
+                const uint64_t off = cbeg + static_cast<uint64_t>(r) * kRound + t * 16;
+                if (off + 16 <= lo || off >= hi) continue;
+                uint4 v;
+                if (off + 16 <= hi) {
+                    v = *reinterpret_cast<const uint4*>(base + off);
+                } else {  // never read past hi
+                    uint32_t w[4] = {0, 0, 0, 0};
+                    for (int k = 0; off + k < hi; ++k) w[k >> 2] |= static_cast<uint32_t>(base[off + k]) << (8 * (k & 3));
+                    v = make_uint4(w[0], w[1], w[2], w[3]);
+                }
+                count_masked(h, v, off, lo, hi, lane32);
+            }
+        }
+        __syncthreads();
+        // thread t owns bin t: sum its 32 copies (rotated: conflict-free) and clear
+        uint32_t s = 0;
+#pragma unroll 8
+        for (int j = 0; j < kCopies; ++j) {
+            uint32_t k = (j + t) & 31;
+            s += h[(t << 5) | k];
+            h[(t << 5) | k] = 0;
+        }
+        if (chunk_hist) chunk_hist[static_cast<uint64_t>(c) * 256 + t] = s;
+        total += s;
+        __syncthreads();
+    }
+    if (total) atomicAdd(&gw[(blockIdx.x % kHistCopies) * 256 + t], static_cast<unsigned long long>(total));
+}
+
+// bits[c] = sum_b chunk_hist[c][b] * len[b]; one wave per chunk.
+__global__ __launch_bounds__(256) void k_chunk_bits(const uint32_t* __restrict__ chunk_hist, uint32_t nchunks,
+                                                    const uint8_t* __restrict__ len, uint64_t* __restrict__ bits) {
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint32_t c = blockIdx.x * 4 + wave;
+    if (c >= nchunks) return;
+    uint4 hv = reinterpret_cast<const uint4*>(chunk_hist + static_cast<uint64_t>(c) * 256)[lane];
+    uint32_t lv = reinterpret_cast<const uint32_t*>(len)[lane];
+    uint64_t s = static_cast<uint64_t>(hv.x) * (lv & 0xFF) + static_cast<uint64_t>(hv.y) * ((lv >> 8) & 0xFF) +
+                 static_cast<uint64_t>(hv.z) * ((lv >> 16) & 0xFF) + static_cast<uint64_t>(hv.w) * (lv >> 24);
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) s += __shfl_down(s, d, 64);
+    if (lane == 0) bits[c] = s;
+}
+
+// start[c] = base + sum_{c' < c} bits[c'], start[nchunks] = total end.
+__global__ __launch_bounds__(1024) void k_scan(const uint64_t* __restrict__ bits, uint32_t nchunks, uint64_t base,
+                                               uint64_t* __restrict__ start) {
+    __shared__ uint64_t wsum[16];
+    const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const uint32_t per = (nchunks + 1023) / 1024;
+    const uint32_t b = t * per, e = min(nchunks, b + per);
+    uint64_t local = 0;
+    for (uint32_t i = b; i < e; ++i) local += bits[i];
+    uint64_t incl = local;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        uint64_t y = __shfl_up(incl, d, 64);
+        if (lane >= static_cast<uint32_t>(d)) incl += y;
+    }
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    uint64_t pre = base;
+    for (uint32_t w = 0; w < wave; ++w) pre += wsum[w];
+    uint64_t run = pre + incl - local;
+    for (uint32_t i = b; i < e; ++i) {
+        start[i] = run;
+        run += bits[i];
+    }
+    if (t == 1023) start[nchunks] = run;
+    // (when nchunks < 1024, the last thread has an empty range and run is the total)
+}
+
+// lowest index i with missing_mask[in[i]] != 0 (error path of compress_with_tree)
+__global__ __launch_bounds__(256) void k_find_first(const uint8_t* __restrict__ in, uint64_t n,
+                                                    const uint8_t* __restrict__ mask,
+                                                    unsigned long long* __restrict__ pos) {
+    __shared__ uint8_t m[256];
+    m[threadIdx.x] = mask[threadIdx.x];
+    __syncthreads();
+    for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
+         i += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
+        if (m[in[i]]) {
+            atomicMin(pos, static_cast<unsigned long long>(i));
+            return;
+        }
+    }
+}
+
+}  // namespace
+
+hipError_t launch_hist(const uint8_t* base, uint64_t lo, uint64_t hi, uint32_t nchunks, uint32_t* chunk_hist,
+                       unsigned long long* gw, hipStream_t s) {
+    if (nchunks == 0) return hipSuccess;
+    uint32_t grid = nchunks < 1024 ? nchunks : 1024;
+    hipLaunchKernelGGL(k_hist, dim3(grid), dim3(kThreads), 0, s, base, lo, hi, nchunks, chunk_hist, gw);
+    return hipGetLastError();
+}
+
+hipError_t launch_chunk_bits(const uint32_t* chunk_hist, uint32_t nchunks, const uint8_t* len, uint64_t* bits,
+                             hipStream_t s) {
+    if (nchunks == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_chunk_bits, dim3((nchunks + 3) / 4), dim3(256), 0, s, chunk_hist, nchunks, len, bits);
+    return hipGetLastError();
+}
+
+hipError_t launch_scan(const uint64_t* bits, uint32_t nchunks, uint64_t base, uint64_t* start, hipStream_t s) {
+    hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, s, bits, nchunks, base, start);
+    return hipGetLastError();
+}
+
+hipError_t launch_find_first(const uint8_t* in, uint64_t n, const uint8_t* missing_mask, unsigned long long* pos,
+                             hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    uint64_t blocks = (n + 255) / 256;
+    uint32_t grid = blocks < 4096 ? static_cast<uint32_t>(blocks) : 4096;
+    hipLaunchKernelGGL(k_find_first, dim3(grid), dim3(256), 0, s, in, n, missing_mask, pos);
+    return hipGetLastError();
+}
+
+}  // namespace huff::dev

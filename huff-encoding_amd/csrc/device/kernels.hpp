@@ -1,0 +1,88 @@
+// kernels.hpp — launch interface of the gfx950 kernels.
+//
+// Data layout in HBM for one encode job of n input bytes:
+//   in            u8[n]                 16-B aligned, read twice (hist, pack)
+//   chunk_hist    u32[nchunks][256]     per 64 KiB chunk, written by hist
+//   gw            u64[8][256]           global weights, one copy per XCD group
+//   chunk_bits    u64[nchunks]          bits per chunk (after the tree is known)
+//   chunk_start   u64[nchunks + 1]      exclusive scan of chunk_bits (+ bit base)
+//   sub_bit       u32[ceil(n/256)]      restart index: bit offset of every
+//                                       256th symbol, relative to its chunk
+//   out           u8[ceil(bits/8)]      the compress_with_tree byte stream
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace huff::dev {
+
+constexpr uint32_t kChunk = 65536;      // input bytes (= symbols) per chunk / workgroup
+constexpr uint32_t kRound = 4096;       // bytes per workgroup round (256 lanes x 16 B)
+constexpr uint32_t kSub = 256;          // symbols per decode lane (restart index stride)
+constexpr uint32_t kShortMaxLen = 27;   // u32 table entries: code << 5 | len
+constexpr uint32_t kLongMaxLen = 57;    // u64 table entries: code << 6 | len
+constexpr uint32_t kHistCopies = 8;     // XCD-group copies of the global weights
+constexpr uint32_t kLutMaxBits = 12;    // primary decode table index bits
+constexpr uint32_t kLutPtr = 0x80000000u;
+
+struct PackArgs {
+    const uint8_t* in;
+    uint64_t n;
+    const void* table;            // [256] u32 or u64 entries
+    const uint64_t* chunk_start;  // [nchunks + 1], bits relative to out bit 0
+    uint32_t nchunks;
+    uint8_t* out;
+    uint32_t* sub_bit;            // may be null
+    const uint8_t* prev_tail;     // 8 bytes, right-aligned (prev_tail[7] precedes in[0])
+    uint32_t prev_tail_len;
+    uint32_t stage_words;
+};
+
+struct DecodeArgs {
+    const uint8_t* comp;          // stream, 4-B aligned; bit 0 = MSB of comp[0]
+    uint64_t comp_bytes;          // readable bytes of comp
+    const uint32_t* lut;          // primary [1 << K] then secondary tables
+    uint32_t lut_bits;            // K
+    uint32_t lut_words;           // total words (primary + secondary)
+    const uint64_t* chunk_start;  // [nchunks + 1]
+    const uint32_t* sub_bit;      // [ceil(n / kSub)]
+    uint32_t nchunks;
+    uint64_t n;
+    uint8_t* out;
+};
+
+struct IndexlessArgs {
+    const uint8_t* comp;
+    uint64_t comp_bytes;
+    uint64_t valid_bits;          // B
+    uint64_t seg_bits;            // S (multiple of the gcd of code lengths)
+    uint64_t nseg;
+    const uint32_t* lut;
+    uint32_t lut_bits;
+    uint64_t* s;                  // [nseg] settled segment starts
+    uint64_t* x;                  // [nseg] exits
+    uint64_t* c;                  // [nseg] symbol counts
+};
+
+size_t pack_lds_bytes(bool long_codes, uint32_t stage_words);
+size_t decode_lds_bytes(uint32_t lut_bits);
+
+hipError_t launch_hist(const uint8_t* base, uint64_t lo, uint64_t hi, uint32_t nchunks, uint32_t* chunk_hist,
+                       unsigned long long* gw, hipStream_t s);
+hipError_t launch_chunk_bits(const uint32_t* chunk_hist, uint32_t nchunks, const uint8_t* len, uint64_t* bits,
+                             hipStream_t s);
+hipError_t launch_scan(const uint64_t* bits, uint32_t nchunks, uint64_t base, uint64_t* start, hipStream_t s);
+hipError_t launch_pack(bool long_codes, const PackArgs& a, hipStream_t s);
+hipError_t launch_decode(const DecodeArgs& a, hipStream_t s);
+hipError_t launch_indexless_spec(const IndexlessArgs& a, hipStream_t s);
+hipError_t launch_indexless_fix(const IndexlessArgs& a, const uint64_t* xin, uint64_t* xout, unsigned int* changed,
+                                hipStream_t s);
+hipError_t launch_indexless_settle(const IndexlessArgs& a, uint64_t* x, hipStream_t s);
+hipError_t launch_indexless_emit(const IndexlessArgs& a, const uint64_t* off, uint8_t* out, hipStream_t s);
+hipError_t launch_find_first(const uint8_t* in, uint64_t n, const uint8_t* missing_mask, unsigned long long* pos,
+                             hipStream_t s);
+hipError_t launch_generate(int kind, uint64_t seed, uint64_t offset, const uint64_t* cdf, uint8_t* out, uint64_t n,
+                           hipStream_t s);
+
+}  // namespace huff::dev

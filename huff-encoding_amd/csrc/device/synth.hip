@@ -1,0 +1,107 @@
+// synth.hip — synthetic benchmark inputs generated in HBM (not reference
+// code). Counter-based, so byte i of a stream depends only on (kind, seed,
+// offset + i) and the CPU checker regenerates the same bytes
+// (oracle/huff_oracle.c orc_gen_*). Never timed.
+#include "kernels.hpp"
+
+namespace huff::dev {
+
+namespace {
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t k, uint64_t seed) {
+    uint64_t z = seed + (k + 1) * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+// kind 0: byte g = LE byte (g % 8) of splitmix64(g / 8)
+__global__ void k_gen_uniform(uint64_t seed, uint64_t offset, uint8_t* out, uint64_t n) {
+    const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+    if ((offset & 7) == 0) {
+        uint64_t words = n / 8;
+        for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < words; i += stride)
+            reinterpret_cast<uint64_t*>(out)[i] = splitmix64(offset / 8 + i, seed);
+        for (uint64_t i = words * 8 + static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride)
+            out[i] = static_cast<uint8_t>(splitmix64((offset + i) / 8, seed) >> (8 * ((offset + i) % 8)));
+        return;
+    }
+    for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride)
+        out[i] = static_cast<uint8_t>(splitmix64((offset + i) / 8, seed) >> (8 * ((offset + i) % 8)));
+}
+
+// kind 1: byte g = first k with splitmix64(g) < cdf[k]
+__global__ void k_gen_zipf(uint64_t seed, uint64_t offset, const uint64_t* __restrict__ cdf_g, uint8_t* out,
+                           uint64_t n) {
+    __shared__ uint64_t cdf[256];
+    cdf[threadIdx.x] = cdf_g[threadIdx.x];
+    __syncthreads();
+    const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+    for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint64_t r = splitmix64(offset + i, seed);
+        int lo = 0, hi = 255;
+        while (lo < hi) {
+            int mid = (lo + hi) >> 1;
+            if (r < cdf[mid]) hi = mid; else lo = mid + 1;
+        }
+        out[i] = static_cast<uint8_t>(lo);
+    }
+}
+
+// kind 2: 64-byte text lines (orc_gen_text)
+__device__ void gen_word(uint32_t k, uint8_t* w, int* len) {
+    const char letters[] = "etaoinshrdlucmfwypvbgkjqxz";
+    uint64_t h = splitmix64(k, 0x7E47ull);
+    int l = 1 + static_cast<int>(h % 9);
+    for (int i = 0; i < l; ++i) {
+        uint64_t r = (h >> (6 + 5 * (i % 10))) ^ static_cast<uint64_t>(i) * 0x9E37ull;
+        int x = static_cast<int>(r % 26), y = static_cast<int>((r >> 7) % 26);
+        w[i] = static_cast<uint8_t>(letters[x < y ? x : y]);
+    }
+    *len = l;
+}
+
+__global__ void k_gen_text(uint64_t seed, uint64_t offset, uint8_t* out, uint64_t n) {
+    const uint64_t first_line = offset / 64;
+    const uint64_t last_line = (offset + n + 63) / 64;
+    const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+    for (uint64_t l = first_line + static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; l < last_line;
+         l += stride) {
+        uint8_t line[64];
+        int p = 0;
+        uint64_t st = 0;
+        while (p < 63) {
+            uint64_t r = splitmix64(l * 16 + st++, seed);
+            uint32_t span = static_cast<uint32_t>(r & 511) + 1;
+            uint32_t k = static_cast<uint32_t>((r >> 9) % span);
+            uint8_t w[10];
+            int wl;
+            gen_word(k, w, &wl);
+            for (int q = 0; q < wl && p < 63; ++q) line[p++] = w[q];
+            if (p < 63) line[p++] = (r >> 40) % 11 == 0 ? ',' : ' ';
+            if (st >= 16) {
+                while (p < 63) line[p++] = ' ';
+            }
+        }
+        line[63] = '\n';
+        for (int i = 0; i < 64; ++i) {
+            uint64_t g = l * 64 + i;
+            if (g >= offset && g < offset + n) out[g - offset] = line[i];
+        }
+    }
+}
+
+}  // namespace
+
+hipError_t launch_generate(int kind, uint64_t seed, uint64_t offset, const uint64_t* cdf, uint8_t* out, uint64_t n,
+                           hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const uint32_t grid = 4096;
+    if (kind == 0) hipLaunchKernelGGL(k_gen_uniform, dim3(grid), dim3(256), 0, s, seed, offset, out, n);
+    else if (kind == 1) hipLaunchKernelGGL(k_gen_zipf, dim3(grid), dim3(256), 0, s, seed, offset, cdf, out, n);
+    else if (kind == 2) hipLaunchKernelGGL(k_gen_text, dim3(grid), dim3(256), 0, s, seed, offset, out, n);
+    else return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+
+}  // namespace huff::dev

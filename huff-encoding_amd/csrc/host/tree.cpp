@@ -1,0 +1,275 @@
+// tree.cpp — HuffTree on the host (huff_coding/src/tree/).
+//
+// The tree decides every output bit, so it is built with the reference's
+// exact tie order: the reference pushes leaves into a Rust std BinaryHeap whose
+// Ord is reversed on weight only (branch_heap.rs:67-71, leaf.rs:31-35) and
+// repeatedly pops the two minima (tree_inner.rs:289-303). RustMaxHeap below is
+// that std heap's algorithm (sift_up on push; on pop the last element is
+// swapped into the root, sifted down to the bottom always taking the right
+// child on ties, then sifted up), keyed so that "a <= b" means a.w >= b.w.
+#include <algorithm>
+#include <utility>
+
+#include "huff_coding.hpp"
+
+namespace huff {
+
+namespace {
+
+struct HeapEntry {
+    uint64_t w;
+    int32_t node;
+};
+
+class RustMaxHeap {
+public:
+    explicit RustMaxHeap(size_t reserve) { v_.reserve(reserve); }
+    size_t size() const { return v_.size(); }
+
+    void push(HeapEntry e) {
+        v_.push_back(e);
+        sift_up(0, v_.size() - 1);
+    }
+
+    HeapEntry pop() {
+        HeapEntry top = v_.back();
+        v_.pop_back();
+        if (!v_.empty()) {
+            std::swap(top, v_[0]);
+            sift_down_to_bottom(0);
+        }
+        return top;
+    }
+
+private:
+    // "a <= b" under the reversed Ord of HuffBranchHeapItem
+    static bool le(const HeapEntry& a, const HeapEntry& b) { return a.w >= b.w; }
+
+    size_t sift_up(size_t start, size_t pos) {
+        HeapEntry hole = v_[pos];
+        while (pos > start) {
+            size_t parent = (pos - 1) >> 1;
+            if (le(hole, v_[parent])) break;
+            v_[pos] = v_[parent];
+            pos = parent;
+        }
+        v_[pos] = hole;
+        return pos;
+    }
+
+    void sift_down_to_bottom(size_t pos) {
+        const size_t end = v_.size();
+        const size_t start = pos;
+        HeapEntry hole = v_[pos];
+        size_t child = 2 * pos + 1;
+        while (end >= 2 && child <= end - 2) {
+            child += le(v_[child], v_[child + 1]) ? 1 : 0;
+            v_[pos] = v_[child];
+            pos = child;
+            child = 2 * pos + 1;
+        }
+        if (child == end - 1) {
+            v_[pos] = v_[child];
+            pos = child;
+        }
+        v_[pos] = hole;
+        sift_up(start, pos);
+    }
+
+    std::vector<HeapEntry> v_;
+};
+
+}  // namespace
+
+Status HuffTree::from_leaves(const uint8_t* letters, const uint64_t* weights, size_t n, HuffTree& out) {
+    if (n == 0) return Status::err(HUFF_E_EMPTY_WEIGHTS, "provided empty weights");
+    out.nodes_.clear();
+    out.nodes_.reserve(2 * n);
+    RustMaxHeap heap(n + 1);
+    for (size_t i = 0; i < n; ++i) {  // branch_heap.rs:52-58
+        HuffNode leaf;
+        leaf.is_leaf = true;
+        leaf.letter = letters[i];
+        leaf.weight = weights[i];
+        out.nodes_.push_back(leaf);
+        heap.push({weights[i], static_cast<int32_t>(out.nodes_.size() - 1)});
+    }
+    while (heap.size() > 1) {  // tree_inner.rs:289-303
+        HeapEntry a = heap.pop();  // min       -> left  (code bit 0)
+        HeapEntry b = heap.pop();  // next_min  -> right (code bit 1)
+        HuffNode joint;
+        joint.weight = a.w + b.w;
+        joint.left = a.node;
+        joint.right = b.node;
+        out.nodes_.push_back(joint);
+        heap.push({joint.weight, static_cast<int32_t>(out.nodes_.size() - 1)});
+    }
+    out.root_ = heap.pop().node;  // tree_inner.rs:306
+    return Status::ok();
+}
+
+Status HuffTree::from_weights(const ByteWeights& w, HuffTree& out) {
+    if (w.is_empty()) return Status::err(HUFF_E_EMPTY_WEIGHTS, "provided empty weights");
+    uint8_t l[257];
+    uint64_t f[257];
+    size_t cnt = w.iter(l, f);  // IntoIter order, §C.1 duplicate included
+    return from_leaves(l, f, cnt, out);
+}
+
+std::vector<LeafCode> HuffTree::leaves() const {
+    std::vector<LeafCode> out;
+    if (nodes_[root_].is_leaf) {  // tree_inner.rs:313-315: a root leaf's code is "0"
+        out.push_back({nodes_[root_].letter, 1, {0}});
+        return out;
+    }
+    struct Frame {
+        int32_t node;
+        uint32_t depth;
+        uint8_t bit;  // bit on the edge into this node
+    };
+    std::vector<Frame> st;
+    std::vector<uint8_t> path;
+    st.push_back({nodes_[root_].right, 1, 1});
+    st.push_back({nodes_[root_].left, 1, 0});
+    while (!st.empty()) {
+        Frame fr = st.back();
+        st.pop_back();
+        path.resize(fr.depth - 1);
+        path.push_back(fr.bit);
+        const HuffNode& nd = nodes_[fr.node];
+        if (nd.is_leaf) {
+            out.push_back({nd.letter, fr.depth, path});
+            continue;
+        }
+        st.push_back({nd.right, fr.depth + 1, 1});
+        st.push_back({nd.left, fr.depth + 1, 0});
+    }
+    return out;
+}
+
+void HuffTree::read_codes(std::array<std::vector<uint8_t>, 256>& codes) const {
+    for (auto& c : codes) c.clear();
+    // leaves() is in left-to-right order = the reference's insert order, so a
+    // later duplicate overwrites an earlier one (HashMap::insert).
+    for (const LeafCode& lc : leaves()) codes[lc.letter] = lc.bits;
+}
+
+bool HuffTree::read_codes_u64(uint64_t code[256], uint8_t len[256], uint32_t* maxlen) const {
+    std::array<std::vector<uint8_t>, 256> codes;
+    read_codes(codes);
+    uint32_t ml = 0;
+    bool ok = true;
+    for (int b = 0; b < 256; ++b) {
+        const auto& c = codes[b];
+        ml = std::max<uint32_t>(ml, static_cast<uint32_t>(c.size()));
+        if (c.size() > 64) {
+            ok = false;
+            code[b] = 0;
+            len[b] = 0;
+            continue;
+        }
+        uint64_t v = 0;
+        for (uint8_t bit : c) v = (v << 1) | bit;
+        code[b] = v;
+        len[b] = static_cast<uint8_t>(c.size());
+    }
+    if (maxlen) *maxlen = ml;
+    return ok;
+}
+
+size_t HuffTree::num_leaves() const {
+    size_t c = 0;
+    std::vector<int32_t> st{root_};
+    while (!st.empty()) {
+        int32_t n = st.back();
+        st.pop_back();
+        if (nodes_[n].is_leaf) {
+            ++c;
+        } else {
+            st.push_back(nodes_[n].left);
+            st.push_back(nodes_[n].right);
+        }
+    }
+    return c;
+}
+
+uint32_t HuffTree::max_depth() const {
+    uint32_t m = 0;
+    for (const LeafCode& lc : leaves()) m = std::max(m, lc.len);
+    return m;
+}
+
+std::vector<uint8_t> HuffTree::as_bin() const {
+    // tree_inner.rs:637-663: preorder; joint -> 1, leaf -> 0 then the letter's
+    // big-endian bits (8 for u8).
+    std::vector<uint8_t> bits;
+    std::vector<int32_t> st{root_};
+    while (!st.empty()) {
+        int32_t n = st.back();
+        st.pop_back();
+        const HuffNode& nd = nodes_[n];
+        if (nd.is_leaf) {
+            bits.push_back(0);
+            for (int k = 7; k >= 0; --k) bits.push_back((nd.letter >> k) & 1);
+        } else {
+            bits.push_back(1);
+            st.push_back(nd.right);
+            st.push_back(nd.left);
+        }
+    }
+    return bits;
+}
+
+Status HuffTree::try_from_bin(const std::vector<uint8_t>& bits, HuffTree& out) {
+    // tree_inner.rs:526-590, iteratively: a 1 opens a joint branch whose two
+    // children follow in preorder; a 0 is a letter branch + 8 letter bits.
+    static const char* kSmall = "Provided BitVec is too small for an encoded HuffTree";
+    static const char* kBig = "Provided BitVec is too big for an encoded HuffTree";
+    out.nodes_.clear();
+    struct Open {
+        int32_t node;
+        int filled;  // children attached so far
+    };
+    std::vector<Open> open;
+    size_t pos = 0;
+    int32_t root = -1;
+    const size_t n = bits.size();
+    for (;;) {
+        if (pos >= n) return Status::err(HUFF_E_FROM_BIN, kSmall);
+        int32_t idx;
+        if (bits[pos++]) {
+            out.nodes_.push_back(HuffNode{});
+            idx = static_cast<int32_t>(out.nodes_.size() - 1);
+        } else {
+            if (n - pos < 8) return Status::err(HUFF_E_FROM_BIN, kSmall);
+            uint8_t letter = 0;
+            for (int k = 0; k < 8; ++k) letter = static_cast<uint8_t>((letter << 1) | bits[pos + k]);
+            pos += 8;
+            HuffNode leaf;
+            leaf.is_leaf = true;
+            leaf.letter = letter;
+            out.nodes_.push_back(leaf);
+            idx = static_cast<int32_t>(out.nodes_.size() - 1);
+        }
+        // attach to the innermost open joint
+        if (open.empty()) {
+            root = idx;
+        } else {
+            Open& o = open.back();
+            if (o.filled == 0) out.nodes_[o.node].left = idx;
+            else out.nodes_[o.node].right = idx;
+            o.filled++;
+        }
+        if (!out.nodes_[idx].is_leaf) {
+            open.push_back({idx, 0});
+        } else {
+            while (!open.empty() && open.back().filled == 2) open.pop_back();
+            if (open.empty()) break;  // root complete
+        }
+    }
+    if (pos != n) return Status::err(HUFF_E_FROM_BIN, kBig);  // tree_inner.rs:586-590
+    out.root_ = root;
+    return Status::ok();
+}
+
+}  // namespace huff

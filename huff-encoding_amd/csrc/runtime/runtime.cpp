@@ -1,0 +1,637 @@
+// runtime.cpp — context, encode job and host-pointer pipelines.
+#include "runtime.hpp"
+
+#include <algorithm>
+#include <cctype>
+#include <numeric>
+#include <cstring>
+#include <string>
+
+namespace {
+
+std::atomic<uint64_t> g_tree_ids{1};
+
+}  // namespace
+
+#define HIP_TRY(expr) HIP_TRY_RT(expr)
+
+// ---------------------------------------------------------------------------
+// trees and their tables
+// ---------------------------------------------------------------------------
+huff_tree::huff_tree() : id(g_tree_ids.fetch_add(1)) {}
+
+const huff::EncTables& huff_tree::enc_tables() const {
+    std::lock_guard<std::mutex> g(m);
+    if (!enc) {
+        auto e = std::make_unique<huff::EncTables>();
+        e->fits64 = t.read_codes_u64(e->code, e->len, &e->maxlen);
+        enc = std::move(e);
+    }
+    return *enc;
+}
+
+huff::Status huff_tree::dec_tables(const huff::DecTables** out) const {
+    std::lock_guard<std::mutex> g(m);
+    if (!dec) {
+        auto d = std::make_unique<huff::DecTables>();
+        HUFF_TRY(huff::build_dec_tables(t, *d));
+        dec = std::move(d);
+    }
+    *out = dec.get();
+    return huff::Status::ok();
+}
+
+huff_compress_data::~huff_compress_data() { delete tree; }
+
+namespace huff {
+
+Status build_dec_tables(const HuffTree& t, DecTables& out) {
+    const auto& nodes = t.nodes();
+    out.lut.clear();
+    if (t.root_is_leaf()) {  // every bit decodes the root letter (comp.rs:506-509)
+        out.bits = 1;
+        out.maxdepth = 1;
+        const uint32_t e = (1u << 8) | nodes[t.root()].letter;
+        out.lut = {e, e};
+        return Status::ok();
+    }
+    const uint32_t maxd = t.max_depth();
+    if (maxd > dev::kLongMaxLen)
+        return Status::err(HUFF_E_CODE_TOO_LONG, "code longer than 57 bits: outside the GPU decoder's range");
+    out.maxdepth = maxd;
+    out.bits = std::min<uint32_t>(maxd, dev::kLutMaxBits - 1);  // 11 bits: 8 KiB of LDS
+    if (out.bits < 1) out.bits = 1;
+    out.lut.assign(1u << out.bits, 0);
+
+    // fill the table rooted at internal node `x` (depth d0, tb index bits)
+    struct Job {
+        int32_t x;
+        uint32_t d0, tb, base;
+    };
+    std::vector<Job> jobs{{t.root(), 0, out.bits, 0}};
+    while (!jobs.empty()) {
+        Job j = jobs.back();
+        jobs.pop_back();
+        struct F {
+            int32_t node;
+            uint32_t r;
+            uint32_t path;
+        };
+        std::vector<F> st{{nodes[j.x].right, 1, 1}, {nodes[j.x].left, 1, 0}};
+        while (!st.empty()) {
+            F f = st.back();
+            st.pop_back();
+            const HuffNode& nd = nodes[f.node];
+            if (nd.is_leaf) {
+                const uint32_t e = ((j.d0 + f.r) << 8) | nd.letter;
+                const uint32_t lo = f.path << (j.tb - f.r), hi = (f.path + 1) << (j.tb - f.r);
+                for (uint32_t i = lo; i < hi; ++i) out.lut[j.base + i] = e;
+            } else if (f.r == j.tb) {
+                const uint32_t sub = static_cast<uint32_t>(out.lut.size());
+                out.lut.resize(out.lut.size() + 256, 0);
+                out.lut[j.base + f.path] = dev::kLutPtr | sub;
+                jobs.push_back({f.node, j.d0 + j.tb, 8, sub});
+            } else {
+                st.push_back({nd.right, f.r + 1, (f.path << 1) | 1});
+                st.push_back({nd.left, f.r + 1, f.path << 1});
+            }
+        }
+    }
+    return Status::ok();
+}
+
+}  // namespace huff
+
+// ---------------------------------------------------------------------------
+// buffers
+// ---------------------------------------------------------------------------
+huff::Status PinnedBuf::ensure(size_t bytes) {
+    if (bytes <= cap) return wait();
+    HUFF_TRY(wait());
+    if (p) hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t c = std::max<size_t>(bytes, 4096);
+    HIP_TRY(hipHostMalloc(&p, c, hipHostMallocDefault));
+    cap = c;
+    if (!ev) HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    return huff::Status::ok();
+}
+
+huff::Status PinnedBuf::wait() {
+    if (ev) HIP_TRY(hipEventSynchronize(ev));
+    return huff::Status::ok();
+}
+
+PinnedBuf::~PinnedBuf() {
+    if (ev) {
+        hipEventSynchronize(ev);
+        hipEventDestroy(ev);
+    }
+    if (p) hipHostFree(p);
+}
+
+huff::Status DevBuf::ensure(size_t bytes) {
+    if (bytes <= cap && p) return huff::Status::ok();
+    release();
+    size_t c = std::max<size_t>((bytes + 255) & ~size_t(255), 256);
+    HIP_TRY(hipMalloc(&p, c));
+    cap = c;
+    return huff::Status::ok();
+}
+
+void DevBuf::release() {
+    if (p) hipFree(p);
+    p = nullptr;
+    cap = 0;
+}
+
+// ---------------------------------------------------------------------------
+// context
+// ---------------------------------------------------------------------------
+huff::Status huff_ctx::activate() const {
+    HIP_TRY(hipSetDevice(device));
+    return huff::Status::ok();
+}
+
+huff::Status huff_ctx::timed(const char* name, const std::function<hipError_t()>& launch) {
+    if (!timing) {
+        HIP_TRY(launch());
+        return huff::Status::ok();
+    }
+    hipEvent_t ev[2];
+    for (auto& e : ev) {
+        if (!free_events.empty()) {
+            e = free_events.back();
+            free_events.pop_back();
+        } else {
+            HIP_TRY(hipEventCreate(&e));
+        }
+    }
+    HIP_TRY(hipEventRecord(ev[0], stream));
+    HIP_TRY(launch());
+    HIP_TRY(hipEventRecord(ev[1], stream));
+    pending.push_back({name, ev[0], ev[1]});
+    return huff::Status::ok();
+}
+
+huff::Status huff_ctx::collect_timing() {
+    if (pending.empty()) return huff::Status::ok();
+    HIP_TRY(hipStreamSynchronize(stream));
+    for (auto& p : pending) {
+        float ms = 0.f;
+        HIP_TRY(hipEventElapsedTime(&ms, p.a, p.b));
+        auto& k = kstats[p.name];
+        k.first += ms;
+        k.second += 1;
+        free_events.push_back(p.a);
+        free_events.push_back(p.b);
+    }
+    pending.clear();
+    return huff::Status::ok();
+}
+
+huff::Status huff_ctx::sync() {
+    HIP_TRY(hipStreamSynchronize(stream));
+    return huff::Status::ok();
+}
+
+huff::Status huff_ctx::upload_enc_tables(const huff_tree* t, const uint8_t* prev_tail, size_t prev_tail_len) {
+    const huff::EncTables& et = t->enc_tables();
+    const bool long_codes = et.maxlen > huff::dev::kShortMaxLen;
+    HUFF_TRY(pin_tab.ensure(256 * 8 + 256 + 16));
+    uint8_t* h = static_cast<uint8_t*>(pin_tab.p);
+    if (long_codes) {
+        uint64_t* e = reinterpret_cast<uint64_t*>(h);
+        for (int b = 0; b < 256; ++b) e[b] = (et.code[b] << 6) | et.len[b];
+    } else {
+        uint32_t* e = reinterpret_cast<uint32_t*>(h);
+        for (int b = 0; b < 256; ++b) e[b] = static_cast<uint32_t>(et.code[b] << 5) | et.len[b];
+    }
+    std::memcpy(h + 2048, et.len, 256);
+    std::memset(h + 2304, 0, 8);
+    if (prev_tail_len) std::memcpy(h + 2304 + 8 - prev_tail_len, prev_tail, prev_tail_len);
+    HUFF_TRY(d_tab.ensure(2048 + 256 + 8));
+    HIP_TRY(hipMemcpyAsync(d_tab.p, h, 2048 + 256 + 8, hipMemcpyHostToDevice, stream));
+    HIP_TRY(hipEventRecord(pin_tab.ev, stream));
+    tab_tree_id = t->id;
+    tab_long = long_codes;
+    return huff::Status::ok();
+}
+
+huff::Status huff_ctx::upload_dec_tables(const huff_tree* t, const huff::DecTables** dt) {
+    HUFF_TRY(t->dec_tables(dt));
+    if (lut_tree_id == t->id) return huff::Status::ok();
+    const size_t bytes = (*dt)->lut.size() * 4;
+    HUFF_TRY(pin_lut.ensure(bytes));
+    std::memcpy(pin_lut.p, (*dt)->lut.data(), bytes);
+    HUFF_TRY(d_lut.ensure(bytes));
+    HIP_TRY(hipMemcpyAsync(d_lut.p, pin_lut.p, bytes, hipMemcpyHostToDevice, stream));
+    HIP_TRY(hipEventRecord(pin_lut.ev, stream));
+    lut_tree_id = t->id;
+    return huff::Status::ok();
+}
+
+// ---------------------------------------------------------------------------
+// encode job
+// ---------------------------------------------------------------------------
+huff::Status huff_enc::init(huff_ctx* c, const uint8_t* d, uint64_t nbytes) {
+    if (reinterpret_cast<uintptr_t>(d) & 15)
+        return huff::Status::err(HUFF_E_INVALID_ARG, "device input must be 16-byte aligned");
+    ctx = c;
+    d_in = d;
+    n = nbytes;
+    nchunks = static_cast<uint32_t>((n + huff::dev::kChunk - 1) / huff::dev::kChunk);
+    have_hist = packed = false;
+    const size_t nc = std::max<uint32_t>(nchunks, 1);
+    HUFF_TRY(chunk_hist.ensure(nc * 256 * 4));
+    HUFF_TRY(gw.ensure(huff::dev::kHistCopies * 256 * 8));
+    HUFF_TRY(chunk_bits.ensure(nc * 8));
+    HUFF_TRY(chunk_start.ensure((nc + 1) * 8));
+    HUFF_TRY(sub_bit.ensure(((n + huff::dev::kSub - 1) / huff::dev::kSub + 1) * 4));
+    HUFF_TRY(mask.ensure(256));
+    HUFF_TRY(pos.ensure(8));
+    return huff::Status::ok();
+}
+
+huff::Status huff_enc::hist() {
+    HUFF_TRY(ctx->activate());
+    hipStream_t s = ctx->stream;
+    HIP_TRY(hipMemsetAsync(gw.p, 0, huff::dev::kHistCopies * 256 * 8, s));
+    HUFF_TRY(ctx->timed("hist", [&] {
+        return huff::dev::launch_hist(d_in, 0, n, nchunks, static_cast<uint32_t*>(chunk_hist.p),
+                                      static_cast<unsigned long long*>(gw.p), s);
+    }));
+    HUFF_TRY(ctx->pin_w.ensure(huff::dev::kHistCopies * 256 * 8));
+    HIP_TRY(hipMemcpyAsync(ctx->pin_w.p, gw.p, huff::dev::kHistCopies * 256 * 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipEventRecord(ctx->pin_w.ev, s));
+    HUFF_TRY(ctx->pin_w.wait());
+    const uint64_t* h = static_cast<const uint64_t*>(ctx->pin_w.p);
+    for (int b = 0; b < 256; ++b) {
+        uint64_t s8 = 0;
+        for (uint32_t k = 0; k < huff::dev::kHistCopies; ++k) s8 += h[k * 256 + b];
+        w[b] = s8;
+    }
+    have_hist = true;
+    packed = false;
+    return huff::Status::ok();
+}
+
+huff::Status huff_enc::bits(const huff_tree* t, uint64_t* total) {
+    if (!have_hist) return huff::Status::err(HUFF_E_STATE, "huff_enc_hist must run before bits/pack");
+    const huff::EncTables& et = t->enc_tables();
+    uint64_t b = 0;
+    for (int i = 0; i < 256; ++i) {
+        if (w[i] && et.len[i] == 0 && et.fits64) {
+            // compress_with_tree reports the FIRST missing letter in input order
+            uint8_t m[256];
+            for (int k = 0; k < 256; ++k) m[k] = (w[k] && et.len[k] == 0) ? 1 : 0;
+            HUFF_TRY(ctx->activate());
+            HIP_TRY(hipMemcpy(mask.p, m, 256, hipMemcpyHostToDevice));
+            unsigned long long init = ~0ull;
+            HIP_TRY(hipMemcpy(pos.p, &init, 8, hipMemcpyHostToDevice));
+            HIP_TRY(huff::dev::launch_find_first(d_in, n, static_cast<const uint8_t*>(mask.p),
+                                                 static_cast<unsigned long long*>(pos.p), ctx->stream));
+            unsigned long long p = 0;
+            HIP_TRY(hipMemcpyAsync(&p, pos.p, 8, hipMemcpyDeviceToHost, ctx->stream));
+            HUFF_TRY(ctx->sync());
+            uint8_t letter = 0;
+            HIP_TRY(hipMemcpy(&letter, d_in + p, 1, hipMemcpyDeviceToHost));
+            huff::Status st = huff::Status::err(HUFF_E_MISSING_LETTER, "letter not found in codes");
+            st.missing_letter = letter;
+            return st;
+        }
+        b += w[i] * et.len[i];
+    }
+    if (!et.fits64 || et.maxlen > huff::dev::kLongMaxLen)
+        return huff::Status::err(HUFF_E_CODE_TOO_LONG, "code longer than 57 bits: outside the GPU encoder's range");
+    *total = b;
+    return huff::Status::ok();
+}
+
+huff::Status huff_enc::pack(const huff_tree* t, uint64_t base, const uint8_t* prev_tail, size_t prev_tail_len,
+                            uint8_t* d_out, size_t out_cap, uint64_t* total) {
+    uint64_t tb = 0;
+    HUFF_TRY(bits(t, &tb));
+    const uint64_t need = ((base & 7) + tb + 7) / 8;
+    if (total) *total = tb;
+    if (need > out_cap) return huff::Status::err(HUFF_E_BUFFER_TOO_SMALL, "output buffer too small");
+    if (prev_tail_len > 8) return huff::Status::err(HUFF_E_INVALID_ARG, "prev_tail holds at most 8 bytes");
+    HUFF_TRY(ctx->activate());
+    hipStream_t s = ctx->stream;
+    HUFF_TRY(ctx->upload_enc_tables(t, prev_tail, prev_tail_len));
+    const uint8_t* d_tab = static_cast<const uint8_t*>(ctx->d_tab.p);
+    HUFF_TRY(ctx->timed("chunk_bits", [&] {
+        return huff::dev::launch_chunk_bits(static_cast<const uint32_t*>(chunk_hist.p), nchunks, d_tab + 2048,
+                                            static_cast<uint64_t*>(chunk_bits.p), s);
+    }));
+    HUFF_TRY(ctx->timed("scan", [&] {
+        return huff::dev::launch_scan(static_cast<const uint64_t*>(chunk_bits.p), nchunks, base & 7,
+                                      static_cast<uint64_t*>(chunk_start.p), s);
+    }));
+    const huff::EncTables& et = t->enc_tables();
+    huff::dev::PackArgs a{};
+    a.in = d_in;
+    a.n = n;
+    a.table = d_tab;
+    a.chunk_start = static_cast<const uint64_t*>(chunk_start.p);
+    a.nchunks = nchunks;
+    a.out = d_out;
+    a.sub_bit = static_cast<uint32_t*>(sub_bit.p);
+    a.prev_tail = d_tab + 2304;
+    a.prev_tail_len = static_cast<uint32_t>(prev_tail_len);
+    a.stage_words = (128 * std::max<uint32_t>(et.maxlen, 1) + 16 + 3) & ~3u;
+    HUFF_TRY(ctx->timed("pack", [&] { return huff::dev::launch_pack(ctx->tab_long, a, s); }));
+    packed = true;
+    packed_tree_id = t->id;
+    bit_base = base;
+    total_bits = tb;
+    return huff::Status::ok();
+}
+
+huff::Status huff_enc::decode(const huff_tree* t, const uint8_t* d_comp, uint64_t comp_bytes, uint8_t* d_out) {
+    if (!packed) return huff::Status::err(HUFF_E_STATE, "no restart index: pack (or upload an index) first");
+    if (reinterpret_cast<uintptr_t>(d_comp) & 3)
+        return huff::Status::err(HUFF_E_INVALID_ARG, "compressed stream must be 4-byte aligned");
+    HUFF_TRY(ctx->activate());
+    const huff::DecTables* dt = nullptr;
+    HUFF_TRY(ctx->upload_dec_tables(t, &dt));
+    huff::dev::DecodeArgs a{};
+    a.comp = d_comp;
+    a.comp_bytes = comp_bytes;
+    a.lut = static_cast<const uint32_t*>(ctx->d_lut.p);
+    a.lut_bits = dt->bits;
+    a.lut_words = static_cast<uint32_t>(dt->lut.size());
+    a.chunk_start = static_cast<const uint64_t*>(chunk_start.p);
+    a.sub_bit = static_cast<const uint32_t*>(sub_bit.p);
+    a.nchunks = nchunks;
+    a.n = n;
+    a.out = d_out;
+    HUFF_TRY(ctx->timed("decode", [&] { return huff::dev::launch_decode(a, ctx->stream); }));
+    return huff::Status::ok();
+}
+
+huff::Status huff_enc::download_index(huff_index_host& idx) {
+    idx.n = n;
+    idx.chunk_start.resize(nchunks + 1);
+    idx.sub_bit.resize((n + huff::dev::kSub - 1) / huff::dev::kSub);
+    HUFF_TRY(ctx->activate());
+    HIP_TRY(hipMemcpyAsync(idx.chunk_start.data(), chunk_start.p, idx.chunk_start.size() * 8, hipMemcpyDeviceToHost,
+                           ctx->stream));
+    if (!idx.sub_bit.empty())
+        HIP_TRY(hipMemcpyAsync(idx.sub_bit.data(), sub_bit.p, idx.sub_bit.size() * 4, hipMemcpyDeviceToHost,
+                               ctx->stream));
+    return ctx->sync();
+}
+
+huff::Status huff_enc::upload_index(const huff_index_host& idx) {
+    if (idx.n != n || idx.chunk_start.size() != nchunks + 1u)
+        return huff::Status::err(HUFF_E_INVALID_ARG, "restart index does not match the job");
+    HUFF_TRY(ctx->activate());
+    HIP_TRY(hipMemcpyAsync(chunk_start.p, idx.chunk_start.data(), idx.chunk_start.size() * 8, hipMemcpyHostToDevice,
+                           ctx->stream));
+    if (!idx.sub_bit.empty())
+        HIP_TRY(hipMemcpyAsync(sub_bit.p, idx.sub_bit.data(), idx.sub_bit.size() * 4, hipMemcpyHostToDevice,
+                               ctx->stream));
+    HUFF_TRY(ctx->sync());
+    packed = true;
+    return huff::Status::ok();
+}
+
+// ---------------------------------------------------------------------------
+// host-pointer pipelines
+// ---------------------------------------------------------------------------
+namespace huff {
+
+static Status stage_input(huff_ctx* ctx, const uint8_t* bytes, size_t n) {
+    HUFF_TRY(ctx->activate());
+    HUFF_TRY(ctx->d_in.ensure(n + 16));
+    if (n) HIP_TRY(hipMemcpyAsync(ctx->d_in.p, bytes, n, hipMemcpyHostToDevice, ctx->stream));
+    return Status::ok();
+}
+
+Status weights_from_host(huff_ctx* ctx, const uint8_t* bytes, size_t n, ByteWeights& out) {
+    out = ByteWeights{};
+    if (n == 0) return Status::ok();
+    HUFF_TRY(stage_input(ctx, bytes, n));
+    huff_enc e;
+    HUFF_TRY(e.init(ctx, static_cast<const uint8_t*>(ctx->d_in.p), n));
+    HUFF_TRY(e.hist());
+    out = ByteWeights::from_counts(e.w);
+    return Status::ok();
+}
+
+Status weights_threaded_from_host(huff_ctx* ctx, const uint8_t* bytes, size_t n, size_t thread_num,
+                                  ByteWeights& out) {
+    // weights.rs:293-319: per-ration histograms (here: one hist256 launch per
+    // ration over the staged buffer), then `w = W_last; w += W_0 .. W_{T-2}`.
+    if (thread_num == 0) return Status::err(HUFF_E_INVALID_ARG, "thread_num must be > 0");
+    auto rations = ration_bounds(n, thread_num);
+    HUFF_TRY(stage_input(ctx, bytes, n));
+    const size_t R = rations.size();
+    DevBuf gws;
+    HUFF_TRY(gws.ensure(R * dev::kHistCopies * 256 * 8));
+    HIP_TRY(hipMemsetAsync(gws.p, 0, R * dev::kHistCopies * 256 * 8, ctx->stream));
+    const uint8_t* d = static_cast<const uint8_t*>(ctx->d_in.p);
+    for (size_t r = 0; r < R; ++r) {
+        const size_t lo = rations[r].first, hi = rations[r].second;
+        if (hi == lo) continue;
+        const size_t abase = lo & ~size_t(15);
+        const uint64_t llo = lo - abase, lhi = hi - abase;
+        const uint32_t nch = static_cast<uint32_t>((lhi + dev::kChunk - 1) / dev::kChunk);
+        HIP_TRY(dev::launch_hist(d + abase, llo, lhi, nch, nullptr,
+                                 static_cast<unsigned long long*>(gws.p) + r * dev::kHistCopies * 256, ctx->stream));
+    }
+    std::vector<uint64_t> h(R * dev::kHistCopies * 256);
+    HIP_TRY(hipMemcpyAsync(h.data(), gws.p, h.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
+    HUFF_TRY(ctx->sync());
+    std::vector<ByteWeights> parts(R);
+    for (size_t r = 0; r < R; ++r) {
+        uint64_t c[256];
+        for (int b = 0; b < 256; ++b) {
+            uint64_t s = 0;
+            for (uint32_t k = 0; k < dev::kHistCopies; ++k) s += h[(r * dev::kHistCopies + k) * 256 + b];
+            c[b] = s;
+        }
+        parts[r] = ByteWeights::from_counts(c);
+    }
+    out = parts[R - 1];
+    for (size_t r = 0; r + 1 < R; ++r) out.add(parts[r]);
+    return Status::ok();
+}
+
+Status compress_host(huff_ctx* ctx, const uint8_t* bytes, size_t n, const huff_tree* t, huff_compress_data** out) {
+    *out = nullptr;
+    if (n == 0) return Status::err(HUFF_E_EMPTY_COMP, "provided comp_bytes are empty");
+    HUFF_TRY(stage_input(ctx, bytes, n));
+    huff_enc e;
+    HUFF_TRY(e.init(ctx, static_cast<const uint8_t*>(ctx->d_in.p), n));
+    HUFF_TRY(e.hist());
+    std::unique_ptr<huff_tree> own;
+    if (!t) {  // compress_bytes: the tree comes from this very histogram
+        own = std::make_unique<huff_tree>();
+        HUFF_TRY(HuffTree::from_weights(ByteWeights::from_counts(e.w), own->t));
+        t = own.get();
+    }
+    uint64_t tb = 0;
+    HUFF_TRY(e.bits(t, &tb));
+    const size_t nbytes = static_cast<size_t>((tb + 7) / 8);
+    HUFF_TRY(ctx->d_out.ensure(nbytes + 16));
+    HUFF_TRY(e.pack(t, 0, nullptr, 0, static_cast<uint8_t*>(ctx->d_out.p), nbytes, &tb));
+    auto cd = std::make_unique<huff_compress_data>();
+    cd->comp.resize(nbytes);
+    HIP_TRY(hipMemcpyAsync(cd->comp.data(), ctx->d_out.p, nbytes, hipMemcpyDeviceToHost, ctx->stream));
+    cd->padding = calc_padding_bits(tb);  // comp.rs:446
+    cd->index = std::make_unique<huff_index_host>();
+    HUFF_TRY(e.download_index(*cd->index));
+    if (own) {
+        cd->tree = own.release();
+    } else {
+        cd->tree = new huff_tree();
+        cd->tree->t = t->t;
+    }
+    *out = cd.release();
+    return Status::ok();
+}
+
+Status decompress_host(huff_ctx* ctx, const huff_compress_data* cd, uint8_t* out, size_t cap, size_t* out_len) {
+    if (!cd->index) {
+        // comp.rs:513-516: all bytes but the last give 8 bits, the last 8 - padding
+        const uint64_t valid = static_cast<uint64_t>(cd->comp.size()) * 8 - cd->padding;
+        std::vector<uint8_t> sym;
+        HUFF_TRY(decode_indexless_host(ctx, cd->comp.data(), cd->comp.size(), valid, cd->tree, sym));
+        *out_len = sym.size();
+        if (cap < sym.size()) return Status::err(HUFF_E_BUFFER_TOO_SMALL, "output buffer too small");
+        if (!sym.empty()) std::memcpy(out, sym.data(), sym.size());
+        return Status::ok();
+    }
+    const uint64_t n = cd->index->n;
+    *out_len = n;
+    if (cap < n) return Status::err(HUFF_E_BUFFER_TOO_SMALL, "output buffer too small");
+    if (n == 0) return Status::ok();
+    HUFF_TRY(ctx->activate());
+    HUFF_TRY(ctx->d_in.ensure(cd->comp.size() + 16));
+    HIP_TRY(hipMemcpyAsync(ctx->d_in.p, cd->comp.data(), cd->comp.size(), hipMemcpyHostToDevice, ctx->stream));
+    HUFF_TRY(ctx->d_out.ensure(n + 16));
+    huff_enc e;
+    // the job's input pointer is unused by decode; give it the output staging (aligned)
+    HUFF_TRY(e.init(ctx, static_cast<const uint8_t*>(ctx->d_out.p), n));
+    HUFF_TRY(e.upload_index(*cd->index));
+    HUFF_TRY(e.decode(cd->tree, static_cast<const uint8_t*>(ctx->d_in.p), cd->comp.size(),
+                      static_cast<uint8_t*>(ctx->d_out.p)));
+    HIP_TRY(hipMemcpyAsync(out, ctx->d_out.p, n, hipMemcpyDeviceToHost, ctx->stream));
+    return ctx->sync();
+}
+
+Status parse_block_size(const char* s, size_t* out) {
+    // huff/src/cli.rs:79-114: digits, then an optional unit (case-insensitive)
+    if (!s) return Status::err(HUFF_E_INVALID_ARG, "Invalid block size");
+    std::string lower;
+    for (const char* p = s; *p; ++p) lower.push_back(static_cast<char>(std::tolower(static_cast<unsigned char>(*p))));
+    size_t i = 0;
+    std::string num;
+    while (i < lower.size() && std::isdigit(static_cast<unsigned char>(lower[i]))) num.push_back(lower[i++]);
+    std::string mult = lower.substr(i);
+    if (num.empty()) return Status::err(HUFF_E_INVALID_ARG, "Invalid block size");
+    unsigned long long v = 0;
+    for (char ch : num) {  // usize::parse: overflow is an error
+        const unsigned d = static_cast<unsigned>(ch - '0');
+        if (v > (~0ull - d) / 10) return Status::err(HUFF_E_INVALID_ARG, "Invalid block size");
+        v = v * 10 + d;
+    }
+    if (v == 0) return Status::err(HUFF_E_INVALID_ARG, "Invalid block size");
+    unsigned long long m;
+    if (mult.empty()) m = 1;
+    else if (mult == "k") m = 1000ull;
+    else if (mult == "m") m = 1000000ull;
+    else if (mult == "g") m = 1000000000ull;
+    else if (mult == "ki") m = 1024ull;
+    else if (mult == "mi") m = 1048576ull;
+    else if (mult == "gi") m = 1073741824ull;
+    else return Status::err(HUFF_E_INVALID_ARG, "Invalid block size");
+    *out = static_cast<size_t>(v * m);
+    return Status::ok();
+}
+
+}  // namespace huff
+
+// ---------------------------------------------------------------------------
+// index-free decode
+// ---------------------------------------------------------------------------
+namespace huff {
+
+Status decode_indexless_dev(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_bytes, uint64_t valid_bits,
+                            const huff_tree* t, DevBuf& out, uint64_t* nsym) {
+    *nsym = 0;
+    if (valid_bits == 0) return Status::ok();
+    if (reinterpret_cast<uintptr_t>(d_comp) & 3)
+        return Status::err(HUFF_E_INVALID_ARG, "compressed stream must be 4-byte aligned");
+    HUFF_TRY(ctx->activate());
+    const DecTables* dt = nullptr;
+    HUFF_TRY(ctx->upload_dec_tables(t, &dt));
+    // segment length: a multiple of the gcd of all code lengths
+    uint32_t g = 0;
+    for (const LeafCode& lc : t->t.leaves()) g = std::gcd(g, lc.len);
+    if (g == 0) g = 1;
+    const uint64_t S = static_cast<uint64_t>(g) * ((2048 + g - 1) / g);
+    const uint64_t nseg = (valid_bits + S - 1) / S;
+    DevBuf s, x0, x1, c, off, flag;
+    HUFF_TRY(s.ensure(nseg * 8));
+    HUFF_TRY(x0.ensure(nseg * 8));
+    HUFF_TRY(x1.ensure(nseg * 8));
+    HUFF_TRY(c.ensure(nseg * 8));
+    HUFF_TRY(off.ensure((nseg + 1) * 8));
+    HUFF_TRY(flag.ensure(4));
+    dev::IndexlessArgs a{};
+    a.comp = d_comp;
+    a.comp_bytes = comp_bytes;
+    a.valid_bits = valid_bits;
+    a.seg_bits = S;
+    a.nseg = nseg;
+    a.lut = static_cast<const uint32_t*>(ctx->d_lut.p);
+    a.lut_bits = dt->bits;
+    a.s = static_cast<uint64_t*>(s.p);
+    a.x = static_cast<uint64_t*>(x0.p);
+    a.c = static_cast<uint64_t*>(c.p);
+    hipStream_t st = ctx->stream;
+    HIP_TRY(dev::launch_indexless_spec(a, st));
+    uint64_t* xa = static_cast<uint64_t*>(x0.p);
+    uint64_t* xb = static_cast<uint64_t*>(x1.p);
+    bool settled = false;
+    for (int it = 0; it < 32 && !settled; ++it) {
+        HIP_TRY(hipMemsetAsync(flag.p, 0, 4, st));
+        HIP_TRY(dev::launch_indexless_fix(a, xa, xb, static_cast<unsigned int*>(flag.p), st));
+        unsigned int changed = 0;
+        HIP_TRY(hipMemcpyAsync(&changed, flag.p, 4, hipMemcpyDeviceToHost, st));
+        HUFF_TRY(ctx->sync());
+        std::swap(xa, xb);
+        settled = changed == 0;
+    }
+    if (!settled) HIP_TRY(dev::launch_indexless_settle(a, xa, st));
+    if (nseg > 0xFFFFFFFFull) return Status::err(HUFF_E_INVALID_ARG, "stream too long for one decode");
+    HIP_TRY(dev::launch_scan(static_cast<const uint64_t*>(c.p), static_cast<uint32_t>(nseg), 0,
+                             static_cast<uint64_t*>(off.p), st));
+    uint64_t total = 0;
+    HIP_TRY(hipMemcpyAsync(&total, static_cast<uint64_t*>(off.p) + nseg, 8, hipMemcpyDeviceToHost, st));
+    HUFF_TRY(ctx->sync());
+    HUFF_TRY(out.ensure(total + 16));
+    HIP_TRY(dev::launch_indexless_emit(a, static_cast<const uint64_t*>(off.p), static_cast<uint8_t*>(out.p), st));
+    *nsym = total;
+    return Status::ok();
+}
+
+Status decode_indexless_host(huff_ctx* ctx, const uint8_t* comp, size_t len, uint64_t valid_bits, const huff_tree* t,
+                             std::vector<uint8_t>& out) {
+    out.clear();
+    HUFF_TRY(ctx->activate());
+    DevBuf d_comp, d_out;
+    HUFF_TRY(d_comp.ensure(len + 16));
+    HIP_TRY(hipMemcpyAsync(d_comp.p, comp, len, hipMemcpyHostToDevice, ctx->stream));
+    uint64_t n = 0;
+    HUFF_TRY(decode_indexless_dev(ctx, static_cast<const uint8_t*>(d_comp.p), len, valid_bits, t, d_out, &n));
+    out.resize(n);
+    if (n) HIP_TRY(hipMemcpyAsync(out.data(), d_out.p, n, hipMemcpyDeviceToHost, ctx->stream));
+    return ctx->sync();
+}
+
+}  // namespace huff

@@ -1,0 +1,162 @@
+// runtime.hpp — context, device workspace and the encode/decode pipeline.
+//
+// huff_ctx owns a HIP stream (or adopts the caller's), pinned staging for the
+// tiny host<->device hops of the pipeline (weights down, code tables up) and
+// the device staging buffers of the host-pointer API. huff_enc is one encode
+// job over bytes already in HBM: hist -> (host) tree -> bits/scan -> pack ->
+// decode, exactly the hot path of SURVEY.md §3.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <functional>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../device/kernels.hpp"
+#include "../host/huff_coding.hpp"
+
+namespace huff {
+
+inline Status hip_status(hipError_t e, const char* what) {
+    if (e == hipSuccess) return Status::ok();
+    return Status::err(HUFF_E_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+#define HIP_TRY_RT(expr) HUFF_TRY(::huff::hip_status((expr), #expr))
+
+// Encode/decode tables derived from a tree (built once per tree, cached).
+struct EncTables {
+    uint64_t code[256];
+    uint8_t len[256];
+    uint32_t maxlen = 0;
+    bool fits64 = true;
+};
+
+struct DecTables {
+    std::vector<uint32_t> lut;  // primary [1 << bits] then 8-bit secondaries
+    uint32_t bits = 0;
+    uint32_t maxdepth = 0;
+};
+
+Status build_dec_tables(const HuffTree& t, DecTables& out);
+
+}  // namespace huff
+
+struct huff_tree {
+    huff::HuffTree t;
+    uint64_t id;
+    mutable std::mutex m;
+    mutable std::unique_ptr<huff::EncTables> enc;
+    mutable std::unique_ptr<huff::DecTables> dec;
+
+    huff_tree();
+    const huff::EncTables& enc_tables() const;
+    huff::Status dec_tables(const huff::DecTables** out) const;
+};
+
+// Host-side copy of the encoder's restart index (travels with CompressData).
+struct huff_index_host {
+    uint64_t n = 0;
+    std::vector<uint64_t> chunk_start;  // nchunks + 1
+    std::vector<uint32_t> sub_bit;      // ceil(n / kSub)
+};
+
+struct huff_compress_data {
+    std::vector<uint8_t> comp;
+    uint8_t padding = 0;
+    huff_tree* tree = nullptr;  // owned clone
+    std::unique_ptr<huff_index_host> index;
+    ~huff_compress_data();
+};
+
+struct PinnedBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    hipEvent_t ev = nullptr;  // last async copy out of/into p
+    huff::Status ensure(size_t bytes);
+    huff::Status wait();
+    ~PinnedBuf();
+};
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    huff::Status ensure(size_t bytes);
+    void release();
+    ~DevBuf() { release(); }
+};
+
+struct huff_ctx {
+    int device = 0;
+    hipStream_t own = nullptr;
+    hipStream_t stream = nullptr;
+    PinnedBuf pin_w;     // weights readback
+    PinnedBuf pin_tab;   // code table / len table / prev tail upload
+    PinnedBuf pin_lut;   // decode table upload
+    DevBuf d_in, d_out;  // staging of the host-pointer API
+    DevBuf d_tab, d_len, d_tail, d_lut;
+    uint64_t tab_tree_id = 0, lut_tree_id = 0;
+    bool tab_long = false;
+
+    // kernel timing
+    struct Timed {
+        std::string name;
+        hipEvent_t a, b;
+    };
+    bool timing = false;
+    std::vector<Timed> pending;
+    std::vector<hipEvent_t> free_events;
+    std::map<std::string, std::pair<double, uint64_t>> kstats;
+    huff::Status timed(const char* name, const std::function<hipError_t()>& launch);
+    huff::Status collect_timing();
+
+    huff::Status activate() const;
+    huff::Status upload_enc_tables(const huff_tree* t, const uint8_t* prev_tail, size_t prev_tail_len);
+    huff::Status upload_dec_tables(const huff_tree* t, const huff::DecTables** dt);
+    huff::Status sync();
+};
+
+struct huff_enc {
+    huff_ctx* ctx = nullptr;
+    const uint8_t* d_in = nullptr;
+    uint64_t n = 0;
+    uint32_t nchunks = 0;
+    DevBuf chunk_hist, gw, chunk_bits, chunk_start, sub_bit, mask, pos;
+    uint64_t w[256] = {};
+    bool have_hist = false;
+    // state of the last pack (for decode)
+    bool packed = false;
+    uint64_t packed_tree_id = 0;
+    uint64_t bit_base = 0, total_bits = 0;
+
+    huff::Status init(huff_ctx* c, const uint8_t* d, uint64_t nbytes);
+    huff::Status hist();
+    huff::Status bits(const huff_tree* t, uint64_t* total);
+    huff::Status pack(const huff_tree* t, uint64_t bit_base, const uint8_t* prev_tail, size_t prev_tail_len,
+                      uint8_t* d_out, size_t out_cap, uint64_t* total);
+    huff::Status decode(const huff_tree* t, const uint8_t* d_comp, uint64_t comp_bytes, uint8_t* d_out);
+    huff::Status download_index(huff_index_host& idx);
+    huff::Status upload_index(const huff_index_host& idx);
+};
+
+namespace huff {
+// host-pointer pipelines used by the C ABI
+Status weights_from_host(huff_ctx* ctx, const uint8_t* bytes, size_t n, ByteWeights& out);
+Status weights_threaded_from_host(huff_ctx* ctx, const uint8_t* bytes, size_t n, size_t thread_num,
+                                  ByteWeights& out);
+Status compress_host(huff_ctx* ctx, const uint8_t* bytes, size_t n, const huff_tree* t, huff_compress_data** out);
+Status decompress_host(huff_ctx* ctx, const huff_compress_data* cd, uint8_t* out, size_t cap, size_t* out_len);
+Status file_compress(huff_ctx* ctx, const char* src, const char* dst, size_t block_size);
+Status file_decompress(huff_ctx* ctx, const char* src, const char* dst, size_t block_size);
+Status parse_block_size(const char* s, size_t* out);
+// decode without a restart index: valid_bits of the stream at d_comp; the
+// symbols land in `out` (grown as needed), their count in *nsym
+Status decode_indexless_dev(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_bytes, uint64_t valid_bits,
+                            const huff_tree* t, DevBuf& out, uint64_t* nsym);
+Status decode_indexless_host(huff_ctx* ctx, const uint8_t* comp, size_t len, uint64_t valid_bits,
+                             const huff_tree* t, std::vector<uint8_t>& out);
+}  // namespace huff

@@ -1,0 +1,130 @@
+"""Device-resident encode/decode jobs (huff_enc_* in include/huffgpu.h).
+
+Inputs already live in HBM (a torch tensor's data_ptr() or a huff_dev_alloc
+pointer). Used by bench.py and the multi-GPU path; the reference-named API in
+__init__ stages host buffers through the same kernels.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Optional
+
+import numpy as np
+
+from . import _lib
+from ._lib import load
+
+
+def _check(rc):
+    from . import _check as chk
+
+    chk(rc)
+
+
+class EncodeJob:
+    """hist256 -> (host) HuffTree -> pack -> (restart-index) decode over one buffer."""
+
+    def __init__(self, ctx, d_in: int, n: int):
+        self.ctx = ctx
+        self.n = n
+        self.h = C.c_void_p()
+        _check(load().huff_enc_create(ctx.h, C.c_void_p(d_in), n, C.byref(self.h)))
+
+    def close(self):
+        if getattr(self, "h", None):
+            load().huff_enc_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def hist(self) -> np.ndarray:
+        """pass 1: the 256 weights (u64) of the job's bytes"""
+        w = (C.c_uint64 * 256)()
+        _check(load().huff_enc_hist(self.h, w))
+        return np.array(w[:], dtype=np.uint64)
+
+    def bits(self, tree) -> int:
+        v = C.c_uint64()
+        _check(load().huff_enc_bits(self.h, tree.h, C.byref(v)))
+        return v.value
+
+    def pack(self, tree, d_out: int, out_cap: int, bit_base: int = 0, prev_tail: Optional[bytes] = None) -> int:
+        """pass 2: writes ceil((bit_base%8 + bits)/8) bytes at d_out; returns bits"""
+        v = C.c_uint64()
+        pt = prev_tail or b""
+        buf = C.create_string_buffer(pt, len(pt)) if pt else None
+        _check(load().huff_enc_pack(self.h, tree.h, bit_base, buf, len(pt), C.c_void_p(d_out), out_cap,
+                                    C.byref(v)))
+        return v.value
+
+    def decode(self, tree, d_comp: int, d_out: int):
+        """block-parallel decode of this job's pack output via its restart index"""
+        _check(load().huff_enc_decode(self.h, tree.h, C.c_void_p(d_comp), C.c_void_p(d_out)))
+
+
+def generate(ctx, kind: str, seed: int, d_out: int, n: int, offset: int = 0, cdf: Optional[np.ndarray] = None):
+    """synthetic input in HBM: kind 'uniform' | 'zipf' | 'text' (cdf for zipf)"""
+    k = {"uniform": 0, "zipf": 1, "text": 2}[kind]
+    cp = None
+    if k == 1:
+        cdf = np.ascontiguousarray(cdf, np.uint64)
+        cp = cdf.ctypes.data_as(C.POINTER(C.c_uint64))
+    _check(load().huff_dev_generate(ctx.h, k, seed, offset, cp, C.c_void_p(d_out), n))
+
+
+def zipf_cdf(alpha: float = 1.2) -> np.ndarray:
+    """P(rank k) ~ k^-alpha, k=1..256, byte = k-1; cdf[k-1] = floor(2^64 * P(<=k))
+    (same definition as oracle/huff_oracle.c orc_zipf_cdf; an input table)."""
+    import math
+
+    p = [math.pow(float(k), -alpha) for k in range(1, 257)]
+    s = 0.0
+    for v in p:  # sequential, in the same order as the C definition
+        s += v
+    acc = 0.0
+    cdf = np.zeros(256, np.uint64)
+    for i in range(256):
+        acc += p[i] / s
+        scaled = acc * 18446744073709551616.0
+        cdf[i] = np.uint64(0xFFFFFFFFFFFFFFFF) if scaled >= 18446744073709551615.0 else np.uint64(int(scaled))
+    cdf[255] = np.uint64(0xFFFFFFFFFFFFFFFF)
+    return cdf
+
+
+class DeviceBuffer:
+    """hipMalloc'd bytes owned by a context (for callers without torch)."""
+
+    def __init__(self, ctx, nbytes: int):
+        self.ctx = ctx
+        self.nbytes = nbytes
+        self.p = C.c_void_p()
+        _check(load().huff_dev_alloc(ctx.h, nbytes, C.byref(self.p)))
+
+    @property
+    def ptr(self) -> int:
+        return self.p.value
+
+    def upload(self, data: np.ndarray):
+        a = np.ascontiguousarray(data, np.uint8)
+        _check(load().huff_memcpy_htod(self.ctx.h, self.p, a.ctypes.data_as(C.c_void_p), a.size))
+
+    def download(self, n: Optional[int] = None) -> np.ndarray:
+        n = self.nbytes if n is None else n
+        out = np.empty(n, np.uint8)
+        _check(load().huff_memcpy_dtoh(self.ctx.h, out.ctypes.data_as(C.c_void_p), self.p, n))
+        return out
+
+    def free(self):
+        if self.p:
+            load().huff_dev_free(self.ctx.h, self.p)
+            self.p = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass

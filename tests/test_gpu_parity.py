@@ -1,0 +1,323 @@
+"""GPU parity: the HIP path through the C ABI vs the oracle, bit-exact.
+
+Small/medium inputs are compared byte-for-byte with the faithful restatement;
+BASELINE-sized inputs (1 GiB) with the oracle's table-driven checker (itself
+checked against the faithful one in test_oracle_golden.py) and through
+size-independent properties (encode -> decode round trip, weights sum = n).
+"""
+import hashlib
+import os
+import tempfile
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+SIZES = [1, 2, 15, 16, 17, 255, 4095, 4096, 4097, 65535, 65536, 65537, 131072 + 333, 1_000_003]
+
+
+def oracle_bytes(O, data):
+    t = O.Tree.from_weights(O.weights_from_bytes(data))
+    comp, pad = O.compress_with_tree(data, t)
+    return O.to_bytes(comp, pad, t), comp, pad, t
+
+
+def inputs(rng):
+    yield "pinned-abbccc", b"abbccc"
+    yield "single", b"a"
+    yield "zero-only", bytes([0])
+    yield "zero-no255", bytes([0, 1, 1, 2, 0, 9])
+    yield "all-256", bytes(range(256)) * 3
+    for n in SIZES:
+        yield f"uniform-{n}", rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+    for n in (100, 70_000, 500_000):
+        yield f"skew-{n}", np.minimum(rng.geometric(0.3, n), 255).astype(np.uint8).tobytes()
+        yield f"two-{n}", rng.integers(0, 2, n, dtype=np.uint8).tobytes()
+        yield f"const-{n}", bytes([7]) * n
+
+
+def test_weights_from_bytes(H, O, ctx):
+    rng = np.random.default_rng(1)
+    for name, data in inputs(rng):
+        g = H.ByteWeights.from_bytes(data, ctx)
+        o = O.weights_from_bytes(data)
+        assert (g.as_array() == o.as_array()).all(), name
+        assert g.len() == o.len, name
+    assert H.ByteWeights.from_bytes(b"", ctx).is_empty()
+
+
+def test_threaded_weights(H, O, ctx):
+    rng = np.random.default_rng(2)
+    cases = [bytes([0, 1] * 12), bytes([0, 1] * 5000), rng.integers(0, 200, 100_003, dtype=np.uint8).tobytes(),
+             b"aaaaa", rng.integers(0, 256, 12 * 65536 + 5, dtype=np.uint8).tobytes()]
+    for data in cases:
+        for T in (1, 3, 12, 100):
+            g = H.ByteWeights.threaded_from_bytes(data, T, ctx)
+            o = O.weights_threaded(data, T)
+            assert (g.as_array() == o.as_array()).all(), (len(data), T)
+            assert g.len() == o.len
+
+
+def test_compress_matches_oracle(H, O, ctx):
+    rng = np.random.default_rng(3)
+    for name, data in inputs(rng):
+        want, comp, pad, _ = oracle_bytes(O, data)
+        cd = H.compress(data, ctx)
+        assert cd.comp_bytes() == comp, name
+        assert cd.padding_bits() == pad, name
+        assert cd.to_bytes() == want, name
+        assert H.decompress(cd, ctx) == data, name
+        # without the restart index (as read from bytes): index-free decode
+        cd2 = H.CompressData.try_from_bytes(want)
+        assert not cd2.has_index()
+        assert H.decompress(cd2, ctx) == data, name
+
+
+def test_pinned_and_derived_vectors(H, ctx, golden):
+    pinned, derived = golden
+    for c in pinned["to_bytes"]:
+        cd = H.compress(c["input_ascii"].encode(), ctx)
+        assert cd.to_bytes().hex() == c["hex"]
+    for c in derived["small"] + derived["survey_crosscheck"]:
+        data = bytes.fromhex(c["input_hex"])
+        assert H.compress(data, ctx).to_bytes().hex() == c["to_bytes"]
+    for c in pinned["roundtrips"]:
+        data = c["input_ascii"].encode()
+        assert H.decompress(H.compress(data, ctx), ctx) == data
+
+
+def test_long_codes(H, O, ctx):
+    """Fibonacci weights: codes past the 27-bit short-table limit (u64 path)"""
+    f = [1, 1]
+    while len(f) < 44:
+        f.append(f[-1] + f[-2])
+    rng = np.random.default_rng(4)
+    # a buffer whose histogram is Fibonacci-shaped would be huge; instead give
+    # the tree explicitly and encode bytes drawn from its letters
+    w = np.zeros(256, np.uint64)
+    letters = rng.choice(256, 44, replace=False)
+    w[letters] = f
+    t = H.HuffTree.from_weights(H.ByteWeights.from_array(w))
+    ot = O.Tree.from_weights(O.weights_from_array(w))
+    assert max(len(v) for v in t.read_codes().values()) > 32
+    data = rng.choice(letters, 300_001).astype(np.uint8).tobytes()
+    cd = H.compress_with_tree(data, t, ctx)
+    comp, pad = O.compress_with_tree(data, ot)
+    assert cd.comp_bytes() == comp and cd.padding_bits() == pad
+    assert H.decompress(cd, ctx) == data
+    assert H.decompress(H.CompressData.try_from_bytes(cd.to_bytes()), ctx) == data
+
+
+def test_missing_letter(H, ctx):
+    t = H.HuffTree.from_weights(H.ByteWeights.from_bytes(b"abb", ctx))
+    with pytest.raises(H.CompressError) as e:
+        H.compress_with_tree(b"abbccc", t, ctx)
+    assert e.value.missing_letter == ord("c")
+    rng = np.random.default_rng(5)
+    data = rng.integers(0, 10, 200_000, dtype=np.uint8)
+    data[150_000] = 77
+    data[199_000] = 66
+    t = H.HuffTree.from_weights(H.ByteWeights.from_array(np.bincount(data[:100_000], minlength=256)))
+    with pytest.raises(H.CompressError) as e:
+        H.compress_with_tree(data.tobytes(), t, ctx)
+    assert e.value.missing_letter == 77  # the first missing letter in input order
+
+
+def test_empty_inputs(H, ctx):
+    with pytest.raises(H.HuffPanic, match="empty weights"):
+        H.compress(b"", ctx)
+    t = H.HuffTree.from_weights(H.ByteWeights.from_bytes(b"ab", ctx))
+    with pytest.raises(H.HuffPanic, match="comp_bytes are empty"):
+        H.compress_with_tree(b"", t, ctx)
+
+
+def test_decompress_foreign_streams(H, O, ctx):
+    """index-free decode of oracle-made streams, incl. odd padding, incomplete
+    final codes and single-leaf trees"""
+    rng = np.random.default_rng(6)
+    for n in (1, 3, 100, 4099, 70_001, 400_000):
+        for hi in (1, 2, 3, 9, 256):
+            data = rng.integers(0, hi, n, dtype=np.uint8).tobytes()
+            raw, comp, pad, t = oracle_bytes(O, data)
+            assert H.decompress(H.CompressData.try_from_bytes(raw), ctx) == O.decompress(comp, pad, t)
+    # arbitrary (non-encoder) payload bytes with an arbitrary padding: whatever
+    # the tree walk yields, incomplete last code dropped
+    t = O.Tree.from_weights(O.weights_from_bytes(b"abracadabra alakazam"))
+    for n in (1, 2, 7, 300, 5000):
+        payload = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        for pad in (0, 3, 7):
+            raw = O.to_bytes(payload, pad, t)
+            assert H.decompress(H.CompressData.try_from_bytes(raw), ctx) == O.decompress(payload, pad, t)
+
+
+def _device_gen(H, ctx, kind, seed, n):
+    import torch
+    from huff_coding import device as D
+
+    x = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
+    D.generate(ctx, kind, seed, x.data_ptr(), n, cdf=D.zipf_cdf(1.2) if kind == "zipf" else None)
+    return x
+
+
+@pytest.mark.parametrize("kind,seed", [("uniform", 0x5EED0001), ("zipf", 0x5EED0002), ("text", 0x5EED0005)])
+def test_device_job_medium(H, O, ctx, kind, seed):
+    import torch
+
+    n = (1 << 24) + 12345  # 16 MiB + a ragged tail
+    x = _device_gen(H, ctx, kind, seed, n)
+    host = x[:n].cpu().numpy()
+    gen = {"uniform": O.gen_uniform, "zipf": O.gen_zipf, "text": O.gen_text}[kind]
+    assert (host == gen(seed, n)).all(), "device generator != oracle generator"
+    job = H.EncodeJob(ctx, x.data_ptr(), n)
+    w = job.hist()
+    assert (w == O.fast_hist(host, 8)).all()
+    tree = H.HuffTree.from_weights(H.ByteWeights.from_array(w))
+    ot = O.Tree.from_weights(O.weights_from_array(w))
+    assert tree.as_bin() == ot.as_bin()
+    bits = job.bits(tree)
+    out = torch.zeros((bits + 7) // 8 + 64, dtype=torch.uint8, device="cuda")
+    assert job.pack(tree, out.data_ptr(), out.numel()) == bits
+    torch.cuda.synchronize()
+    code, ln = ot.code_table()
+    want, wbits = O.fast_encode(host, code, ln, threads=8)
+    got = out[: (bits + 7) // 8].cpu().numpy()
+    assert wbits == bits and (got == want).all()
+    dec = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
+    job.decode(tree, out.data_ptr(), dec.data_ptr())
+    torch.cuda.synchronize()
+    assert torch.equal(dec[:n], x[:n])
+
+
+def test_device_job_full_size_uniform(H, O, ctx):
+    """BASELINE config 2: 1 GiB uniform, bit-exact vs the checker + round trip"""
+    import torch
+
+    n = 1 << 30
+    x = _device_gen(H, ctx, "uniform", 0x5EED0001, n)
+    job = H.EncodeJob(ctx, x.data_ptr(), n)
+    w = job.hist()
+    assert int(w.sum()) == n
+    tree = H.HuffTree.from_weights(H.ByteWeights.from_array(w))
+    assert set(len(v) for v in tree.read_codes().values()) == {8}
+    bits = job.bits(tree)
+    assert bits == 8 * n
+    out = torch.zeros(bits // 8 + 64, dtype=torch.uint8, device="cuda")
+    job.pack(tree, out.data_ptr(), out.numel())
+    dec = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
+    job.decode(tree, out.data_ptr(), dec.data_ptr())
+    torch.cuda.synchronize()
+    assert torch.equal(dec[:n], x[:n])
+    host = x[:n].cpu().numpy()
+    ot = O.Tree.from_weights(O.weights_from_array(w))
+    code, ln = ot.code_table()
+    want, _ = O.fast_encode(host, code, ln, threads=16)
+    got = out[: n].cpu().numpy()
+    assert hashlib.sha256(got.tobytes()).digest() == hashlib.sha256(want.tobytes()).digest()
+
+
+def test_device_job_full_size_zipf(H, O, ctx):
+    """BASELINE config 3: 1 GiB Zipf(1.2), encode + decode, bit-exact"""
+    import torch
+
+    n = 1 << 30
+    x = _device_gen(H, ctx, "zipf", 0x5EED0002, n)
+    job = H.EncodeJob(ctx, x.data_ptr(), n)
+    w = job.hist()
+    tree = H.HuffTree.from_weights(H.ByteWeights.from_array(w))
+    bits = job.bits(tree)
+    assert 5.2 < bits / n < 5.4
+    out = torch.zeros((bits + 7) // 8 + 64, dtype=torch.uint8, device="cuda")
+    job.pack(tree, out.data_ptr(), out.numel())
+    dec = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
+    job.decode(tree, out.data_ptr(), dec.data_ptr())
+    torch.cuda.synchronize()
+    assert torch.equal(dec[:n], x[:n])
+    host = x[:n].cpu().numpy()
+    ot = O.Tree.from_weights(O.weights_from_array(w))
+    code, ln = ot.code_table()
+    want, wb = O.fast_encode(host, code, ln, threads=16)
+    assert wb == bits
+    got = out[: (bits + 7) // 8].cpu().numpy()
+    assert (got == want).all()
+
+
+def test_shard_stitching_on_one_gpu(H, O, ctx):
+    """the multi-GPU data path (bit_base + prev_tail) on one device: shards
+    encoded independently concatenate to the single-stream bytes"""
+    import torch
+
+    rng = np.random.default_rng(8)
+    n = 3_000_017
+    data = np.minimum(rng.geometric(0.2, n), 255).astype(np.uint8)
+    x = torch.from_numpy(data).cuda()
+    w = np.bincount(data, minlength=256).astype(np.uint64)
+    tree = H.HuffTree.from_weights(H.ByteWeights.from_array(w))
+    ot = O.Tree.from_weights(O.weights_from_array(w))
+    code, ln = ot.code_table()
+    want, total = O.fast_encode(data, code, ln, threads=8)
+    bounds = [0, 1_000_003, 1_000_003 + 65536 * 7 + 5, n]
+    pieces = []
+    base = 0
+    for r in range(3):
+        lo, hi = bounds[r], bounds[r + 1]
+        seg = torch.empty(hi - lo + 64, dtype=torch.uint8, device="cuda")
+        seg[: hi - lo] = x[lo:hi]  # 16-B aligned copy of the shard
+        job = H.EncodeJob(ctx, seg.data_ptr(), hi - lo)
+        job.hist()
+        bits = job.bits(tree)
+        out = torch.zeros((base % 8 + bits + 7) // 8 + 64, dtype=torch.uint8, device="cuda")
+        tail = data[max(0, lo - 8):lo].tobytes()
+        job.pack(tree, out.data_ptr(), out.numel(), bit_base=base, prev_tail=tail)
+        torch.cuda.synchronize()
+        nbytes = (base % 8 + bits + 7) // 8
+        own = out[:nbytes].cpu().numpy()
+        # global bytes [base/8, (base+bits)/8) are this shard's; the last shard
+        # also owns its zero-padded final byte
+        keep = nbytes if r == 2 else (base % 8 + bits) // 8
+        pieces.append(own[:keep])
+        # each shard decodes its own symbols from its local stream
+        dec = torch.empty(hi - lo + 64, dtype=torch.uint8, device="cuda")
+        job.decode(tree, out.data_ptr(), dec.data_ptr())
+        torch.cuda.synchronize()
+        assert (dec[: hi - lo].cpu().numpy() == data[lo:hi]).all()
+        base += bits
+    got = np.concatenate(pieces)
+    assert base == total and got.size == want.size and (got == want).all()
+
+
+def test_file_path_matches_cli(H, O, ctx, golden):
+    rng = np.random.default_rng(9)
+    with tempfile.TemporaryDirectory() as d:
+        srcs = [O.gen_text(11, 3000), O.gen_text(12, 777), rng.integers(0, 256, 5000, dtype=np.uint8),
+                np.array([0, 1] * 40 + [3] * 9, np.uint8), O.gen_text(99, 300_000)]
+        for k, src in enumerate(srcs):
+            src = bytes(src)
+            p = os.path.join(d, f"f{k}")
+            open(p, "wb").write(src)
+            for bs in (len(src) + 10, len(src), 1000, 64, 37, 65536):
+                want = O.cli_compress(src, bs)
+                H.read_compress_write(p, p + ".hff", bs, ctx)
+                got = open(p + ".hff", "rb").read()
+                assert got == want, (k, bs)
+                try:
+                    want_dec = O.cli_decompress(want, bs)
+                except O.OracleError as e:
+                    with pytest.raises(H.CliError) as ex:
+                        H.read_decompress_write(p + ".hff", p + ".out", bs, ctx)
+                    assert ex.value.code == e.code
+                    continue
+                H.read_decompress_write(p + ".hff", p + ".out", bs, ctx)
+                assert open(p + ".out", "rb").read() == want_dec, (k, bs)
+        # header errors (huff/src/comp.rs:95-144)
+        bad = os.path.join(d, "bad.hff")
+        for blob, code in ((b"\x00\x00", 11), (b"\x80\x00\x00\x00\x02\xff\xff", 12),
+                           (b"\x00\x00\x00\x00\x09\xff", 11), (b"\x00\x00\x00\x00\x02\xff\xff\x00", 12)):
+            open(bad, "wb").write(blob)
+            with pytest.raises(H.CliError) as ex:
+                H.read_decompress_write(bad, bad + ".out", 2_000_000_000, ctx)
+            assert ex.value.code == code
+        empty = os.path.join(d, "empty")
+        open(empty, "wb").close()
+        with pytest.raises(H.HuffPanic, match="empty weights"):
+            H.read_compress_write(empty, empty + ".hff", 100, ctx)
