@@ -1,0 +1,87 @@
+"""Multi-GPU sharding of the encode/decode path.
+
+One process per GPU. The input is cut into contiguous shards (rank r owns
+bytes [r*n, (r+1)*n) of the global stream). Per step:
+
+  1. every rank runs hist256 on its shard (pass 1);
+  2. ONE collective: all_gather of a 258 x int64 row per rank = its 256
+     weights + its last <= 8 input bytes + their count (RCCL over xGMI on GPUs,
+     gloo in the CPU tests). Every rank now has every rank's histogram;
+  3. every rank builds the identical HuffTree from the summed weights on the
+     host (the tree is a deterministic function of the weights);
+  4. rank r's first bit is O_r = sum_{q<r} bits_q with bits_q = h_q . len —
+     no second collective; the 8 bytes before the shard (previous ranks'
+     tails) let the shard's first, shared byte be completed locally;
+  5. pack at bit_base O_r, then decode locally from the shard's own stream.
+
+The concatenation over ranks of owned_bytes() is byte-identical to
+compress_with_tree over the whole input (the last rank owns the zero-padded
+final byte). Messages are 2 KiB per rank: latency-bound, not link-bound.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import List, Optional
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class ShardPlan:
+    hists: np.ndarray         # [world, 256] u64 per-rank weights
+    weights: np.ndarray       # [256] u64 global weights
+    bit_base: int             # O_r
+    bits: int                 # this rank's bits
+    per_rank_bits: np.ndarray
+    prev_tail: bytes          # <= 8 input bytes right before this shard
+
+
+def exchange(weights: np.ndarray, tail: bytes, device: Optional[torch.device] = None, group=None):
+    """all_gather of [weights(256) | tail bytes | tail length] -> (hists, tails)"""
+    world = dist.get_world_size(group)
+    row = np.zeros(258, np.int64)
+    row[:256] = np.asarray(weights, np.uint64).view(np.int64)
+    t = bytes(tail[-8:])
+    row[256] = np.frombuffer(t.ljust(8, b"\0"), np.int64)[0]
+    row[257] = len(t)
+    rt = torch.from_numpy(row)
+    if device is not None:
+        rt = rt.to(device)
+    rows = [torch.empty_like(rt) for _ in range(world)]
+    dist.all_gather(rows, rt, group=group)
+    allr = torch.stack(rows).cpu().numpy()
+    hists = allr[:, :256].view(np.uint64).copy()
+    tails = [allr[q, 256:257].view(np.uint8)[: int(allr[q, 257])].tobytes() for q in range(world)]
+    return hists, tails
+
+
+def plan(hists: np.ndarray, tails: List[bytes], code_len: np.ndarray, rank: int) -> ShardPlan:
+    per = hists.astype(np.uint64) @ np.asarray(code_len, np.uint64)
+    before = b"".join(tails[:rank])
+    return ShardPlan(hists=hists, weights=hists.sum(axis=0, dtype=np.uint64), bit_base=int(per[:rank].sum()),
+                     bits=int(per[rank]), per_rank_bits=per, prev_tail=before[-8:])
+
+
+def owned_bytes(local: np.ndarray, bit_base: int, bits: int, is_last: bool) -> np.ndarray:
+    """the bytes of the global stream this rank contributes: its local stream
+    starts at global byte bit_base//8; the partial final byte belongs to the
+    next rank (which completes it), except on the last rank"""
+    end = bit_base % 8 + bits
+    keep = (end + 7) // 8 if is_last else end // 8
+    return local[:keep]
+
+
+def encode_shard_plan(job, shard_tail: bytes, rank: int, device=None, group=None, tree_from_weights=None):
+    """steps 1-4: hist, exchange, tree, offsets. Returns (tree, plan)."""
+    if tree_from_weights is None:
+        from . import ByteWeights, HuffTree
+
+        def tree_from_weights(w):
+            return HuffTree.from_weights(ByteWeights.from_array(w))
+    w = job.hist()
+    hists, tails = exchange(w, shard_tail, device=device, group=group)
+    tree = tree_from_weights(hists.sum(axis=0, dtype=np.uint64))
+    _, ln = tree.code_table()
+    return tree, plan(hists, tails, ln, rank)
