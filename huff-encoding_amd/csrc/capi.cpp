@@ -65,6 +65,9 @@ int huff_ctx_create(int device, huff_ctx** out) {
             return st;
         }
         c->stream = c->own;
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
+            c->cu_count = cus;
         *out = c;
         return huff::Status::ok();
     });

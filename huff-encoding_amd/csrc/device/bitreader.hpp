@@ -12,6 +12,13 @@
 
 namespace huff::dev {
 
+// wave-level LDS ordering: every lane's LDS ops issued before this point are
+// visible to every lane of the wave after it (no workgroup barrier needed)
+__device__ __forceinline__ void wave_sync() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+}
+
 struct BitSrc {
     const uint32_t* w;
     const uint8_t* b;

@@ -25,6 +25,8 @@ constexpr uint32_t kLongMaxLen = 57;    // u64 table entries: code << 6 | len
 constexpr uint32_t kHistCopies = 8;     // XCD-group copies of the global weights
 constexpr uint32_t kLutMaxBits = 12;    // primary decode table index bits
 constexpr uint32_t kLutPtr = 0x80000000u;
+constexpr uint32_t kPackWaveRound = 1024;  // bytes per wave round in pack (64 lanes x 16 B)
+
 
 struct PackArgs {
     const uint8_t* in;
@@ -36,7 +38,8 @@ struct PackArgs {
     uint32_t* sub_bit;            // may be null
     const uint8_t* prev_tail;     // 8 bytes, right-aligned (prev_tail[7] precedes in[0])
     uint32_t prev_tail_len;
-    uint32_t stage_words;
+    uint32_t stage_words;         // per wave
+    uint32_t grid;                // persistent workgroups (4 waves each)
 };
 
 struct DecodeArgs {
@@ -48,6 +51,7 @@ struct DecodeArgs {
     const uint64_t* chunk_start;  // [nchunks + 1]
     const uint32_t* sub_bit;      // [ceil(n / kSub)]
     uint32_t nchunks;
+    uint32_t max_len;             // longest code (> 32: window slow path)
     uint64_t n;
     uint8_t* out;
 };

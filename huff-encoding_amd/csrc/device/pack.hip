@@ -2,34 +2,38 @@
 // (huff_coding/src/comp.rs:419-451: per letter, look the code up and append
 // its bits MSB-first to the output bytes).
 //
-// One workgroup encodes one 64 KiB chunk whose first output bit is known
-// (chunk_start, an exclusive scan of per-chunk bit counts). It walks the chunk
-// in rounds of 4 KiB (256 lanes x 16 bytes):
-//   1. 16 table lookups per lane from an LDS code table replicated 32x as
-//      [letter][copy] (lane l reads copy l % 32: conflict-free for any data);
-//   2. a workgroup exclusive scan of the lanes' bit counts;
-//   3. each lane appends its codes into a 64-bit accumulator and emits 32-bit
-//      big-endian words into an LDS staging image of the output: words wholly
-//      its own with ds_write, the first/last (shared with a neighbour lane)
-//      with ds_or;
-//   4. complete 16-byte segments go to HBM with one dwordx4 store per lane
+// Work unit: one 64 KiB chunk per WAVE, whose first output bit is known
+// (chunk_start = exclusive scan of per-chunk bit counts). Workgroups are
+// persistent (4 waves, grid sized to residency) so the code table is copied
+// into LDS once per workgroup; each wave then walks its chunks in rounds of
+// 1 KiB (64 lanes x 16 bytes) with no workgroup barrier:
+//   1. 16 lookups per lane in the LDS code table, replicated 32x as
+//      [letter][copy] (lane l reads copy l % 32: bank-conflict-free on any
+//      data);
+//   2. a wave-wide exclusive scan of the lanes' bit counts (DPP shuffles);
+//   3. each lane appends its codes to a 64-bit accumulator and emits 32-bit
+//      big-endian words into the wave's LDS staging image of the output: words
+//      wholly its own with ds_write, the two it shares with neighbours ds_or;
+//   4. complete 16-byte segments leave as one dwordx4 store per lane
 //      (byte-swapped: the stream is MSB-first); the partial last segment is
 //      carried to the next round.
-// The first output byte of a chunk is shared with the previous chunk: the
-// workgroup recomputes the previous chunk's last <= 7 bits from the last input
-// bytes before it (or from prev_tail for the first chunk of a shard), so every
-// output byte is written by exactly one workgroup and no fix-up pass or global
-// atomic is needed. Chunk c owns bytes [cs/8, ce/8) (the last chunk through
-// ceil(ce/8), zero-padded like comp.rs:446-447).
+// Loads run 3 rounds (3 KiB per wave) ahead of the encoder.
+// A chunk's first output byte is shared with the previous chunk: the wave
+// recomputes the previous chunk's last <= 7 bits from the input bytes before
+// it (from prev_tail for the first chunk of a shard), so every output byte is
+// written by exactly one wave: no fix-up pass and no global atomics. Chunk c
+// owns bytes [cs/8, ce/8) (the last chunk through ceil(ce/8), zero-padded as
+// comp.rs:446-447 pads).
 //
 // Roofline: HBM-bound; algorithmic traffic n (read) + ceil(bits/8) (write).
-#include "kernels.hpp"
+#include "bitreader.hpp"
 
 namespace huff::dev {
 
 namespace {
 
 constexpr int kThreads = 256;
+constexpr int kWaves = kThreads / 64;
 
 template <bool LONG>
 struct Entry;
@@ -48,8 +52,6 @@ struct Entry<true> {
     static constexpr uint32_t kTableWords = 256 * 32 * 2;
 };
 
-__device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
-
 template <bool LONG>
 __device__ __forceinline__ void emit_codes(uint32_t* __restrict__ stage, uint64_t p,
                                            const typename Entry<LONG>::T (&ent)[16]) {
@@ -60,7 +62,7 @@ __device__ __forceinline__ void emit_codes(uint32_t* __restrict__ stage, uint64_
     uint64_t acc = 0;
     auto flush = [&]() {
         if (nacc >= 32) {
-            uint32_t word = static_cast<uint32_t>(acc >> (nacc - 32));
+            const uint32_t word = static_cast<uint32_t>(acc >> (nacc - 32));
             if (shared_first) {
                 __hip_atomic_fetch_or(&stage[w], word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 shared_first = false;
@@ -90,7 +92,7 @@ __device__ __forceinline__ void emit_codes(uint32_t* __restrict__ stage, uint64_
         }
     }
     if (nacc) {
-        uint32_t word = static_cast<uint32_t>(acc << (32 - nacc));
+        const uint32_t word = static_cast<uint32_t>(acc << (32 - nacc));
         __hip_atomic_fetch_or(&stage[w], word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
 }
@@ -98,10 +100,10 @@ __device__ __forceinline__ void emit_codes(uint32_t* __restrict__ stage, uint64_
 __device__ __forceinline__ void store_segment(const uint32_t* __restrict__ stage, uint32_t s, uint64_t gbyte,
                                               uint64_t own_lo, uint64_t own_hi, uint8_t* __restrict__ out) {
     uint4 v;
-    v.x = bswap32(stage[4 * s + 0]);
-    v.y = bswap32(stage[4 * s + 1]);
-    v.z = bswap32(stage[4 * s + 2]);
-    v.w = bswap32(stage[4 * s + 3]);
+    v.x = __builtin_bswap32(stage[4 * s + 0]);
+    v.y = __builtin_bswap32(stage[4 * s + 1]);
+    v.z = __builtin_bswap32(stage[4 * s + 2]);
+    v.w = __builtin_bswap32(stage[4 * s + 3]);
     if (gbyte >= own_lo && gbyte + 16 <= own_hi) {
         *reinterpret_cast<uint4*>(out + gbyte) = v;
         return;
@@ -117,8 +119,7 @@ __device__ __forceinline__ void store_segment(const uint32_t* __restrict__ stage
 __device__ __forceinline__ uint4 load_lane(const uint8_t* __restrict__ in, uint64_t n, uint64_t g) {
     if (g + 16 <= n) return *reinterpret_cast<const uint4*>(in + g);
     uint32_t w[4] = {0, 0, 0, 0};
-    for (int i = 0; i < 16; ++i)
-        if (g + i < n) w[i >> 2] |= static_cast<uint32_t>(in[g + i]) << (8 * (i & 3));
+    for (int i = 0; g + i < n && i < 16; ++i) w[i >> 2] |= static_cast<uint32_t>(in[g + i]) << (8 * (i & 3));
     return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
@@ -128,10 +129,8 @@ __global__ __launch_bounds__(kThreads) void k_pack(PackArgs a) {
     using T = typename E::T;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     T* tab = reinterpret_cast<T*>(lds);
-    uint32_t* stage = lds + E::kTableWords;
-    uint32_t* scratch = stage + a.stage_words;
-
     const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6, copy = t & 31;
+    uint32_t* stage = lds + E::kTableWords + wave * a.stage_words;
 
     // replicate the table: thread t writes copy t%32 of letters t/32 + 8i
     const T* tg = reinterpret_cast<const T*>(a.table);
@@ -140,108 +139,110 @@ __global__ __launch_bounds__(kThreads) void k_pack(PackArgs a) {
         const uint32_t e = (t >> 5) + 8 * i;
         tab[(e << 5) | copy] = tg[e];
     }
-    for (uint32_t i = t; i < a.stage_words; i += kThreads) stage[i] = 0;
-
-    const uint32_t c = blockIdx.x;
-    const uint64_t sym0 = static_cast<uint64_t>(c) * kChunk;
-    const uint64_t nsym = (a.n - sym0 < kChunk) ? a.n - sym0 : kChunk;
-    const uint64_t cs = a.chunk_start[c];
-    const uint64_t ce = a.chunk_start[c + 1];
-    uint64_t stage_bit0 = (cs >> 7) << 7;  // global bit of stage word 0's MSB (16-B aligned)
-    const uint64_t own_lo = cs >> 3;
-    const uint64_t own_hi = (c + 1 == a.nchunks) ? (ce + 7) >> 3 : ce >> 3;
+    for (uint32_t i = lane; i < a.stage_words; i += 64) stage[i] = 0;
     __syncthreads();
 
-    // bits of the shared first byte that belong to the symbols before this chunk
-    if (t == 0 && (cs & 7)) {
-        const int64_t floor8 = static_cast<int64_t>(cs & ~7ull);
-        int64_t pos = static_cast<int64_t>(cs);
-        for (uint32_t k = 1; k <= 8 && pos > floor8; ++k) {
-            uint8_t b;
-            if (sym0 >= k) {
-                b = a.in[sym0 - k];
-            } else {
-                const uint32_t j = k - static_cast<uint32_t>(sym0);
-                if (j > a.prev_tail_len) break;
-                b = a.prev_tail[8 - j];
-            }
-            const T ent = tab[static_cast<uint32_t>(b) << 5];
-            const int64_t len = static_cast<int64_t>(ent & E::kMask);
-            const uint64_t code = static_cast<uint64_t>(ent >> E::kShift);
-            if (len == 0) break;
-            const int64_t start = pos - len;  // may precede bit 0 of out (a shard's first byte)
-            for (int64_t q = (start > floor8 ? start : floor8); q < pos; ++q) {
-                if ((code >> (pos - 1 - q)) & 1) {
-                    const uint64_t sb = static_cast<uint64_t>(q) - stage_bit0;
-                    stage[sb >> 5] |= 0x80000000u >> (sb & 31);
+    for (uint32_t c = blockIdx.x * kWaves + wave; c < a.nchunks; c += a.grid * kWaves) {
+        const uint64_t sym0 = static_cast<uint64_t>(c) * kChunk;
+        const uint64_t nsym = (a.n - sym0 < kChunk) ? a.n - sym0 : kChunk;
+        const uint64_t cs = a.chunk_start[c];
+        const uint64_t ce = a.chunk_start[c + 1];
+        uint64_t stage_bit0 = (cs >> 7) << 7;  // global bit of stage word 0's MSB (16-B aligned)
+        const uint64_t own_lo = cs >> 3;
+        const uint64_t own_hi = (c + 1 == a.nchunks) ? (ce + 7) >> 3 : ce >> 3;
+        const uint32_t nrounds = static_cast<uint32_t>((nsym + kPackWaveRound - 1) / kPackWaveRound);
+        const uint8_t* cin = a.in + sym0;
+        const uint64_t cn = nsym;
+
+        // loads run 3 rounds ahead
+        uint4 v0 = load_lane(cin, cn, lane * 16);
+        uint4 v1 = nrounds > 1 ? load_lane(cin, cn, 1 * kPackWaveRound + lane * 16) : make_uint4(0, 0, 0, 0);
+        uint4 v2 = nrounds > 2 ? load_lane(cin, cn, 2 * kPackWaveRound + lane * 16) : make_uint4(0, 0, 0, 0);
+
+        // bits of the shared first byte that belong to the symbols before this chunk
+        if (lane == 0 && (cs & 7)) {
+            const int64_t floor8 = static_cast<int64_t>(cs & ~7ull);
+            int64_t pos = static_cast<int64_t>(cs);
+            for (uint32_t k = 1; k <= 8 && pos > floor8; ++k) {
+                uint8_t b;
+                if (sym0 >= k) {
+                    b = a.in[sym0 - k];
+                } else {
+                    const uint32_t j = k - static_cast<uint32_t>(sym0);
+                    if (j > a.prev_tail_len) break;
+                    b = a.prev_tail[8 - j];
                 }
+                const T ent = tab[static_cast<uint32_t>(b) << 5];
+                const int64_t len = static_cast<int64_t>(ent & E::kMask);
+                const uint64_t code = static_cast<uint64_t>(ent >> E::kShift);
+                if (len == 0) break;
+                const int64_t start = pos - len;  // may precede bit 0 of out (a shard's first byte)
+                for (int64_t q = (start > floor8 ? start : floor8); q < pos; ++q) {
+                    if ((code >> (pos - 1 - q)) & 1) {
+                        const uint64_t sb = static_cast<uint64_t>(q) - stage_bit0;
+                        stage[sb >> 5] |= 0x80000000u >> (sb & 31);
+                    }
+                }
+                pos = start;
             }
-            pos = start;
         }
-    }
-    __syncthreads();
+        wave_sync();
 
-    const uint32_t nrounds = static_cast<uint32_t>((nsym + kRound - 1) / kRound);
-    uint64_t round_bit = cs;
-    uint4 v_next = load_lane(a.in, a.n, sym0 + t * 16);
-    for (uint32_t r = 0; r < nrounds; ++r) {
-        const uint4 v = v_next;
-        if (r + 1 < nrounds) v_next = load_lane(a.in, a.n, sym0 + static_cast<uint64_t>(r + 1) * kRound + t * 16);
-        const uint64_t s_in_chunk = static_cast<uint64_t>(r) * kRound + t * 16;
-        const int nvalid = s_in_chunk >= nsym ? 0 : (nsym - s_in_chunk >= 16 ? 16 : static_cast<int>(nsym - s_in_chunk));
+        uint64_t round_bit = cs;
+        for (uint32_t r = 0; r < nrounds; ++r) {
+            const uint4 v = v0;
+            v0 = v1;
+            v1 = v2;
+            if (r + 3 < nrounds) v2 = load_lane(cin, cn, static_cast<uint64_t>(r + 3) * kPackWaveRound + lane * 16);
+            const uint64_t s_in_chunk = static_cast<uint64_t>(r) * kPackWaveRound + lane * 16;
+            const int nvalid = s_in_chunk >= nsym ? 0 : (nsym - s_in_chunk >= 16 ? 16 : static_cast<int>(nsym - s_in_chunk));
 
-        T ent[16];
-        uint32_t bits = 0;
-        const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+            T ent[16];
+            uint32_t bits = 0;
+            const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            const uint32_t b = (wv[k >> 2] >> (8 * (k & 3))) & 0xFFu;
-            const T e = tab[(b << 5) | copy];
-            ent[k] = (k < nvalid) ? e : T(0);
-            bits += static_cast<uint32_t>(ent[k] & E::kMask);
-        }
-
-        // workgroup exclusive scan of bits
-        uint32_t incl = bits;
+            for (int k = 0; k < 16; ++k) {
+                const uint32_t b = (wv[k >> 2] >> (8 * (k & 3))) & 0xFFu;
+                const T e = tab[(b << 5) | copy];
+                ent[k] = (k < nvalid) ? e : T(0);
+                bits += static_cast<uint32_t>(ent[k] & E::kMask);
+            }
+            // wave exclusive scan of the bit counts
+            uint32_t incl = bits;
 #pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t y = __shfl_up(incl, d, 64);
-            if (lane >= static_cast<uint32_t>(d)) incl += y;
-        }
-        if (lane == 63) scratch[wave] = incl;
-        __syncthreads();
-        uint32_t pre = 0, tot = 0;
-#pragma unroll
-        for (uint32_t w = 0; w < 4; ++w) {
-            const uint32_t x = scratch[w];
-            pre += (w < wave) ? x : 0u;
-            tot += x;
-        }
-        const uint32_t excl = pre + incl - bits;
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint32_t y = __shfl_up(incl, d, 64);
+                if (lane >= static_cast<uint32_t>(d)) incl += y;
+            }
+            const uint32_t tot = __shfl(incl, 63, 64);
+            const uint32_t excl = incl - bits;
 
-        if (a.sub_bit && nvalid > 0 && (s_in_chunk & (kSub - 1)) == 0)
-            a.sub_bit[(sym0 + s_in_chunk) / kSub] = static_cast<uint32_t>(round_bit - cs + excl);
+            if (a.sub_bit && nvalid > 0 && (s_in_chunk & (kSub - 1)) == 0)
+                a.sub_bit[(sym0 + s_in_chunk) / kSub] = static_cast<uint32_t>(round_bit - cs + excl);
 
-        if (bits) emit_codes<LONG>(stage, round_bit - stage_bit0 + excl, ent);
-        __syncthreads();
+            if (bits) emit_codes<LONG>(stage, round_bit - stage_bit0 + excl, ent);
+            wave_sync();
 
-        const uint64_t end_bit = round_bit + tot;
-        const bool last = (r + 1 == nrounds);
-        const uint32_t nseg_done = static_cast<uint32_t>((end_bit - stage_bit0) >> 7);
-        const uint32_t nseg_store = last ? static_cast<uint32_t>((end_bit - stage_bit0 + 127) >> 7) : nseg_done;
-        for (uint32_t s = t; s < nseg_store; s += kThreads)
-            store_segment(stage, s, (stage_bit0 >> 3) + 16ull * s, own_lo, own_hi, a.out);
-        if (!last) {
+            const uint64_t end_bit = round_bit + tot;
+            const bool last = (r + 1 == nrounds);
+            const uint32_t nseg_done = static_cast<uint32_t>((end_bit - stage_bit0) >> 7);
+            const uint32_t nseg_store = last ? static_cast<uint32_t>((end_bit - stage_bit0 + 127) >> 7) : nseg_done;
+            for (uint32_t s = lane; s < nseg_store; s += 64)
+                store_segment(stage, s, (stage_bit0 >> 3) + 16ull * s, own_lo, own_hi, a.out);
             const uint32_t used_words = static_cast<uint32_t>((end_bit - stage_bit0 + 31) >> 5);
             uint32_t keep = 0;
-            if (t < 4) keep = stage[nseg_done * 4 + t];
-            __syncthreads();
-            for (uint32_t i = 4 + t; i < used_words; i += kThreads) stage[i] = 0;
-            if (t < 4) stage[t] = keep;
-            stage_bit0 += static_cast<uint64_t>(nseg_done) << 7;
-            __syncthreads();
+            if (!last && lane < 4) keep = stage[nseg_done * 4 + lane];
+            wave_sync();
+            // clear what this round wrote; carry the partial segment to the front
+            for (uint32_t i = lane; i < used_words; i += 64) stage[i] = 0;
+            wave_sync();
+            if (!last) {
+                if (lane < 4) stage[lane] = keep;
+                stage_bit0 += static_cast<uint64_t>(nseg_done) << 7;
+                wave_sync();
+            }
+            round_bit = end_bit;
         }
-        round_bit = end_bit;
     }
 }
 
@@ -249,16 +250,16 @@ __global__ __launch_bounds__(kThreads) void k_pack(PackArgs a) {
 
 size_t pack_lds_bytes(bool long_codes, uint32_t stage_words) {
     const uint32_t table = long_codes ? Entry<true>::kTableWords : Entry<false>::kTableWords;
-    return static_cast<size_t>(table + stage_words + 16) * 4;
+    return static_cast<size_t>(table + kWaves * stage_words) * 4;
 }
 
 hipError_t launch_pack(bool long_codes, const PackArgs& a, hipStream_t s) {
     if (a.nchunks == 0) return hipSuccess;
     const size_t lds = pack_lds_bytes(long_codes, a.stage_words);
     if (long_codes) {
-        hipLaunchKernelGGL(k_pack<true>, dim3(a.nchunks), dim3(kThreads), lds, s, a);
+        hipLaunchKernelGGL(k_pack<true>, dim3(a.grid), dim3(kThreads), lds, s, a);
     } else {
-        hipLaunchKernelGGL(k_pack<false>, dim3(a.nchunks), dim3(kThreads), lds, s, a);
+        hipLaunchKernelGGL(k_pack<false>, dim3(a.grid), dim3(kThreads), lds, s, a);
     }
     return hipGetLastError();
 }

@@ -340,7 +340,11 @@ huff::Status huff_enc::pack(const huff_tree* t, uint64_t base, const uint8_t* pr
     a.sub_bit = static_cast<uint32_t*>(sub_bit.p);
     a.prev_tail = d_tab + 2304;
     a.prev_tail_len = static_cast<uint32_t>(prev_tail_len);
-    a.stage_words = (128 * std::max<uint32_t>(et.maxlen, 1) + 16 + 3) & ~3u;
+    // one wave round is 1 KiB: <= 1024*maxlen bits + a < 128-bit carry
+    a.stage_words = (32 * std::max<uint32_t>(et.maxlen, 1) + 8 + 3) & ~3u;
+    const size_t lds = huff::dev::pack_lds_bytes(ctx->tab_long, a.stage_words);
+    const uint32_t per_cu = std::max<uint32_t>(1, std::min<uint32_t>(8, static_cast<uint32_t>((160 * 1024) / lds)));
+    a.grid = std::max<uint32_t>(1, std::min<uint32_t>((nchunks + 3) / 4, ctx->cu_count * per_cu));
     HUFF_TRY(ctx->timed("pack", [&] { return huff::dev::launch_pack(ctx->tab_long, a, s); }));
     packed = true;
     packed_tree_id = t->id;
@@ -365,6 +369,7 @@ huff::Status huff_enc::decode(const huff_tree* t, const uint8_t* d_comp, uint64_
     a.chunk_start = static_cast<const uint64_t*>(chunk_start.p);
     a.sub_bit = static_cast<const uint32_t*>(sub_bit.p);
     a.nchunks = nchunks;
+    a.max_len = dt->maxdepth;
     a.n = n;
     a.out = d_out;
     HUFF_TRY(ctx->timed("decode", [&] { return huff::dev::launch_decode(a, ctx->stream); }));

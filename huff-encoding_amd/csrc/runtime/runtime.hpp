@@ -92,6 +92,7 @@ struct DevBuf {
 
 struct huff_ctx {
     int device = 0;
+    int cu_count = 256;
     hipStream_t own = nullptr;
     hipStream_t stream = nullptr;
     PinnedBuf pin_w;     // weights readback
