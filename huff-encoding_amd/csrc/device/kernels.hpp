@@ -52,6 +52,7 @@ struct DecodeArgs {
     const uint32_t* sub_bit;      // [ceil(n / kSub)]
     uint32_t nchunks;
     uint32_t max_len;             // longest code (> 32: window slow path)
+    uint32_t lut_rep_log2;        // primary table copies in LDS (bank spread)
     uint64_t n;
     uint8_t* out;
 };
@@ -70,7 +71,7 @@ struct IndexlessArgs {
 };
 
 size_t pack_lds_bytes(bool long_codes, uint32_t stage_words);
-size_t decode_lds_bytes(uint32_t lut_bits);
+size_t decode_lds_bytes(uint32_t lut_bits, uint32_t rep_log2);
 
 hipError_t launch_hist(const uint8_t* base, uint64_t lo, uint64_t hi, uint32_t nchunks, uint32_t* chunk_hist,
                        unsigned long long* gw, hipStream_t s);

@@ -4,6 +4,7 @@
 #include <algorithm>
 #include <cctype>
 #include <numeric>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 
@@ -370,6 +371,13 @@ huff::Status huff_enc::decode(const huff_tree* t, const uint8_t* d_comp, uint64_
     a.sub_bit = static_cast<const uint32_t*>(sub_bit.p);
     a.nchunks = nchunks;
     a.max_len = dt->maxdepth;
+    // replicate the primary table up to 4 KiB of LDS (fewer bank conflicts,
+    // occupancy kept); HUFF_DEC_LUT_REP_LOG2 overrides for experiments
+    {
+        int rep = std::max(0, std::min(5, 10 - static_cast<int>(dt->bits)));
+        if (const char* env = std::getenv("HUFF_DEC_LUT_REP_LOG2")) rep = std::max(0, std::min(5, std::atoi(env)));
+        a.lut_rep_log2 = static_cast<uint32_t>(rep);
+    }
     a.n = n;
     a.out = d_out;
     HUFF_TRY(ctx->timed("decode", [&] { return huff::dev::launch_decode(a, ctx->stream); }));

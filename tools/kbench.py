@@ -1,0 +1,74 @@
+#!/usr/bin/env python3
+"""Kernel microbenchmark for profiling: repeat one phase of the hot path.
+
+    python tools/kbench.py --phase pack --workload zipf --iters 20
+
+phase: hist | pack | decode | all. Inputs are generated on the device once;
+the selected phase is launched `iters` times back to back so rocprofv3
+(--kernel-trace / --pmc) sees many identical dispatches.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "huff-encoding_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import huff_coding as H  # noqa: E402
+from huff_coding import device as D  # noqa: E402
+
+SEEDS = {"uniform": 0x5EED0001, "zipf": 0x5EED0002, "text": 0x5EED0005}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--phase", default="all", choices=["hist", "pack", "decode", "all"])
+    ap.add_argument("--workload", default="uniform", choices=sorted(SEEDS))
+    ap.add_argument("--bytes", type=int, default=1 << 30)
+    ap.add_argument("--iters", type=int, default=20)
+    args = ap.parse_args()
+    torch.cuda.set_device(0)
+    ctx = H.Context(0)
+    ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    n = args.bytes
+    x = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
+    D.generate(ctx, args.workload, SEEDS[args.workload], x.data_ptr(), n,
+               cdf=D.zipf_cdf(1.2) if args.workload == "zipf" else None)
+    job = H.EncodeJob(ctx, x.data_ptr(), n)
+    w = job.hist()
+    tree = H.HuffTree.from_weights(H.ByteWeights.from_array(w))
+    bits = job.bits(tree)
+    out = torch.empty((bits + 7) // 8 + 64, dtype=torch.uint8, device="cuda")
+    dec = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
+    job.pack(tree, out.data_ptr(), out.numel())
+    job.decode(tree, out.data_ptr(), dec.data_ptr())
+    torch.cuda.synchronize()
+    assert torch.equal(dec[:n], x[:n])
+    ctx.set_timing(True)
+    ctx.reset_timing()
+    t0 = time.perf_counter()
+    for _ in range(args.iters):
+        if args.phase in ("hist", "all"):
+            job.hist()
+        if args.phase in ("pack", "all"):
+            job.pack(tree, out.data_ptr(), out.numel())
+        if args.phase in ("decode", "all"):
+            job.decode(tree, out.data_ptr(), dec.data_ptr())
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    res = {"phase": args.phase, "workload": args.workload, "n": n, "comp_bytes": (bits + 7) // 8,
+           "iters": args.iters, "wall_ms_per_iter": el * 1e3 / args.iters}
+    for k in ("hist", "chunk_bits", "scan", "pack", "decode"):
+        ms, c = ctx.kernel_time(k)
+        if c:
+            res[k + "_ms"] = ms / c
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
