@@ -138,6 +138,7 @@ def main():
         out = state["out"]
         job.pack(tree, out.data_ptr(), state["cap"], bit_base=base, prev_tail=tail)
         job.decode(tree, out.data_ptr(), dec.data_ptr())
+        state["fixed8"] = bool((ln[total > 0] == 8).all()) and os.environ.get("HUFF_DISABLE_FIXED8", "0") in ("", "0")
         return bits, tree
 
     for _ in range(args.warmup):
@@ -200,6 +201,7 @@ def main():
         "data": "synthetic (counter-based generator on device; see DESIGN.md)",
         "config": {"workload": WORKLOADS[kind], "bytes_per_gpu": n, "global_bytes": n * world,
                    "compressed_bytes_per_gpu": comp_bytes, "bits_per_byte": round(bits / n, 4),
+                   "kernel_path": "fixed8 byte map (all codes 8 bits)" if state.get("fixed8") else "general bit pack/decode",
                    "parallelism": f"shard{world}", "collective": "all_gather u64[257] over RCCL" if world > 1 else None},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": ach, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": None},

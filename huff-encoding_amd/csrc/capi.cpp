@@ -58,7 +58,9 @@ int huff_ctx_create(int device, huff_ctx** out) {
         auto* c = new huff_ctx();
         c->device = device;
         huff::Status st = c->activate();
-        if (!st && hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess)
+        // a blocking stream: ordered after work on the legacy default stream
+        // (where PyTorch allocates and fills tensors unless told otherwise)
+        if (!st && hipStreamCreateWithFlags(&c->own, hipStreamDefault) != hipSuccess)
             st = huff::Status::err(HUFF_E_HIP, "hipStreamCreate failed");
         if (st) {
             delete c;

@@ -19,6 +19,14 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_wave_barrier();
 }
 
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+
+// 16-byte streaming load that does not pollute the caches
+__device__ __forceinline__ uint4 ld_nt(const uint4* p) {
+    const u32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+
 struct BitSrc {
     const uint32_t* w;
     const uint8_t* b;

@@ -1,0 +1,90 @@
+// bytemap.hip — fixed-length fast path.
+//
+// When every code of the tree is exactly 8 bits (the reference's tree for
+// near-uniform byte frequencies: 256 equal-ish weights always merge leaf
+// pairs first, tree_inner.rs:289-303, giving a complete depth-8 tree), the
+// byte-aligned stream of compress_with_tree (comp.rs:424-444) is a byte-for-
+// byte substitution: out[i] = code[in[i]], and decode is the inverse map.
+// One streaming kernel does both: 16-byte coalesced loads, a 256-entry LDS
+// table replicated 32x ([byte][copy], lane l reads copy l % 32: no bank
+// conflicts), 16-byte stores. It also writes the restart index, which for
+// 8-bit codes is arithmetic (symbol s starts at bit 8 s).
+//
+// Roofline: HBM-bound, n bytes read + n bytes written.
+#include "bitreader.hpp"
+
+namespace huff::dev {
+
+namespace {
+
+constexpr int kThreads = 256;
+
+__device__ __forceinline__ uint32_t map4(const uint32_t* tab, uint32_t w, uint32_t copy) {
+    const uint32_t b0 = tab[((w & 0xFFu) << 5) | copy];
+    const uint32_t b1 = tab[(((w >> 8) & 0xFFu) << 5) | copy];
+    const uint32_t b2 = tab[(((w >> 16) & 0xFFu) << 5) | copy];
+    const uint32_t b3 = tab[((w >> 24) << 5) | copy];
+    return b0 | (b1 << 8) | (b2 << 16) | (b3 << 24);
+}
+
+__global__ __launch_bounds__(kThreads) void k_bytemap(BytemapArgs a) {
+    __shared__ __attribute__((aligned(16))) uint32_t tab[256 * 32];
+    const uint32_t t = threadIdx.x, copy = t & 31;
+#pragma unroll 4
+    for (int i = 0; i < 32; ++i) {
+        const uint32_t e = (t >> 5) + 8 * i;
+        tab[(e << 5) | copy] = (a.table[e] >> a.shift) & 0xFFu;
+    }
+    __syncthreads();
+    const uint64_t gid = static_cast<uint64_t>(blockIdx.x) * kThreads + t;
+    const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kThreads;
+    const uint64_t nvec = a.n / 16;
+    const uint4* src = reinterpret_cast<const uint4*>(a.src);
+    uint4* dst = reinterpret_cast<uint4*>(a.dst);
+    uint64_t v = gid;
+    for (; v + 3 * stride < nvec; v += 4 * stride) {
+        uint4 x[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) x[k] = ld_nt(src + v + k * stride);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            uint4 y;
+            y.x = map4(tab, x[k].x, copy);
+            y.y = map4(tab, x[k].y, copy);
+            y.z = map4(tab, x[k].z, copy);
+            y.w = map4(tab, x[k].w, copy);
+            dst[v + k * stride] = y;
+        }
+    }
+    for (; v < nvec; v += stride) {
+        const uint4 x = src[v];
+        uint4 y;
+        y.x = map4(tab, x.x, copy);
+        y.y = map4(tab, x.y, copy);
+        y.z = map4(tab, x.z, copy);
+        y.w = map4(tab, x.w, copy);
+        dst[v] = y;
+    }
+    for (uint64_t i = nvec * 16 + gid; i < a.n; i += stride) a.dst[i] = static_cast<uint8_t>(tab[(a.src[i] << 5) | copy]);
+    // restart index of an 8-bit-per-symbol stream
+    if (a.chunk_start)
+        for (uint64_t c = gid; c <= a.nchunks; c += stride) a.chunk_start[c] = a.base_bits + c * kChunk * 8;
+    if (a.sub_bit) {
+        const uint64_t nsub = (a.n + kSub - 1) / kSub;
+        for (uint64_t g = gid; g < nsub; g += stride) a.sub_bit[g] = static_cast<uint32_t>(((g * kSub) % kChunk) * 8);
+    }
+}
+
+}  // namespace
+
+hipError_t launch_bytemap(const BytemapArgs& a, hipStream_t s) {
+    if (a.n == 0 && !a.chunk_start) return hipSuccess;
+    const uint64_t nvec = a.n / 16;
+    uint64_t blocks = (nvec + kThreads * 4 - 1) / (kThreads * 4);
+    if (blocks < 1) blocks = 1;
+    const uint32_t grid = static_cast<uint32_t>(blocks < 2048 ? blocks : 2048);
+    hipLaunchKernelGGL(k_bytemap, dim3(grid), dim3(kThreads), 0, s, a);
+    return hipGetLastError();
+}
+
+}  // namespace huff::dev

@@ -129,29 +129,35 @@ __global__ __launch_bounds__(256) void k_chunk_bits(const uint32_t* __restrict__
 // start[c] = base + sum_{c' < c} bits[c'], start[nchunks] = total end.
 __global__ __launch_bounds__(1024) void k_scan(const uint64_t* __restrict__ bits, uint32_t nchunks, uint64_t base,
                                                uint64_t* __restrict__ start) {
-    __shared__ uint64_t wsum[16];
+    // tiles of 1024 in index order; the next tile's values are loaded while
+    // the current one is scanned
+    __shared__ uint64_t wsum[2][16];
     const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
-    const uint32_t per = (nchunks + 1023) / 1024;
-    const uint32_t b = t * per, e = min(nchunks, b + per);
-    uint64_t local = 0;
-    for (uint32_t i = b; i < e; ++i) local += bits[i];
-    uint64_t incl = local;
+    uint64_t carry = base;
+    uint64_t v_next = t < nchunks ? bits[t] : 0;
+    for (uint32_t tile = 0, k = 0; tile < nchunks; tile += 1024, k ^= 1) {
+        const uint64_t v = v_next;
+        const uint32_t i = tile + t;
+        v_next = (i + 1024 < nchunks) ? bits[i + 1024] : 0;
+        uint64_t incl = v;
 #pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        uint64_t y = __shfl_up(incl, d, 64);
-        if (lane >= static_cast<uint32_t>(d)) incl += y;
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint64_t y = __shfl_up(incl, d, 64);
+            if (lane >= static_cast<uint32_t>(d)) incl += y;
+        }
+        if (lane == 63) wsum[k][wave] = incl;
+        __syncthreads();
+        uint64_t pre = carry, tot = 0;
+#pragma unroll
+        for (uint32_t w = 0; w < 16; ++w) {
+            const uint64_t x = wsum[k][w];
+            pre += (w < wave) ? x : 0;
+            tot += x;
+        }
+        if (i < nchunks) start[i] = pre + incl - v;
+        carry += tot;  // wsum[k] is rewritten only two tiles later, after a barrier
     }
-    if (lane == 63) wsum[wave] = incl;
-    __syncthreads();
-    uint64_t pre = base;
-    for (uint32_t w = 0; w < wave; ++w) pre += wsum[w];
-    uint64_t run = pre + incl - local;
-    for (uint32_t i = b; i < e; ++i) {
-        start[i] = run;
-        run += bits[i];
-    }
-    if (t == 1023) start[nchunks] = run;
-    // (when nchunks < 1024, the last thread has an empty range and run is the total)
+    if (t == 0) start[nchunks] = carry;
 }
 
 // lowest index i with missing_mask[in[i]] != 0 (error path of compress_with_tree)

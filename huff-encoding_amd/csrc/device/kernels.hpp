@@ -70,6 +70,19 @@ struct IndexlessArgs {
     uint64_t* c;                  // [nseg] symbol counts
 };
 
+// dst[i] = (table[src[i]] >> shift) & 0xFF (+ arithmetic restart index)
+struct BytemapArgs {
+    const uint8_t* src;
+    uint8_t* dst;
+    uint64_t n;
+    const uint32_t* table;        // 256 entries
+    uint32_t shift;
+    uint64_t* chunk_start;        // may be null
+    uint32_t nchunks;
+    uint64_t base_bits;
+    uint32_t* sub_bit;            // may be null
+};
+
 size_t pack_lds_bytes(bool long_codes, uint32_t stage_words);
 size_t decode_lds_bytes(uint32_t lut_bits, uint32_t rep_log2);
 
@@ -85,6 +98,7 @@ hipError_t launch_indexless_fix(const IndexlessArgs& a, const uint64_t* xin, uin
                                 hipStream_t s);
 hipError_t launch_indexless_settle(const IndexlessArgs& a, uint64_t* x, hipStream_t s);
 hipError_t launch_indexless_emit(const IndexlessArgs& a, const uint64_t* off, uint8_t* out, hipStream_t s);
+hipError_t launch_bytemap(const BytemapArgs& a, hipStream_t s);
 hipError_t launch_find_first(const uint8_t* in, uint64_t n, const uint8_t* missing_mask, unsigned long long* pos,
                              hipStream_t s);
 hipError_t launch_generate(int kind, uint64_t seed, uint64_t offset, const uint64_t* cdf, uint8_t* out, uint64_t n,

@@ -46,6 +46,11 @@ huff_compress_data::~huff_compress_data() { delete tree; }
 
 namespace huff {
 
+bool fixed8_disabled() {
+    const char* e = std::getenv("HUFF_DISABLE_FIXED8");  // read per call: tests flip it
+    return e && *e && *e != '0';
+}
+
 Status build_dec_tables(const HuffTree& t, DecTables& out) {
     const auto& nodes = t.nodes();
     out.lut.clear();
@@ -60,6 +65,11 @@ Status build_dec_tables(const HuffTree& t, DecTables& out) {
     if (maxd > dev::kLongMaxLen)
         return Status::err(HUFF_E_CODE_TOO_LONG, "code longer than 57 bits: outside the GPU decoder's range");
     out.maxdepth = maxd;
+    {
+        uint32_t mind = 255;
+        for (const LeafCode& lc : t.leaves()) mind = std::min(mind, lc.len);
+        out.all8 = (mind == 8 && maxd == 8);
+    }
     out.bits = std::min<uint32_t>(maxd, dev::kLutMaxBits - 1);  // 11 bits: 8 KiB of LDS
     if (out.bits < 1) out.bits = 1;
     out.lut.assign(1u << out.bits, 0);
@@ -322,6 +332,29 @@ huff::Status huff_enc::pack(const huff_tree* t, uint64_t base, const uint8_t* pr
     hipStream_t s = ctx->stream;
     HUFF_TRY(ctx->upload_enc_tables(t, prev_tail, prev_tail_len));
     const uint8_t* d_tab = static_cast<const uint8_t*>(ctx->d_tab.p);
+    const huff::EncTables& et = t->enc_tables();
+    if ((base & 7) == 0 && et.maxlen == 8 && !huff::fixed8_disabled()) {
+        bool all8 = true;
+        for (int b = 0; b < 256; ++b) all8 &= (w[b] == 0 || et.len[b] == 8);
+        if (all8) {  // every code 8 bits: byte substitution (bytemap.hip)
+            huff::dev::BytemapArgs m{};
+            m.src = d_in;
+            m.dst = d_out;
+            m.n = n;
+            m.table = reinterpret_cast<const uint32_t*>(d_tab);
+            m.shift = 5;  // short entries are code << 5 | len
+            m.chunk_start = static_cast<uint64_t*>(chunk_start.p);
+            m.nchunks = nchunks;
+            m.base_bits = 0;
+            m.sub_bit = static_cast<uint32_t*>(sub_bit.p);
+            HUFF_TRY(ctx->timed("pack", [&] { return huff::dev::launch_bytemap(m, s); }));
+            packed = true;
+            packed_tree_id = t->id;
+            bit_base = base;
+            total_bits = tb;
+            return huff::Status::ok();
+        }
+    }
     HUFF_TRY(ctx->timed("chunk_bits", [&] {
         return huff::dev::launch_chunk_bits(static_cast<const uint32_t*>(chunk_hist.p), nchunks, d_tab + 2048,
                                             static_cast<uint64_t*>(chunk_bits.p), s);
@@ -330,7 +363,6 @@ huff::Status huff_enc::pack(const huff_tree* t, uint64_t base, const uint8_t* pr
         return huff::dev::launch_scan(static_cast<const uint64_t*>(chunk_bits.p), nchunks, base & 7,
                                       static_cast<uint64_t*>(chunk_start.p), s);
     }));
-    const huff::EncTables& et = t->enc_tables();
     huff::dev::PackArgs a{};
     a.in = d_in;
     a.n = n;
@@ -361,6 +393,16 @@ huff::Status huff_enc::decode(const huff_tree* t, const uint8_t* d_comp, uint64_
     HUFF_TRY(ctx->activate());
     const huff::DecTables* dt = nullptr;
     HUFF_TRY(ctx->upload_dec_tables(t, &dt));
+    if (dt->all8 && (bit_base & 7) == 0 && !huff::fixed8_disabled()) {  // inverse byte substitution
+        huff::dev::BytemapArgs m{};
+        m.src = d_comp;
+        m.dst = d_out;
+        m.n = n;
+        m.table = static_cast<const uint32_t*>(ctx->d_lut.p);  // entries (8 << 8) | letter
+        m.shift = 0;
+        HUFF_TRY(ctx->timed("decode", [&] { return huff::dev::launch_bytemap(m, ctx->stream); }));
+        return huff::Status::ok();
+    }
     huff::dev::DecodeArgs a{};
     a.comp = d_comp;
     a.comp_bytes = comp_bytes;
@@ -576,12 +618,26 @@ namespace huff {
 Status decode_indexless_dev(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_bytes, uint64_t valid_bits,
                             const huff_tree* t, DevBuf& out, uint64_t* nsym) {
     *nsym = 0;
+    uint64_t* nsym_out_alias = nsym;
     if (valid_bits == 0) return Status::ok();
     if (reinterpret_cast<uintptr_t>(d_comp) & 3)
         return Status::err(HUFF_E_INVALID_ARG, "compressed stream must be 4-byte aligned");
     HUFF_TRY(ctx->activate());
     const DecTables* dt = nullptr;
     HUFF_TRY(ctx->upload_dec_tables(t, &dt));
+    if (dt->all8 && !fixed8_disabled()) {  // every code 8 bits: one symbol per whole byte
+        const uint64_t nsym = valid_bits / 8;
+        HUFF_TRY(out.ensure(nsym + 16));
+        dev::BytemapArgs m{};
+        m.src = d_comp;
+        m.dst = static_cast<uint8_t*>(out.p);
+        m.n = nsym;
+        m.table = static_cast<const uint32_t*>(ctx->d_lut.p);
+        m.shift = 0;
+        HIP_TRY(dev::launch_bytemap(m, ctx->stream));
+        *nsym_out_alias = nsym;
+        return Status::ok();
+    }
     // segment length: a multiple of the gcd of all code lengths
     uint32_t g = 0;
     for (const LeafCode& lc : t->t.leaves()) g = std::gcd(g, lc.len);

@@ -40,7 +40,11 @@ struct DecTables {
     std::vector<uint32_t> lut;  // primary [1 << bits] then 8-bit secondaries
     uint32_t bits = 0;
     uint32_t maxdepth = 0;
+    bool all8 = false;          // every leaf at depth 8: decode is a byte map
 };
+
+// HUFF_DISABLE_FIXED8=1 forces the general kernels even for all-8-bit codes
+bool fixed8_disabled();
 
 Status build_dec_tables(const HuffTree& t, DecTables& out);
 

@@ -13,7 +13,9 @@
  *  - Plain pointers and sizes only. "host" pointers are CPU memory; "d_"
  *    pointers are device (HBM) memory of the context's GPU.
  *  - One huff_ctx per host thread. A context owns its HIP stream (or adopts
- *    the caller's via huff_ctx_set_stream) and its device workspace. Calls on
+ *    the caller's via huff_ctx_set_stream) and its device workspace. The own
+ *    stream is a blocking stream, so it runs after work already queued on the
+ *    legacy default stream (PyTorch's default). Calls on
  *    different contexts are thread-safe; the host-only functions (weights,
  *    tree) are reentrant and need no context.
  *  - Only the u8 alphabet is supported (the reference's ByteWeights path);

@@ -189,10 +189,15 @@ def test_device_job_medium(H, O, ctx, kind, seed):
     assert torch.equal(dec[:n], x[:n])
 
 
-def test_device_job_full_size_uniform(H, O, ctx):
-    """BASELINE config 2: 1 GiB uniform, bit-exact vs the checker + round trip"""
+@pytest.mark.parametrize("general", [False, True], ids=["fixed8", "general"])
+def test_device_job_full_size_uniform(H, O, ctx, general, monkeypatch):
+    """BASELINE config 2: 1 GiB uniform, bit-exact vs the checker + round trip.
+    Every code is 8 bits here, so the byte-map kernel runs unless
+    HUFF_DISABLE_FIXED8 forces the general pack/decode kernels."""
     import torch
 
+    if general:
+        monkeypatch.setenv("HUFF_DISABLE_FIXED8", "1")
     n = 1 << 30
     x = _device_gen(H, ctx, "uniform", 0x5EED0001, n)
     job = H.EncodeJob(ctx, x.data_ptr(), n)

@@ -14,7 +14,7 @@ from collections import defaultdict
 
 
 def short(name: str) -> str:
-    for k in ("k_hist", "k_chunk_bits", "k_scan", "k_pack", "k_decode", "k_spec", "k_fix", "k_emit", "k_gen"):
+    for k in ("k_hist", "k_chunk_bits", "k_scan", "k_pack", "k_decode", "k_spec", "k_fix", "k_emit", "k_gen", "k_bytemap", "k_settle", "k_find_first"):
         if k in name:
             return k + ("<long>" if "ILb1E" in name else "")
     return name[:40]
