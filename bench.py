@@ -35,6 +35,7 @@ import torch.distributed as dist  # noqa: E402
 
 import huff_coding as H  # noqa: E402
 from huff_coding import device as D  # noqa: E402
+from huff_coding import mgpu  # noqa: E402
 
 METRIC = "encode+decode GB/s on 1 GiB bytes at 1/2/4/8 MI355X; % HBM roofline"
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
@@ -86,14 +87,19 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="gloo: rehearse the N>1 path with several ranks on one GPU")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
 
     ctx = H.Context(local)
     stream = torch.cuda.current_stream()
@@ -108,38 +114,28 @@ def main():
     dec = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
     state = {"out": None, "cap": 0}
 
-    def exchange(w):
-        """all ranks' weights (and the 8 input bytes before each rank)"""
-        if world == 1:
-            return w[None, :], b""
-        row = torch.empty(257, dtype=torch.int64, device="cuda")
-        row[:256] = torch.from_numpy(w.view(np.int64)).cuda(non_blocking=False)
-        row[256:] = x[n - 8:n].view(torch.int64)
-        rows = [torch.empty_like(row) for _ in range(world)]
-        dist.all_gather(rows, row)
-        allr = torch.stack(rows).cpu().numpy()
-        hists = allr[:, :256].view(np.uint64)
-        tail = allr[rank - 1, 256:].view(np.uint8).tobytes() if rank > 0 else b""
-        return hists, tail
+    dev = torch.device("cuda", local) if args.dist_backend == "nccl" else None
 
     def step():
+        """pass 1 -> (N>1: one all_gather) -> host tree -> pass 2 -> decode"""
         w = job.hist()
-        hists, tail = exchange(w)
+        if world > 1:
+            hists, tails = mgpu.exchange(w, x[n - 8:n], device=dev)
+        else:
+            hists, tails = w[None, :], [b""]
         total = hists.sum(axis=0, dtype=np.uint64)
         tree = H.HuffTree.from_weights(H.ByteWeights.from_array(total))
         _, ln = tree.code_table()
-        per_rank_bits = hists @ ln.astype(np.uint64)
-        base = int(per_rank_bits[:rank].sum())
-        bits = int(per_rank_bits[rank])
-        need = (base % 8 + bits + 7) // 8 + 64
+        pl = mgpu.plan(hists, tails, ln, rank)
+        need = (pl.bit_base % 8 + pl.bits + 7) // 8 + 64
         if need > state["cap"]:
             state["out"] = torch.empty(need, dtype=torch.uint8, device="cuda")
             state["cap"] = need
         out = state["out"]
-        job.pack(tree, out.data_ptr(), state["cap"], bit_base=base, prev_tail=tail)
+        job.pack(tree, out.data_ptr(), state["cap"], bit_base=pl.bit_base, prev_tail=pl.prev_tail)
         job.decode(tree, out.data_ptr(), dec.data_ptr())
         state["fixed8"] = bool((ln[total > 0] == 8).all()) and os.environ.get("HUFF_DISABLE_FIXED8", "0") in ("", "0")
-        return bits, tree
+        return pl.bits, tree
 
     for _ in range(args.warmup):
         step()
@@ -161,7 +157,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev or "cpu")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
 
@@ -202,7 +198,7 @@ def main():
         "config": {"workload": WORKLOADS[kind], "bytes_per_gpu": n, "global_bytes": n * world,
                    "compressed_bytes_per_gpu": comp_bytes, "bits_per_byte": round(bits / n, 4),
                    "kernel_path": "fixed8 byte map (all codes 8 bits)" if state.get("fixed8") else "general bit pack/decode",
-                   "parallelism": f"shard{world}", "collective": "all_gather u64[257] over RCCL" if world > 1 else None},
+                   "parallelism": f"shard{world}", "collective": (f"all_gather int64[258] (weights + tail bytes) over {'RCCL' if args.dist_backend == 'nccl' else 'gloo (rehearsal)'}" if world > 1 else None)},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": ach, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": None},
         "kernels": kernels,

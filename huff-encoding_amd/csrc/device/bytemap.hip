@@ -27,6 +27,12 @@ __device__ __forceinline__ uint32_t map4(const uint32_t* tab, uint32_t w, uint32
     return b0 | (b1 << 8) | (b2 << 16) | (b3 << 24);
 }
 
+__device__ __forceinline__ void st_nt(uint4* p, uint4 v) {
+    u32x4_t w = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(w, reinterpret_cast<u32x4_t*>(p));
+}
+
+template <int DEPTH, bool NT_STORE>
 __global__ __launch_bounds__(kThreads) void k_bytemap(BytemapArgs a) {
     __shared__ __attribute__((aligned(16))) uint32_t tab[256 * 32];
     const uint32_t t = threadIdx.x, copy = t & 31;
@@ -42,18 +48,21 @@ __global__ __launch_bounds__(kThreads) void k_bytemap(BytemapArgs a) {
     const uint4* src = reinterpret_cast<const uint4*>(a.src);
     uint4* dst = reinterpret_cast<uint4*>(a.dst);
     uint64_t v = gid;
-    for (; v + 3 * stride < nvec; v += 4 * stride) {
-        uint4 x[4];
+    for (; v + (DEPTH - 1) * stride < nvec; v += DEPTH * stride) {
+        uint4 x[DEPTH];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) x[k] = ld_nt(src + v + k * stride);
+        for (int k = 0; k < DEPTH; ++k) x[k] = ld_nt(src + v + k * stride);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
+        for (int k = 0; k < DEPTH; ++k) {
             uint4 y;
             y.x = map4(tab, x[k].x, copy);
             y.y = map4(tab, x[k].y, copy);
             y.z = map4(tab, x[k].z, copy);
             y.w = map4(tab, x[k].w, copy);
-            dst[v + k * stride] = y;
+            if (NT_STORE)
+                st_nt(dst + v + k * stride, y);
+            else
+                dst[v + k * stride] = y;
         }
     }
     for (; v < nvec; v += stride) {
@@ -79,11 +88,13 @@ __global__ __launch_bounds__(kThreads) void k_bytemap(BytemapArgs a) {
 
 hipError_t launch_bytemap(const BytemapArgs& a, hipStream_t s) {
     if (a.n == 0 && !a.chunk_start) return hipSuccess;
+    // one pass, no grid stride: each thread maps 4 x 16 B (measured on 1 GiB:
+    // 0.43 ms for 2 GiB moved; a 2048-block grid-stride loop 0.46-0.47 ms)
     const uint64_t nvec = a.n / 16;
     uint64_t blocks = (nvec + kThreads * 4 - 1) / (kThreads * 4);
     if (blocks < 1) blocks = 1;
-    const uint32_t grid = static_cast<uint32_t>(blocks < 2048 ? blocks : 2048);
-    hipLaunchKernelGGL(k_bytemap, dim3(grid), dim3(kThreads), 0, s, a);
+    const uint32_t grid = static_cast<uint32_t>(blocks < (1u << 20) ? blocks : (1u << 20));
+    hipLaunchKernelGGL((k_bytemap<4, true>), dim3(grid), dim3(kThreads), 0, s, a);
     return hipGetLastError();
 }
 

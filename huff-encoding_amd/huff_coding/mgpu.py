@@ -38,17 +38,28 @@ class ShardPlan:
     prev_tail: bytes          # <= 8 input bytes right before this shard
 
 
-def exchange(weights: np.ndarray, tail: bytes, device: Optional[torch.device] = None, group=None):
-    """all_gather of [weights(256) | tail bytes | tail length] -> (hists, tails)"""
+def exchange(weights: np.ndarray, tail, device: Optional[torch.device] = None, group=None):
+    """all_gather of [weights(256) | tail bytes | tail length] -> (hists, tails).
+
+    `tail` is the shard's last <= 8 input bytes: host bytes, or a uint8
+    tensor already on `device` (then it never leaves the GPU before the
+    collective)."""
     world = dist.get_world_size(group)
     row = np.zeros(258, np.int64)
     row[:256] = np.asarray(weights, np.uint64).view(np.int64)
-    t = bytes(tail[-8:])
-    row[256] = np.frombuffer(t.ljust(8, b"\0"), np.int64)[0]
-    row[257] = len(t)
+    dev_tail = isinstance(tail, torch.Tensor)
+    if dev_tail:
+        tail = tail[-8:]
+        row[257] = tail.numel()
+    else:
+        t = bytes(tail[-8:])
+        row[256] = np.frombuffer(t.ljust(8, b"\0"), np.int64)[0]
+        row[257] = len(t)
     rt = torch.from_numpy(row)
     if device is not None:
-        rt = rt.to(device)
+        rt = rt.to(device, non_blocking=False)
+    if dev_tail and tail.numel():
+        rt.view(torch.uint8)[256 * 8: 256 * 8 + tail.numel()] = tail
     rows = [torch.empty_like(rt) for _ in range(world)]
     dist.all_gather(rows, rt, group=group)
     allr = torch.stack(rows).cpu().numpy()

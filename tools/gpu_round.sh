@@ -1,0 +1,28 @@
+#!/usr/bin/env bash
+# One GPU-box session: parity tests, N=1 benches, a 2-rank rehearsal of the
+# N>1 path (gloo, both ranks on the one GPU), rocprofv3 profiles.
+#   tools/gpu_round.sh <tag> [skip-tests] [skip-prof]
+set -euo pipefail
+tag=${1:-dev}
+root=${GRAFT_REPO_ROOT:-$(pwd)}
+cd "$root"
+out=gpurun_out/$tag
+mkdir -p "$out"
+if [ "${2:-}" != "skip-tests" ]; then
+  timeout -k 10 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider > "$out/gpu_tests.log" 2>&1
+fi
+timeout -k 10 400 python bench.py > "$out/bench_uniform.json" 2> "$out/bench_uniform.err"
+for w in zipf text; do
+  timeout -k 10 300 python bench.py --workload $w --no-cpu-baseline > "$out/bench_$w.json" 2> "$out/bench_$w.err"
+done
+HUFF_DISABLE_FIXED8=1 timeout -k 10 300 python bench.py --no-cpu-baseline > "$out/bench_uniform_general.json" 2> "$out/bench_uniform_general.err"
+timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+  --master-port 29533 bench.py --gpus 2 --steps 5 --warmup 2 --workload text --bytes-per-gpu $((1<<28)) \
+  --dist-backend gloo > "$out/bench_2rank_gloo.json" 2> "$out/bench_2rank_gloo.err"
+if [ "${3:-}" != "skip-prof" ]; then
+  for w in uniform zipf; do
+    bash tools/profile.sh all $w "${tag}_all_$w" > /dev/null
+    python tools/summarize_prof.py "gpurun_out/prof/${tag}_all_$w" > "$out/prof_all_$w.json"
+  done
+fi
+echo "gpu_round $tag done"
