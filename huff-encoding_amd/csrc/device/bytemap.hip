@@ -32,49 +32,48 @@ __device__ __forceinline__ void st_nt(uint4* p, uint4 v) {
     __builtin_nontemporal_store(w, reinterpret_cast<u32x4_t*>(p));
 }
 
-template <int DEPTH, bool NT_STORE>
+// One-shot grid: workgroup w maps the 16 KiB [w * 16 KiB, +16 KiB), lane t
+// the four 16-B pieces t, t+256, t+512, t+768 of it (each a coalesced 4 KiB
+// row per wave set). The data loads are issued before the table is staged in
+// LDS, so the table setup hides under the HBM latency.
 __global__ __launch_bounds__(kThreads) void k_bytemap(BytemapArgs a) {
     __shared__ __attribute__((aligned(16))) uint32_t tab[256 * 32];
     const uint32_t t = threadIdx.x, copy = t & 31;
-#pragma unroll 4
-    for (int i = 0; i < 32; ++i) {
-        const uint32_t e = (t >> 5) + 8 * i;
-        tab[(e << 5) | copy] = (a.table[e] >> a.shift) & 0xFFu;
-    }
-    __syncthreads();
-    const uint64_t gid = static_cast<uint64_t>(blockIdx.x) * kThreads + t;
-    const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kThreads;
     const uint64_t nvec = a.n / 16;
+    const uint64_t v0 = static_cast<uint64_t>(blockIdx.x) * (kThreads * 4) + t;
     const uint4* src = reinterpret_cast<const uint4*>(a.src);
     uint4* dst = reinterpret_cast<uint4*>(a.dst);
-    uint64_t v = gid;
-    for (; v + (DEPTH - 1) * stride < nvec; v += DEPTH * stride) {
-        uint4 x[DEPTH];
+    uint4 x[4];
 #pragma unroll
-        for (int k = 0; k < DEPTH; ++k) x[k] = ld_nt(src + v + k * stride);
+    for (int k = 0; k < 4; ++k) {
+        const uint64_t v = v0 + k * kThreads;
+        x[k] = v < nvec ? ld_nt(src + v) : make_uint4(0, 0, 0, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    {  // lane t stages entry t into its 32 copies (one 128-B run)
+        const uint32_t e = (a.table[t] >> a.shift) & 0xFFu;
+        uint4* row = reinterpret_cast<uint4*>(tab + (t << 5));
 #pragma unroll
-        for (int k = 0; k < DEPTH; ++k) {
+        for (int i = 0; i < 8; ++i) row[i] = make_uint4(e, e, e, e);
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): table stores done; data loads stay in flight
+    __builtin_amdgcn_s_barrier();
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint64_t v = v0 + k * kThreads;
+        if (v < nvec) {
             uint4 y;
             y.x = map4(tab, x[k].x, copy);
             y.y = map4(tab, x[k].y, copy);
             y.z = map4(tab, x[k].z, copy);
             y.w = map4(tab, x[k].w, copy);
-            if (NT_STORE)
-                st_nt(dst + v + k * stride, y);
-            else
-                dst[v + k * stride] = y;
+            st_nt(dst + v, y);
         }
     }
-    for (; v < nvec; v += stride) {
-        const uint4 x = src[v];
-        uint4 y;
-        y.x = map4(tab, x.x, copy);
-        y.y = map4(tab, x.y, copy);
-        y.z = map4(tab, x.z, copy);
-        y.w = map4(tab, x.w, copy);
-        dst[v] = y;
-    }
-    for (uint64_t i = nvec * 16 + gid; i < a.n; i += stride) a.dst[i] = static_cast<uint8_t>(tab[(a.src[i] << 5) | copy]);
+    const uint64_t gid = static_cast<uint64_t>(blockIdx.x) * kThreads + t;
+    const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kThreads;
+    if (blockIdx.x == gridDim.x - 1)
+        for (uint64_t i = nvec * 16 + t; i < a.n; i += kThreads) a.dst[i] = static_cast<uint8_t>(tab[(a.src[i] << 5) | copy]);
     // restart index of an 8-bit-per-symbol stream
     if (a.chunk_start)
         for (uint64_t c = gid; c <= a.nchunks; c += stride) a.chunk_start[c] = a.base_bits + c * kChunk * 8;
@@ -88,13 +87,11 @@ __global__ __launch_bounds__(kThreads) void k_bytemap(BytemapArgs a) {
 
 hipError_t launch_bytemap(const BytemapArgs& a, hipStream_t s) {
     if (a.n == 0 && !a.chunk_start) return hipSuccess;
-    // one pass, no grid stride: each thread maps 4 x 16 B (measured on 1 GiB:
-    // 0.43 ms for 2 GiB moved; a 2048-block grid-stride loop 0.46-0.47 ms)
     const uint64_t nvec = a.n / 16;
     uint64_t blocks = (nvec + kThreads * 4 - 1) / (kThreads * 4);
     if (blocks < 1) blocks = 1;
-    const uint32_t grid = static_cast<uint32_t>(blocks < (1u << 20) ? blocks : (1u << 20));
-    hipLaunchKernelGGL((k_bytemap<4, true>), dim3(grid), dim3(kThreads), 0, s, a);
+    if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_bytemap, dim3(static_cast<uint32_t>(blocks)), dim3(kThreads), 0, s, a);
     return hipGetLastError();
 }
 

@@ -10,7 +10,7 @@
 // chunk the 32 copies are summed (rotated reads, conflict-free) into the
 // per-chunk histogram row; the workgroup's totals go to one of 8 XCD-group
 // copies of the global weights with one atomic per bin.
-#include "kernels.hpp"
+#include "bitreader.hpp"
 
 namespace huff::dev {
 
@@ -19,12 +19,6 @@ namespace {
 constexpr int kThreads = 256;
 constexpr int kCopies = 32;
 
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ uint4 ld_nt(const uint4* p) {
-    u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
-    return make_uint4(v.x, v.y, v.z, v.w);
-}
 
 __device__ __forceinline__ void count_word(uint32_t* h, uint32_t w, uint32_t lane32) {
 #pragma unroll
@@ -111,6 +105,80 @@ __global__ __launch_bounds__(kThreads) void k_hist(const uint8_t* __restrict__ b
     if (total) atomicAdd(&gw[(blockIdx.x % kHistCopies) * 256 + t], static_cast<unsigned long long>(total));
 }
 
+// One chunk per workgroup (one-shot grid: the streaming-read shape that
+// measured fastest on this chip, tools/calib.hip): all 16 loads of a lane are
+// issued before the first count, the chunk's row is written, and the global
+// weights are summed from the rows afterwards (k_rows_sum) instead of with
+// per-workgroup atomics.
+__global__ __launch_bounds__(kThreads) void k_hist1(const uint8_t* __restrict__ base, uint64_t lo, uint64_t hi,
+                                                    uint32_t* __restrict__ chunk_hist) {
+    __shared__ __attribute__((aligned(16))) uint32_t h[256 * kCopies];
+    const uint32_t t = threadIdx.x;
+    const uint32_t lane32 = t & 31;
+    uint4* h4 = reinterpret_cast<uint4*>(h);
+#pragma unroll
+    for (int i = 0; i < 256 * kCopies / 4 / kThreads; ++i) h4[t + i * kThreads] = make_uint4(0, 0, 0, 0);
+    const uint32_t c = blockIdx.x;
+    const uint64_t cbeg = static_cast<uint64_t>(c) * kChunk;
+    const bool full = cbeg >= lo && cbeg + kChunk <= hi;
+    if (full) {
+        const uint4* p = reinterpret_cast<const uint4*>(base + cbeg) + t;
+        uint4 v[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[r] = ld_nt(p + r * kThreads);
+        __builtin_amdgcn_sched_barrier(0);  // no use of v[] hoisted above the last load
+        // LDS zeroing done everywhere; a bare barrier (no fence) so the
+        // 16 loads stay in flight across it
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0), vmcnt/expcnt untouched
+        __builtin_amdgcn_s_barrier();
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            count_word(h, v[r].x, lane32);
+            count_word(h, v[r].y, lane32);
+            count_word(h, v[r].z, lane32);
+            count_word(h, v[r].w, lane32);
+        }
+    } else {
+        __syncthreads();
+        for (int r = 0; r < 16; ++r) {
+            const uint64_t off = cbeg + static_cast<uint64_t>(r) * kRound + t * 16;
+            if (off + 16 <= lo || off >= hi) continue;
+            uint4 v;
+            if (off + 16 <= hi) {
+                v = *reinterpret_cast<const uint4*>(base + off);
+            } else {  // never read past hi
+                uint32_t w[4] = {0, 0, 0, 0};
+                for (int k = 0; off + k < hi; ++k) w[k >> 2] |= static_cast<uint32_t>(base[off + k]) << (8 * (k & 3));
+                v = make_uint4(w[0], w[1], w[2], w[3]);
+            }
+            count_masked(h, v, off, lo, hi, lane32);
+        }
+    }
+    __syncthreads();
+    uint32_t s = 0;
+#pragma unroll 8
+    for (int j = 0; j < kCopies; ++j) s += h[(t << 5) | ((j + t) & 31)];
+    chunk_hist[static_cast<uint64_t>(c) * 256 + t] = s;
+}
+
+// gw[copy][b] += sum over a stripe of chunks of chunk_hist[c][b]
+__global__ __launch_bounds__(256) void k_rows_sum(const uint32_t* __restrict__ chunk_hist, uint32_t nchunks,
+                                                  unsigned long long* __restrict__ gw) {
+    const uint32_t t = threadIdx.x;
+    uint64_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+    uint32_t c = blockIdx.x;
+    const uint32_t g = gridDim.x;
+    for (; c + 3 * g < nchunks; c += 4 * g) {
+        s0 += chunk_hist[static_cast<uint64_t>(c) * 256 + t];
+        s1 += chunk_hist[static_cast<uint64_t>(c + g) * 256 + t];
+        s2 += chunk_hist[static_cast<uint64_t>(c + 2 * g) * 256 + t];
+        s3 += chunk_hist[static_cast<uint64_t>(c + 3 * g) * 256 + t];
+    }
+    for (; c < nchunks; c += g) s0 += chunk_hist[static_cast<uint64_t>(c) * 256 + t];
+    const uint64_t s = s0 + s1 + s2 + s3;
+    if (s) atomicAdd(&gw[(blockIdx.x % kHistCopies) * 256 + t], static_cast<unsigned long long>(s));
+}
+
 // bits[c] = sum_b chunk_hist[c][b] * len[b]; one wave per chunk.
 __global__ __launch_bounds__(256) void k_chunk_bits(const uint32_t* __restrict__ chunk_hist, uint32_t nchunks,
                                                     const uint8_t* __restrict__ len, uint64_t* __restrict__ bits) {
@@ -181,6 +249,12 @@ __global__ __launch_bounds__(256) void k_find_first(const uint8_t* __restrict__ 
 hipError_t launch_hist(const uint8_t* base, uint64_t lo, uint64_t hi, uint32_t nchunks, uint32_t* chunk_hist,
                        unsigned long long* gw, hipStream_t s) {
     if (nchunks == 0) return hipSuccess;
+    if (chunk_hist) {  // per-chunk rows wanted: one-shot grid, then the row sum
+        hipLaunchKernelGGL(k_hist1, dim3(nchunks), dim3(kThreads), 0, s, base, lo, hi, chunk_hist);
+        const uint32_t g = nchunks < 512 ? nchunks : 512;
+        hipLaunchKernelGGL(k_rows_sum, dim3(g), dim3(256), 0, s, chunk_hist, nchunks, gw);
+        return hipGetLastError();
+    }
     uint32_t grid = nchunks < 1024 ? nchunks : 1024;
     hipLaunchKernelGGL(k_hist, dim3(grid), dim3(kThreads), 0, s, base, lo, hi, nchunks, chunk_hist, gw);
     return hipGetLastError();

@@ -26,6 +26,11 @@ constexpr uint32_t kHistCopies = 8;     // XCD-group copies of the global weight
 constexpr uint32_t kLutMaxBits = 12;    // primary decode table index bits
 constexpr uint32_t kLutPtr = 0x80000000u;
 constexpr uint32_t kPackWaveRound = 1024;  // bytes per wave round in pack (64 lanes x 16 B)
+// multi-symbol decode entry: up to 3 letters in bits [0, 24), bits used in
+// [24, 29), letter count in [29, 31); kMsSlow: the first code is longer than
+// the table's index bits (decode it with the single-symbol tables)
+constexpr uint32_t kMsMaxBits = 12;
+constexpr uint32_t kMsSlow = 0x80000000u;
 
 
 struct PackArgs {
@@ -53,6 +58,9 @@ struct DecodeArgs {
     uint32_t nchunks;
     uint32_t max_len;             // longest code (> 32: window slow path)
     uint32_t lut_rep_log2;        // primary table copies in LDS (bank spread)
+    const uint32_t* mlut;         // multi-symbol table [1 << mlut_bits] (null: none)
+    uint32_t mlut_bits;
+    uint32_t variant;             // kernel choice for experiments (0 = default)
     uint64_t n;
     uint8_t* out;
 };
@@ -85,6 +93,7 @@ struct BytemapArgs {
 
 size_t pack_lds_bytes(bool long_codes, uint32_t stage_words);
 size_t decode_lds_bytes(uint32_t lut_bits, uint32_t rep_log2);
+size_t decode_ms_lds_bytes(uint32_t mlut_bits, uint32_t rep_log2);
 
 hipError_t launch_hist(const uint8_t* base, uint64_t lo, uint64_t hi, uint32_t nchunks, uint32_t* chunk_hist,
                        unsigned long long* gw, hipStream_t s);

@@ -51,6 +51,39 @@ bool fixed8_disabled() {
     return e && *e && *e != '0';
 }
 
+static uint32_t ms_bits() {  // HUFF_DEC_MS_BITS: experiments only
+    const char* e = std::getenv("HUFF_DEC_MS_BITS");
+    const int v = e ? std::atoi(e) : static_cast<int>(dev::kMsMaxBits);
+    return static_cast<uint32_t>(std::max(4, std::min(static_cast<int>(dev::kMsMaxBits), v)));
+}
+
+void build_multi_table(const HuffTree& t, uint32_t mbits, DecTables& out) {
+    // entry i: walk the tree from the root over the mbits bits of i (MSB
+    // first), restarting at the root after every leaf, up to 3 letters; the
+    // walk is the reference's decompress (comp.rs:487-519) applied to i
+    const auto& nodes = t.nodes();
+    out.mbits = mbits;
+    out.moff = static_cast<uint32_t>(out.lut.size());
+    out.lut.resize(out.lut.size() + (1u << mbits), 0);
+    uint32_t* m = out.lut.data() + out.moff;
+    const bool root_leaf = t.root_is_leaf();
+    for (uint32_t i = 0; i < (1u << mbits); ++i) {
+        uint32_t syms = 0, count = 0, used = 0;
+        int32_t x = t.root();
+        for (uint32_t p = 0; p < mbits && count < 3; ++p) {
+            const uint32_t bit = (i >> (mbits - 1 - p)) & 1u;
+            if (!root_leaf) x = bit ? nodes[x].right : nodes[x].left;
+            if (nodes[x].is_leaf) {  // root-leaf tree: every bit is one letter
+                syms |= static_cast<uint32_t>(nodes[x].letter) << (8 * count);
+                ++count;
+                used = p + 1;
+                x = t.root();
+            }
+        }
+        m[i] = count ? (syms | (used << 24) | (count << 29)) : dev::kMsSlow;
+    }
+}
+
 Status build_dec_tables(const HuffTree& t, DecTables& out) {
     const auto& nodes = t.nodes();
     out.lut.clear();
@@ -59,6 +92,7 @@ Status build_dec_tables(const HuffTree& t, DecTables& out) {
         out.maxdepth = 1;
         const uint32_t e = (1u << 8) | nodes[t.root()].letter;
         out.lut = {e, e};
+        build_multi_table(t, ms_bits(), out);
         return Status::ok();
     }
     const uint32_t maxd = t.max_depth();
@@ -108,6 +142,7 @@ Status build_dec_tables(const HuffTree& t, DecTables& out) {
             }
         }
     }
+    build_multi_table(t, ms_bits(), out);
     return Status::ok();
 }
 
@@ -419,6 +454,15 @@ huff::Status huff_enc::decode(const huff_tree* t, const uint8_t* d_comp, uint64_
         int rep = std::max(0, std::min(5, 10 - static_cast<int>(dt->bits)));
         if (const char* env = std::getenv("HUFF_DEC_LUT_REP_LOG2")) rep = std::max(0, std::min(5, std::atoi(env)));
         a.lut_rep_log2 = static_cast<uint32_t>(rep);
+    }
+    a.mlut = static_cast<const uint32_t*>(ctx->d_lut.p) + dt->moff;
+    a.mlut_bits = dt->mbits;
+    a.variant = 0;
+    if (const char* env = std::getenv("HUFF_DEC_VARIANT")) a.variant = static_cast<uint32_t>(std::atoi(env));
+    if (a.variant == 0) {  // multi-symbol kernel: its own table replication
+        a.lut_rep_log2 = 0;
+        if (const char* env = std::getenv("HUFF_DEC_MS_REP_LOG2"))
+            a.lut_rep_log2 = static_cast<uint32_t>(std::max(0, std::min(3, std::atoi(env))));
     }
     a.n = n;
     a.out = d_out;

@@ -41,7 +41,13 @@ struct DecTables {
     uint32_t bits = 0;
     uint32_t maxdepth = 0;
     bool all8 = false;          // every leaf at depth 8: decode is a byte map
+    // multi-symbol table, appended to `lut` at word `moff`: [1 << mbits]
+    // entries for the top mbits bits of the window (dev::kMs* layout)
+    uint32_t mbits = 0, moff = 0;
 };
+
+// append the multi-symbol table (decode.hip k_decode_ms) to out.lut
+void build_multi_table(const HuffTree& t, uint32_t mbits, DecTables& out);
 
 // HUFF_DISABLE_FIXED8=1 forces the general kernels even for all-8-bit codes
 bool fixed8_disabled();

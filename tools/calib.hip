@@ -1,0 +1,108 @@
+// calib.hip — HBM ceilings on this box for the access shapes the codec uses.
+//   hipcc --offload-arch=gfx950 -O3 tools/calib.hip -o tools/calib && tools/calib
+// Prints GB/s (1e9) for: streaming read (16 B/lane, nontemporal / plain;
+// grid-stride and one-shot grids), streaming copy (plain / nontemporal
+// stores), 1 GiB each, best of 20 launches.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+
+#define CK(x)                                                                   \
+    do {                                                                        \
+        hipError_t e_ = (x);                                                    \
+        if (e_ != hipSuccess) {                                                 \
+            std::printf("HIP error %s at %d\n", hipGetErrorString(e_), __LINE__); \
+            std::exit(1);                                                       \
+        }                                                                       \
+    } while (0)
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+template <bool NT, int DEPTH>
+__global__ __launch_bounds__(256) void k_read(const u32x4* __restrict__ p, size_t nvec, unsigned* out) {
+    const size_t stride = static_cast<size_t>(gridDim.x) * 256;
+    size_t i = static_cast<size_t>(blockIdx.x) * 256 + threadIdx.x;
+    unsigned acc = 0;
+    for (; i + (DEPTH - 1) * stride < nvec; i += DEPTH * stride) {
+        u32x4 v[DEPTH];
+#pragma unroll
+        for (int k = 0; k < DEPTH; ++k) v[k] = NT ? __builtin_nontemporal_load(p + i + k * stride) : p[i + k * stride];
+#pragma unroll
+        for (int k = 0; k < DEPTH; ++k) acc ^= v[k].x ^ v[k].y ^ v[k].z ^ v[k].w;
+    }
+    for (; i < nvec; i += stride) {
+        u32x4 v = p[i];
+        acc ^= v.x ^ v.y ^ v.z ^ v.w;
+    }
+    if (acc == 0x12345678u) out[0] = acc;
+}
+
+template <bool NTL, bool NTS, int DEPTH>
+__global__ __launch_bounds__(256) void k_copy(const u32x4* __restrict__ p, u32x4* __restrict__ q, size_t nvec) {
+    const size_t stride = static_cast<size_t>(gridDim.x) * 256;
+    size_t i = static_cast<size_t>(blockIdx.x) * 256 + threadIdx.x;
+    for (; i + (DEPTH - 1) * stride < nvec; i += DEPTH * stride) {
+        u32x4 v[DEPTH];
+#pragma unroll
+        for (int k = 0; k < DEPTH; ++k) v[k] = NTL ? __builtin_nontemporal_load(p + i + k * stride) : p[i + k * stride];
+#pragma unroll
+        for (int k = 0; k < DEPTH; ++k) {
+            if (NTS)
+                __builtin_nontemporal_store(v[k], q + i + k * stride);
+            else
+                q[i + k * stride] = v[k];
+        }
+    }
+    for (; i < nvec; i += stride) q[i] = p[i];
+}
+
+template <typename F>
+static float best_ms(F launch) {
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    float best = 1e30f;
+    for (int r = 0; r < 20; ++r) {
+        CK(hipEventRecord(a));
+        launch();
+        CK(hipEventRecord(b));
+        CK(hipEventSynchronize(b));
+        float ms = 0;
+        CK(hipEventElapsedTime(&ms, a, b));
+        if (r >= 2 && ms < best) best = ms;
+    }
+    return best;
+}
+
+int main() {
+    const size_t n = size_t(1) << 30, nvec = n / 16;
+    u32x4 *p, *q;
+    unsigned* o;
+    CK(hipMalloc(&p, n));
+    CK(hipMalloc(&q, n));
+    CK(hipMalloc(&o, 64));
+    CK(hipMemset(p, 1, n));
+    CK(hipMemset(q, 0, n));
+    const unsigned grids[] = {1024, 2048, 4096, 0};
+    for (unsigned g : grids) {
+        const unsigned G4 = g ? g : static_cast<unsigned>(nvec / (256 * 4));
+        const unsigned G8 = g ? g : static_cast<unsigned>(nvec / (256 * 8));
+        float t;
+        t = best_ms([&] { hipLaunchKernelGGL((k_read<true, 4>), dim3(G4), dim3(256), 0, 0, p, nvec, o); });
+        std::printf("read  nt d4 grid %7u : %.4f ms %.0f GB/s\n", G4, t, n / t / 1e6);
+        t = best_ms([&] { hipLaunchKernelGGL((k_read<false, 4>), dim3(G4), dim3(256), 0, 0, p, nvec, o); });
+        std::printf("read  pl d4 grid %7u : %.4f ms %.0f GB/s\n", G4, t, n / t / 1e6);
+        t = best_ms([&] { hipLaunchKernelGGL((k_read<true, 8>), dim3(G8), dim3(256), 0, 0, p, nvec, o); });
+        std::printf("read  nt d8 grid %7u : %.4f ms %.0f GB/s\n", G8, t, n / t / 1e6);
+        t = best_ms([&] { hipLaunchKernelGGL((k_copy<true, false, 4>), dim3(G4), dim3(256), 0, 0, p, q, nvec); });
+        std::printf("copy  ntl pls d4 grid %7u : %.4f ms %.0f GB/s (2n)\n", G4, t, 2 * n / t / 1e6);
+        t = best_ms([&] { hipLaunchKernelGGL((k_copy<true, true, 4>), dim3(G4), dim3(256), 0, 0, p, q, nvec); });
+        std::printf("copy  ntl nts d4 grid %7u : %.4f ms %.0f GB/s (2n)\n", G4, t, 2 * n / t / 1e6);
+        t = best_ms([&] { hipLaunchKernelGGL((k_copy<false, false, 4>), dim3(G4), dim3(256), 0, 0, p, q, nvec); });
+        std::printf("copy  pll pls d4 grid %7u : %.4f ms %.0f GB/s (2n)\n", G4, t, 2 * n / t / 1e6);
+    }
+    float t = best_ms([&] { CK(hipMemcpyAsync(q, p, n, hipMemcpyDeviceToDevice, 0)); });
+    std::printf("hipMemcpy d2d : %.4f ms %.0f GB/s (2n)\n", t, 2 * n / t / 1e6);
+    return 0;
+}
