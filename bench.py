@@ -116,26 +116,27 @@ def main():
 
     dev = torch.device("cuda", local) if args.dist_backend == "nccl" else None
 
+    state["out"] = torch.empty(n + 128, dtype=torch.uint8, device="cuda")
+    state["cap"] = n + 128
+
     def step():
-        """pass 1 -> (N>1: one all_gather) -> host tree -> pass 2 -> decode"""
+        """pass 1 -> (N>1: one all_gather) -> pass 2 (native: tree, bit base, pack) -> decode"""
         w = job.hist()
         if world > 1:
             hists, tails = mgpu.exchange(w, x[n - 8:n], device=dev)
         else:
             hists, tails = w[None, :], [b""]
-        total = hists.sum(axis=0, dtype=np.uint64)
-        tree = H.HuffTree.from_weights(H.ByteWeights.from_array(total))
-        _, ln = tree.code_table()
-        pl = mgpu.plan(hists, tails, ln, rank)
-        need = (pl.bit_base % 8 + pl.bits + 7) // 8 + 64
-        if need > state["cap"]:
-            state["out"] = torch.empty(need, dtype=torch.uint8, device="cuda")
-            state["cap"] = need
-        out = state["out"]
-        job.pack(tree, out.data_ptr(), state["cap"], bit_base=pl.bit_base, prev_tail=pl.prev_tail)
-        job.decode(tree, out.data_ptr(), dec.data_ptr())
-        state["fixed8"] = bool((ln[total > 0] == 8).all()) and os.environ.get("HUFF_DISABLE_FIXED8", "0") in ("", "0")
-        return pl.bits, tree
+        try:
+            tree, base, bits = job.pack_shards(hists, rank, tails, state["out"].data_ptr(), state["cap"])
+        except H.HuffError as e:  # compressed shard larger than the buffer: grow once, redo
+            if getattr(e, "bits_needed", None) is None:
+                raise
+            state["cap"] = (e.bit_base % 8 + e.bits_needed + 7) // 8 + 128
+            state["out"] = torch.empty(state["cap"], dtype=torch.uint8, device="cuda")
+            tree, base, bits = job.pack_shards(hists, rank, tails, state["out"].data_ptr(), state["cap"])
+        job.decode(tree, state["out"].data_ptr(), dec.data_ptr())
+        state["hists"] = hists
+        return bits, tree
 
     for _ in range(args.warmup):
         step()
@@ -161,6 +162,9 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
 
+    _, ln = tree.code_table()
+    total = state["hists"].sum(axis=0, dtype=np.uint64)
+    state["fixed8"] = bool((ln[total > 0] == 8).all()) and os.environ.get("HUFF_DISABLE_FIXED8", "0") in ("", "0")
     ms_per_step = elapsed * 1e3 / args.steps
     value = world * n / (elapsed / args.steps) / 1e9
     comp_bytes = (bits + 7) // 8
@@ -203,6 +207,7 @@ def main():
                      "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": None},
         "kernels": kernels,
         "kernel_enc_GBps": round(n / (enc_ms * 1e-3) / 1e9, 1),
+        "host_gap_ms": round(ms_per_step - sum(k["avg_ms"] for k in kernels.values()), 4),
         "kernel_dec_GBps": kernels.get("decode", {}).get("GBps"),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

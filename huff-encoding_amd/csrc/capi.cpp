@@ -364,6 +364,41 @@ int huff_enc_pack(huff_enc* e, const huff_tree* t, uint64_t bit_base, const uint
     return guarded([&] { return e->pack(t, bit_base, prev_tail, prev_tail_len, d_out, out_cap, total_bits); });
 }
 
+int huff_enc_pack_shards(huff_enc* e, const uint64_t* hists, uint32_t world, uint32_t rank, const uint8_t* tails,
+                         const uint8_t* tail_lens, uint8_t* d_out, size_t out_cap, huff_tree** tree_out,
+                         uint64_t* bit_base_out, uint64_t* bits_out) {
+    if (!e || !hists || !world || rank >= world || !d_out || !tree_out || (rank && (!tails || !tail_lens)))
+        return fail(HUFF_E_INVALID_ARG, "null or out-of-range argument");
+    if (reinterpret_cast<uintptr_t>(d_out) & 15) return fail(HUFF_E_INVALID_ARG, "d_out must be 16-byte aligned");
+    *tree_out = nullptr;
+    return guarded([&]() -> huff::Status {
+        huff::ByteWeights g;  // from_bytes of the concatenation: plain per-bin sums
+        for (uint32_t q = 0; q < world; ++q)
+            for (int b = 0; b < 256; ++b) g.weights[b] += hists[static_cast<size_t>(q) * 256 + b];
+        g.len = 0;
+        for (int b = 0; b < 256; ++b) g.len += g.weights[b] != 0;
+        auto t = std::make_unique<huff_tree>();
+        HUFF_TRY(huff::HuffTree::from_weights(g, t->t));
+        const huff::EncTables& et = t->enc_tables();
+        uint64_t base = 0;
+        for (uint32_t q = 0; q < rank; ++q)
+            for (int b = 0; b < 256; ++b) base += hists[static_cast<size_t>(q) * 256 + b] * et.len[b];
+        uint8_t prev[8];
+        size_t np = 0;
+        for (uint32_t q = rank; q-- > 0 && np < 8;) {  // last <= 8 bytes before this shard
+            const size_t tl = tail_lens[q] > 8 ? 8 : tail_lens[q];
+            for (size_t k = tl; k-- > 0 && np < 8;) prev[7 - np++] = tails[static_cast<size_t>(q) * 8 + k];
+        }
+        if (bit_base_out) *bit_base_out = base;
+        uint64_t bits = 0;
+        huff::Status st = e->pack(t.get(), base, prev + 8 - np, np, d_out, out_cap, &bits);
+        if (bits_out) *bits_out = bits;
+        HUFF_TRY(st);
+        *tree_out = t.release();
+        return huff::Status::ok();
+    });
+}
+
 int huff_enc_decode(huff_enc* e, const huff_tree* t, const uint8_t* d_comp, uint8_t* d_out) {
     if (!e || !t || !d_comp || (!d_out && e->n)) return fail(HUFF_E_INVALID_ARG, "null argument");
     return guarded([&] {

@@ -618,6 +618,8 @@ hipError_t launch_decode(const DecodeArgs& a, hipStream_t s) {
     } else if (a.variant == 1 || !a.mlut) {
         hipLaunchKernelGGL(k_decode_short, dim3(a.nchunks), dim3(kThreads),
                            decode_lds_bytes(a.lut_bits, a.lut_rep_log2), s, a);
+    } else if (a.variant == 7) {
+        return launch_decode_ring(a, s);
     } else if (a.variant >= 3 && a.variant <= 6) {
         const uint32_t nent = ((1u << a.mlut_bits) + 3) & ~3u;
         switch (a.variant) {

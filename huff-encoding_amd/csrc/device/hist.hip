@@ -10,6 +10,8 @@
 // chunk the 32 copies are summed (rotated reads, conflict-free) into the
 // per-chunk histogram row; the workgroup's totals go to one of 8 XCD-group
 // copies of the global weights with one atomic per bin.
+#include <cstdlib>
+
 #include "bitreader.hpp"
 
 namespace huff::dev {
@@ -110,8 +112,12 @@ __global__ __launch_bounds__(kThreads) void k_hist(const uint8_t* __restrict__ b
 // issued before the first count, the chunk's row is written, and the global
 // weights are summed from the rows afterwards (k_rows_sum) instead of with
 // per-workgroup atomics.
+template <int MODE>  // MODE 1: timing experiment only (no counting)
 __global__ __launch_bounds__(kThreads) void k_hist1(const uint8_t* __restrict__ base, uint64_t lo, uint64_t hi,
-                                                    uint32_t* __restrict__ chunk_hist) {
+                                                    uint32_t* __restrict__ chunk_hist,
+                                                    unsigned long long* __restrict__ gw) {
+    if (blockIdx.x == 0)  // k_rows_sum (next on the stream) accumulates into gw
+        for (uint32_t i = threadIdx.x; i < kHistCopies * 256; i += kThreads) gw[i] = 0;
     __shared__ __attribute__((aligned(16))) uint32_t h[256 * kCopies];
     const uint32_t t = threadIdx.x;
     const uint32_t lane32 = t & 31;
@@ -131,12 +137,19 @@ __global__ __launch_bounds__(kThreads) void k_hist1(const uint8_t* __restrict__ 
         // 16 loads stay in flight across it
         __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0), vmcnt/expcnt untouched
         __builtin_amdgcn_s_barrier();
+        if (MODE == 1) {
+            uint32_t x = 0;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            count_word(h, v[r].x, lane32);
-            count_word(h, v[r].y, lane32);
-            count_word(h, v[r].z, lane32);
-            count_word(h, v[r].w, lane32);
+            for (int r = 0; r < 16; ++r) x ^= v[r].x ^ v[r].y ^ v[r].z ^ v[r].w;
+            if (x == 0x9e3779b9u) h[t] = x;
+        } else {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                count_word(h, v[r].x, lane32);
+                count_word(h, v[r].y, lane32);
+                count_word(h, v[r].z, lane32);
+                count_word(h, v[r].w, lane32);
+            }
         }
     } else {
         __syncthreads();
@@ -250,12 +263,27 @@ hipError_t launch_hist(const uint8_t* base, uint64_t lo, uint64_t hi, uint32_t n
                        unsigned long long* gw, hipStream_t s) {
     if (nchunks == 0) return hipSuccess;
     if (chunk_hist) {  // per-chunk rows wanted: one-shot grid, then the row sum
-        hipLaunchKernelGGL(k_hist1, dim3(nchunks), dim3(kThreads), 0, s, base, lo, hi, chunk_hist);
+        static const int mode = [] {
+            const char* e = std::getenv("HUFF_HIST_EXPERIMENT");
+            return e ? std::atoi(e) : 0;
+        }();
+        if (mode == 2) {
+            hipMemsetAsync(gw, 0, kHistCopies * 256 * 8, s);
+            uint32_t grid = nchunks < 1024 ? nchunks : 1024;
+            hipLaunchKernelGGL(k_hist, dim3(grid), dim3(kThreads), 0, s, base, lo, hi, nchunks, chunk_hist, gw);
+            return hipGetLastError();
+        }
+        if (mode == 1)
+            hipLaunchKernelGGL(k_hist1<1>, dim3(nchunks), dim3(kThreads), 0, s, base, lo, hi, chunk_hist, gw);
+        else
+            hipLaunchKernelGGL(k_hist1<0>, dim3(nchunks), dim3(kThreads), 0, s, base, lo, hi, chunk_hist, gw);
         const uint32_t g = nchunks < 512 ? nchunks : 512;
         hipLaunchKernelGGL(k_rows_sum, dim3(g), dim3(256), 0, s, chunk_hist, nchunks, gw);
         return hipGetLastError();
     }
     uint32_t grid = nchunks < 1024 ? nchunks : 1024;
+    const hipError_t e = hipMemsetAsync(gw, 0, kHistCopies * 256 * 8, s);
+    if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_hist, dim3(grid), dim3(kThreads), 0, s, base, lo, hi, nchunks, chunk_hist, gw);
     return hipGetLastError();
 }

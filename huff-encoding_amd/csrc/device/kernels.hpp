@@ -102,6 +102,8 @@ hipError_t launch_chunk_bits(const uint32_t* chunk_hist, uint32_t nchunks, const
 hipError_t launch_scan(const uint64_t* bits, uint32_t nchunks, uint64_t base, uint64_t* start, hipStream_t s);
 hipError_t launch_pack(bool long_codes, const PackArgs& a, hipStream_t s);
 hipError_t launch_decode(const DecodeArgs& a, hipStream_t s);
+hipError_t launch_decode_ring(const DecodeArgs& a, hipStream_t s);
+size_t decode_ring_lds_bytes(uint32_t mlut_bits);
 hipError_t launch_indexless_spec(const IndexlessArgs& a, hipStream_t s);
 hipError_t launch_indexless_fix(const IndexlessArgs& a, const uint64_t* xin, uint64_t* xout, unsigned int* changed,
                                 hipStream_t s);

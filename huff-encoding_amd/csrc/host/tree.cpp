@@ -23,18 +23,17 @@ struct HeapEntry {
 
 class RustMaxHeap {
 public:
-    explicit RustMaxHeap(size_t reserve) { v_.reserve(reserve); }
-    size_t size() const { return v_.size(); }
+    explicit RustMaxHeap(size_t reserve) : v_(reserve) {}
+    size_t size() const { return n_; }
 
     void push(HeapEntry e) {
-        v_.push_back(e);
-        sift_up(0, v_.size() - 1);
+        v_[n_++] = e;
+        sift_up(0, n_ - 1);
     }
 
     HeapEntry pop() {
-        HeapEntry top = v_.back();
-        v_.pop_back();
-        if (!v_.empty()) {
+        HeapEntry top = v_[--n_];
+        if (n_) {
             std::swap(top, v_[0]);
             sift_down_to_bottom(0);
         }
@@ -46,37 +45,40 @@ private:
     static bool le(const HeapEntry& a, const HeapEntry& b) { return a.w >= b.w; }
 
     size_t sift_up(size_t start, size_t pos) {
-        HeapEntry hole = v_[pos];
+        HeapEntry* v = v_.data();
+        const HeapEntry hole = v[pos];
         while (pos > start) {
-            size_t parent = (pos - 1) >> 1;
-            if (le(hole, v_[parent])) break;
-            v_[pos] = v_[parent];
+            const size_t parent = (pos - 1) >> 1;
+            if (le(hole, v[parent])) break;
+            v[pos] = v[parent];
             pos = parent;
         }
-        v_[pos] = hole;
+        v[pos] = hole;
         return pos;
     }
 
     void sift_down_to_bottom(size_t pos) {
-        const size_t end = v_.size();
+        HeapEntry* v = v_.data();
+        const size_t end = n_;
         const size_t start = pos;
-        HeapEntry hole = v_[pos];
+        const HeapEntry hole = v[pos];
         size_t child = 2 * pos + 1;
         while (end >= 2 && child <= end - 2) {
-            child += le(v_[child], v_[child + 1]) ? 1 : 0;
-            v_[pos] = v_[child];
+            child += le(v[child], v[child + 1]) ? 1 : 0;
+            v[pos] = v[child];
             pos = child;
             child = 2 * pos + 1;
         }
         if (child == end - 1) {
-            v_[pos] = v_[child];
+            v[pos] = v[child];
             pos = child;
         }
-        v_[pos] = hole;
+        v[pos] = hole;
         sift_up(start, pos);
     }
 
     std::vector<HeapEntry> v_;
+    size_t n_ = 0;
 };
 
 }  // namespace
@@ -155,23 +157,49 @@ void HuffTree::read_codes(std::array<std::vector<uint8_t>, 256>& codes) const {
 }
 
 bool HuffTree::read_codes_u64(uint64_t code[256], uint8_t len[256], uint32_t* maxlen) const {
-    std::array<std::vector<uint8_t>, 256> codes;
-    read_codes(codes);
+    // read_codes (tree_inner.rs:356-440) without materialising bit vectors:
+    // preorder, left before right, a later leaf of the same letter overwrites
+    uint32_t true_len[256] = {};
+    bool seen[256] = {};
+    for (int b = 0; b < 256; ++b) {
+        code[b] = 0;
+        len[b] = 0;
+    }
+    if (nodes_[root_].is_leaf) {  // tree_inner.rs:313-315: a root leaf's code is "0"
+        const uint8_t l = nodes_[root_].letter;
+        len[l] = 1;
+        if (maxlen) *maxlen = 1;
+        return true;
+    }
+    struct Frame {
+        int32_t node;
+        uint32_t depth;
+        uint64_t code;  // low 64 bits of the path (exact while depth <= 64)
+    };
+    Frame st[512];
+    int sp = 0;
+    st[sp++] = {nodes_[root_].right, 1, 1};
+    st[sp++] = {nodes_[root_].left, 1, 0};
+    while (sp) {
+        const Frame fr = st[--sp];
+        const HuffNode& nd = nodes_[fr.node];
+        if (nd.is_leaf) {
+            const uint8_t l = nd.letter;
+            seen[l] = true;
+            true_len[l] = fr.depth;
+            code[l] = fr.depth <= 64 ? fr.code : 0;
+            len[l] = fr.depth <= 64 ? static_cast<uint8_t>(fr.depth) : 0;
+            continue;
+        }
+        st[sp++] = {nd.right, fr.depth + 1, (fr.code << 1) | 1};
+        st[sp++] = {nd.left, fr.depth + 1, fr.code << 1};
+    }
     uint32_t ml = 0;
     bool ok = true;
     for (int b = 0; b < 256; ++b) {
-        const auto& c = codes[b];
-        ml = std::max<uint32_t>(ml, static_cast<uint32_t>(c.size()));
-        if (c.size() > 64) {
-            ok = false;
-            code[b] = 0;
-            len[b] = 0;
-            continue;
-        }
-        uint64_t v = 0;
-        for (uint8_t bit : c) v = (v << 1) | bit;
-        code[b] = v;
-        len[b] = static_cast<uint8_t>(c.size());
+        if (!seen[b]) continue;
+        ml = std::max(ml, true_len[b]);
+        ok &= true_len[b] <= 64;
     }
     if (maxlen) *maxlen = ml;
     return ok;

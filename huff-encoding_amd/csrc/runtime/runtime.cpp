@@ -165,7 +165,15 @@ huff::Status PinnedBuf::ensure(size_t bytes) {
 }
 
 huff::Status PinnedBuf::wait() {
-    if (ev) HIP_TRY(hipEventSynchronize(ev));
+    if (!ev) return huff::Status::ok();
+    // spin briefly (the waits here guard ~10 us copies on the critical path
+    // between pass 1 and pass 2), then block
+    for (int i = 0; i < 200000; ++i) {
+        const hipError_t q = hipEventQuery(ev);
+        if (q == hipSuccess) return huff::Status::ok();
+        if (q != hipErrorNotReady) HIP_TRY(q);
+    }
+    HIP_TRY(hipEventSynchronize(ev));
     return huff::Status::ok();
 }
 
@@ -303,7 +311,6 @@ huff::Status huff_enc::init(huff_ctx* c, const uint8_t* d, uint64_t nbytes) {
 huff::Status huff_enc::hist() {
     HUFF_TRY(ctx->activate());
     hipStream_t s = ctx->stream;
-    HIP_TRY(hipMemsetAsync(gw.p, 0, huff::dev::kHistCopies * 256 * 8, s));
     HUFF_TRY(ctx->timed("hist", [&] {
         return huff::dev::launch_hist(d_in, 0, n, nchunks, static_cast<uint32_t*>(chunk_hist.p),
                                       static_cast<unsigned long long*>(gw.p), s);
@@ -457,9 +464,12 @@ huff::Status huff_enc::decode(const huff_tree* t, const uint8_t* d_comp, uint64_
     }
     a.mlut = static_cast<const uint32_t*>(ctx->d_lut.p) + dt->moff;
     a.mlut_bits = dt->mbits;
-    a.variant = 0;
+    // kernel choice: the multi-symbol ring decoder pays off when lookups
+    // return more than one letter (mean code length well under the 12-bit
+    // table index); near-8-bit codes run the single-symbol kernel
+    a.variant = (total_bits < 7 * n) ? 7u : 1u;
     if (const char* env = std::getenv("HUFF_DEC_VARIANT")) a.variant = static_cast<uint32_t>(std::atoi(env));
-    if (a.variant == 0) {  // multi-symbol kernel: its own table replication
+    if (a.variant == 0 || a.variant == 7) {  // multi-symbol kernels: no table replication
         a.lut_rep_log2 = 0;
         if (const char* env = std::getenv("HUFF_DEC_MS_REP_LOG2"))
             a.lut_rep_log2 = static_cast<uint32_t>(std::max(0, std::min(3, std::atoi(env))));

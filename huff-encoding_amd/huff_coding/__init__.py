@@ -291,10 +291,11 @@ class HuffTree:
 
     def code_table(self):
         """(u64 code right-aligned, u8 len) per byte"""
-        code = (C.c_uint64 * 256)()
-        ln = (C.c_uint8 * 256)()
-        _check(load().huff_tree_read_codes(self.h, code, ln))
-        return np.array(code[:], np.uint64), np.array(ln[:], np.uint8)
+        code = np.zeros(256, np.uint64)
+        ln = np.zeros(256, np.uint8)
+        _check(load().huff_tree_read_codes(self.h, code.ctypes.data_as(C.POINTER(C.c_uint64)),
+                                           ln.ctypes.data_as(C.POINTER(C.c_uint8))))
+        return code, ln
 
     def as_bin(self) -> str:
         """tree_inner.rs:632-668 as a '0'/'1' string"""

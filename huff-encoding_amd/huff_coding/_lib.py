@@ -85,9 +85,10 @@ SIGNATURES = [
     ("huff_decompress", i, [vp, vp, u8p, sz, szp]),
     ("huff_enc_create", i, [vp, vp, sz, C.POINTER(vp)]),
     ("huff_enc_free", None, [vp]),
-    ("huff_enc_hist", i, [vp, u64p]),
+    ("huff_enc_hist", i, [vp, vp]),
     ("huff_enc_bits", i, [vp, vp, u64p]),
     ("huff_enc_pack", i, [vp, vp, C.c_uint64, vp, sz, vp, sz, u64p]),
+    ("huff_enc_pack_shards", i, [vp, vp, C.c_uint32, C.c_uint32, vp, vp, vp, sz, C.POINTER(vp), u64p, u64p]),
     ("huff_enc_decode", i, [vp, vp, vp, vp]),
     ("huff_dev_generate", i, [vp, i, C.c_uint64, C.c_uint64, u64p, vp, sz]),
     ("huff_dev_alloc", i, [vp, sz, C.POINTER(vp)]),

@@ -43,9 +43,9 @@ class EncodeJob:
 
     def hist(self) -> np.ndarray:
         """pass 1: the 256 weights (u64) of the job's bytes"""
-        w = (C.c_uint64 * 256)()
-        _check(load().huff_enc_hist(self.h, w))
-        return np.array(w[:], dtype=np.uint64)
+        w = np.empty(256, np.uint64)
+        _check(load().huff_enc_hist(self.h, w.ctypes.data))
+        return w
 
     def bits(self, tree) -> int:
         v = C.c_uint64()
@@ -60,6 +60,37 @@ class EncodeJob:
         _check(load().huff_enc_pack(self.h, tree.h, bit_base, buf, len(pt), C.c_void_p(d_out), out_cap,
                                     C.byref(v)))
         return v.value
+
+    def pack_shards(self, hists: np.ndarray, rank: int, tails, d_out: int, out_cap: int):
+        """pass 2 for shard `rank` of len(hists) shards: tree of the summed
+        weights, bit base and shared-byte tail computed natively, then pack.
+        Returns (HuffTree, bit_base, bits). Raises HuffError(BUFFER_TOO_SMALL)
+        with .bits_needed when out_cap is short."""
+        from . import HuffError, HuffTree
+
+        h = np.ascontiguousarray(hists, dtype=np.uint64)
+        world = h.shape[0]
+        tp = lp = None
+        if rank:  # the tails of the shards before this one
+            tb = np.zeros(world * 8, np.uint8)
+            tl = np.zeros(world, np.uint8)
+            for q, t in enumerate(tails[:rank]):
+                t = bytes(t[-8:])
+                tb[q * 8: q * 8 + len(t)] = np.frombuffer(t, np.uint8)
+                tl[q] = len(t)
+            tp, lp = tb.ctypes.data, tl.ctypes.data
+        tree_h = C.c_void_p()
+        base = C.c_uint64()
+        bits = C.c_uint64()
+        rc = load().huff_enc_pack_shards(self.h, h.ctypes.data, world, rank, tp, lp, d_out, out_cap,
+                                         C.byref(tree_h), C.byref(base), C.byref(bits))
+        try:
+            _check(rc)
+        except HuffError as e:
+            e.bits_needed = bits.value
+            e.bit_base = base.value
+            raise
+        return HuffTree(tree_h), base.value, bits.value
 
     def decode(self, tree, d_comp: int, d_out: int):
         """block-parallel decode of this job's pack output via its restart index"""

@@ -182,6 +182,19 @@ int huff_enc_bits(huff_enc* e, const huff_tree* t, uint64_t* total_bits);
 int huff_enc_pack(huff_enc* e, const huff_tree* t, uint64_t bit_base,
                   const uint8_t* prev_tail, size_t prev_tail_len,
                   uint8_t* d_out, size_t out_cap, uint64_t* total_bits);
+/* Multi-shard pass 2 in one call: the job is shard `rank` of
+ * `world` contiguous shards of one stream. hists = world x 256 per-shard
+ * weights (the exchanged huff_enc_hist results), tails = world x 8 bytes where
+ * shard q's last tail_lens[q] (<= 8) input bytes sit at tails[q*8 ...]. Builds
+ * the tree of the summed weights (ByteWeights::from_bytes of the whole
+ * stream), this shard's bit base (exclusive sum of the shards' bits) and
+ * previous-tail bytes, and packs as huff_enc_pack. *tree_out receives the tree
+ * (free with huff_tree_free). world = 1 is the single-GPU encode. On
+ * HUFF_E_BUFFER_TOO_SMALL *bits_out still holds the bits needed. */
+int huff_enc_pack_shards(huff_enc* e, const uint64_t* hists, uint32_t world, uint32_t rank,
+                         const uint8_t* tails, const uint8_t* tail_lens,
+                         uint8_t* d_out, size_t out_cap, huff_tree** tree_out,
+                         uint64_t* bit_base_out, uint64_t* bits_out);
 /* Block-parallel decode of what huff_enc_pack wrote (same job, same tree),
  * using its restart index: d_comp is the pack's d_out, d_out gets n bytes. */
 int huff_enc_decode(huff_enc* e, const huff_tree* t, const uint8_t* d_comp, uint8_t* d_out);

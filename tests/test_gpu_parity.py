@@ -291,6 +291,59 @@ def test_shard_stitching_on_one_gpu(H, O, ctx):
     assert base == total and got.size == want.size and (got == want).all()
 
 
+def test_pack_shards_on_one_gpu(H, O, ctx):
+    """huff_enc_pack_shards (native tree + bit base + tail, then pack) for 4
+    shards, one of them shorter than 8 bytes: the owned bytes concatenate to
+    the single-stream compress_with_tree bytes"""
+    import torch
+
+    from huff_coding import mgpu
+
+    rng = np.random.default_rng(11)
+    n = 2_500_003
+    data = np.minimum(rng.geometric(0.15, n), 255).astype(np.uint8)
+    x = torch.from_numpy(data).cuda()
+    bounds = [0, 900_001, 900_004, 1_700_000, n]
+    world = len(bounds) - 1
+    jobs, segs, hists, tails = [], [], [], []
+    for r in range(world):
+        lo, hi = bounds[r], bounds[r + 1]
+        seg = torch.empty(hi - lo + 64, dtype=torch.uint8, device="cuda")
+        seg[: hi - lo] = x[lo:hi]
+        job = H.EncodeJob(ctx, seg.data_ptr(), hi - lo)
+        hists.append(job.hist())
+        tails.append(data[lo:hi][-8:].tobytes())
+        jobs.append(job)
+        segs.append(seg)
+    hists = np.stack(hists)
+    w = np.bincount(data, minlength=256).astype(np.uint64)
+    ot = O.Tree.from_weights(O.weights_from_array(w))
+    code, ln = ot.code_table()
+    want, total = O.fast_encode(data, code, ln, threads=8)
+    pieces, base_expect = [], 0
+    for r in range(world):
+        lo, hi = bounds[r], bounds[r + 1]
+        cap = (hi - lo) * 2 + 128
+        out = torch.zeros(cap, dtype=torch.uint8, device="cuda")
+        tree, base, bits = jobs[r].pack_shards(hists, r, tails, out.data_ptr(), cap)
+        assert tree.as_bin() == ot.as_bin()
+        assert base == base_expect
+        torch.cuda.synchronize()
+        pieces.append(mgpu.owned_bytes(out.cpu().numpy(), base, bits, r == world - 1))
+        dec = torch.empty(hi - lo + 64, dtype=torch.uint8, device="cuda")
+        jobs[r].decode(tree, out.data_ptr(), dec.data_ptr())
+        torch.cuda.synchronize()
+        assert (dec[: hi - lo].cpu().numpy() == data[lo:hi]).all()
+        base_expect += bits
+    got = np.concatenate(pieces)
+    assert base_expect == total and got.size == want.size and (got == want).all()
+    # a short buffer reports the bits it needs
+    small = torch.zeros(64, dtype=torch.uint8, device="cuda")
+    with pytest.raises(H.HuffError) as ei:
+        jobs[0].pack_shards(hists, 0, tails, small.data_ptr(), 64)
+    assert ei.value.bits_needed == int(hists[0].astype(np.uint64) @ ln.astype(np.uint64))
+
+
 def test_file_path_matches_cli(H, O, ctx, golden):
     rng = np.random.default_rng(9)
     with tempfile.TemporaryDirectory() as d:

@@ -57,6 +57,22 @@ __global__ __launch_bounds__(256) void k_copy(const u32x4* __restrict__ p, u32x4
     for (; i < nvec; i += stride) q[i] = p[i];
 }
 
+// one-shot: block of T threads reads T*NL*16 contiguous bytes, NL loads per
+// lane issued together; `lds` bytes of dynamic LDS limit blocks per CU
+template <int NL>
+__global__ __launch_bounds__(1024) void k_read_blk(const u32x4* __restrict__ p, unsigned* out) {
+    extern __shared__ unsigned sh[];
+    const size_t base = static_cast<size_t>(blockIdx.x) * blockDim.x * NL + threadIdx.x;
+    u32x4 v[NL];
+#pragma unroll
+    for (int k = 0; k < NL; ++k) v[k] = __builtin_nontemporal_load(p + base + k * blockDim.x);
+    unsigned acc = 0;
+#pragma unroll
+    for (int k = 0; k < NL; ++k) acc ^= v[k].x ^ v[k].y ^ v[k].z ^ v[k].w;
+    sh[threadIdx.x] = acc;
+    if (acc == 0x12345678u) out[0] = sh[(threadIdx.x + 1) % blockDim.x];
+}
+
 template <typename F>
 static float best_ms(F launch) {
     hipEvent_t a, b;
@@ -84,7 +100,7 @@ int main() {
     CK(hipMalloc(&o, 64));
     CK(hipMemset(p, 1, n));
     CK(hipMemset(q, 0, n));
-    const unsigned grids[] = {1024, 2048, 4096, 0};
+    const unsigned grids[] = {0};
     for (unsigned g : grids) {
         const unsigned G4 = g ? g : static_cast<unsigned>(nvec / (256 * 4));
         const unsigned G8 = g ? g : static_cast<unsigned>(nvec / (256 * 8));
@@ -101,6 +117,18 @@ int main() {
         std::printf("copy  ntl nts d4 grid %7u : %.4f ms %.0f GB/s (2n)\n", G4, t, 2 * n / t / 1e6);
         t = best_ms([&] { hipLaunchKernelGGL((k_copy<false, false, 4>), dim3(G4), dim3(256), 0, 0, p, q, nvec); });
         std::printf("copy  pll pls d4 grid %7u : %.4f ms %.0f GB/s (2n)\n", G4, t, 2 * n / t / 1e6);
+    }
+    {
+        const unsigned thr[] = {256, 512, 1024};
+        const unsigned ldsk[] = {0, 32, 64};
+        for (unsigned T : thr)
+            for (unsigned L : ldsk) {
+                float t;
+                t = best_ms([&] { hipLaunchKernelGGL((k_read_blk<4>), dim3(nvec / (T * 4)), dim3(T), L * 1024, 0, p, o); });
+                std::printf("read_blk nl4  T%4u lds%2uK : %.4f ms %.0f GB/s\n", T, L, t, n / t / 1e6);
+                t = best_ms([&] { hipLaunchKernelGGL((k_read_blk<16>), dim3(nvec / (T * 16)), dim3(T), L * 1024, 0, p, o); });
+                std::printf("read_blk nl16 T%4u lds%2uK : %.4f ms %.0f GB/s\n", T, L, t, n / t / 1e6);
+            }
     }
     float t = best_ms([&] { CK(hipMemcpyAsync(q, p, n, hipMemcpyDeviceToDevice, 0)); });
     std::printf("hipMemcpy d2d : %.4f ms %.0f GB/s (2n)\n", t, 2 * n / t / 1e6);

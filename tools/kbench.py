@@ -41,6 +41,15 @@ def main():
                cdf=D.zipf_cdf(1.2) if args.workload == "zipf" else None)
     job = H.EncodeJob(ctx, x.data_ptr(), n)
     w = job.hist()
+    if args.phase == "hist":  # timing of pass 1 alone (also for experiment builds)
+        ctx.set_timing(True)
+        ctx.reset_timing()
+        for _ in range(args.iters):
+            job.hist()
+        torch.cuda.synchronize()
+        ms, c = ctx.kernel_time("hist")
+        print(json.dumps({"phase": "hist", "workload": args.workload, "n": n, "iters": args.iters, "hist_ms": ms / c}))
+        return
     tree = H.HuffTree.from_weights(H.ByteWeights.from_array(w))
     bits = job.bits(tree)
     out = torch.empty((bits + 7) // 8 + 64, dtype=torch.uint8, device="cuda")
