@@ -27,6 +27,12 @@ __device__ __forceinline__ uint4 ld_nt(const uint4* p) {
     return make_uint4(v.x, v.y, v.z, v.w);
 }
 
+// 16-byte streaming store
+__device__ __forceinline__ void st_nt(uint4* p, uint4 v) {
+    u32x4_t w = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(w, reinterpret_cast<u32x4_t*>(p));
+}
+
 struct BitSrc {
     const uint32_t* w;
     const uint8_t* b;

@@ -27,10 +27,6 @@ __device__ __forceinline__ uint32_t map4(const uint32_t* tab, uint32_t w, uint32
     return b0 | (b1 << 8) | (b2 << 16) | (b3 << 24);
 }
 
-__device__ __forceinline__ void st_nt(uint4* p, uint4 v) {
-    u32x4_t w = {v.x, v.y, v.z, v.w};
-    __builtin_nontemporal_store(w, reinterpret_cast<u32x4_t*>(p));
-}
 
 // One-shot grid: workgroup w maps the 16 KiB [w * 16 KiB, +16 KiB), lane t
 // the four 16-B pieces t, t+256, t+512, t+768 of it (each a coalesced 4 KiB
