@@ -45,6 +45,7 @@ struct PackArgs {
     uint32_t prev_tail_len;
     uint32_t stage_words;         // per wave
     uint32_t grid;                // persistent workgroups (4 waves each)
+    uint32_t max_len;             // longest code (groups codes for the OR emit)
 };
 
 struct DecodeArgs {

@@ -97,6 +97,32 @@ __device__ __forceinline__ void emit_codes(uint32_t* __restrict__ stage, uint64_
     }
 }
 
+// short codes: groups of G consecutive codes (G * max_len <= 32) are joined
+// in a register and ORed into their (at most) two stage words at the group's
+// bit offset: no serial 64-bit accumulator, no per-code branch.
+template <int G>
+__device__ __forceinline__ void emit_codes_or(uint32_t* __restrict__ stage, uint32_t p, const uint32_t (&ent)[16]) {
+    uint32_t o = p;
+#pragma unroll
+    for (int k = 0; k < 16; k += G) {
+        uint32_t code = 0, len = 0;
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            const uint32_t l = ent[k + g] & 31u;
+            code = (code << l) | (ent[k + g] >> 5);
+            len += l;
+        }
+        const uint32_t s = o & 31u;
+        // the group left-aligned at bit s of a 64-bit window starting at word o/32
+        // (an empty entry past the chunk end has len 0 and code 0: ORs zero)
+        const uint64_t v = static_cast<uint64_t>(code) << ((64u - s - len) & 63u);
+        uint32_t* w = stage + (o >> 5);
+        __hip_atomic_fetch_or(w, static_cast<uint32_t>(v >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_fetch_or(w + 1, static_cast<uint32_t>(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        o += len;
+    }
+}
+
 __device__ __forceinline__ void store_segment(const uint32_t* __restrict__ stage, uint32_t s, uint64_t gbyte,
                                               uint64_t own_lo, uint64_t own_hi, uint8_t* __restrict__ out) {
     uint4 v;
@@ -123,7 +149,7 @@ __device__ __forceinline__ uint4 load_lane(const uint8_t* __restrict__ in, uint6
     return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
-template <bool LONG>
+template <bool LONG, int G = 1>
 __global__ __launch_bounds__(kThreads) void k_pack(PackArgs a) {
     using E = Entry<LONG>;
     using T = typename E::T;
@@ -220,7 +246,11 @@ __global__ __launch_bounds__(kThreads) void k_pack(PackArgs a) {
             if (a.sub_bit && nvalid > 0 && (s_in_chunk & (kSub - 1)) == 0)
                 a.sub_bit[(sym0 + s_in_chunk) / kSub] = static_cast<uint32_t>(round_bit - cs + excl);
 
-            if (bits) emit_codes<LONG>(stage, round_bit - stage_bit0 + excl, ent);
+            if constexpr (LONG) {
+                if (bits) emit_codes<LONG>(stage, round_bit - stage_bit0 + excl, ent);
+            } else {
+                emit_codes_or<G>(stage, static_cast<uint32_t>(round_bit - stage_bit0 + excl), ent);
+            }
             wave_sync();
 
             const uint64_t end_bit = round_bit + tot;
@@ -258,8 +288,12 @@ hipError_t launch_pack(bool long_codes, const PackArgs& a, hipStream_t s) {
     const size_t lds = pack_lds_bytes(long_codes, a.stage_words);
     if (long_codes) {
         hipLaunchKernelGGL(k_pack<true>, dim3(a.grid), dim3(kThreads), lds, s, a);
+    } else if (a.max_len <= 8) {  // 4 codes per OR pair
+        hipLaunchKernelGGL((k_pack<false, 4>), dim3(a.grid), dim3(kThreads), lds, s, a);
+    } else if (a.max_len <= 16) {
+        hipLaunchKernelGGL((k_pack<false, 2>), dim3(a.grid), dim3(kThreads), lds, s, a);
     } else {
-        hipLaunchKernelGGL(k_pack<false>, dim3(a.grid), dim3(kThreads), lds, s, a);
+        hipLaunchKernelGGL((k_pack<false, 1>), dim3(a.grid), dim3(kThreads), lds, s, a);
     }
     return hipGetLastError();
 }
