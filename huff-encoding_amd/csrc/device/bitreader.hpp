@@ -27,6 +27,19 @@ __device__ __forceinline__ uint4 ld_nt(const uint4* p) {
     return make_uint4(v.x, v.y, v.z, v.w);
 }
 
+// inclusive prefix sum over the 64 lanes of a wave with DPP (no LDS round
+// trips): row_shr 1/2/4/8 within each 16-lane row, then row_bcast 15 / 31
+// carry the row totals upward. Lanes with no source read `old` = 0.
+__device__ __forceinline__ uint32_t wave_scan_incl(uint32_t x) {
+    x += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x111, 0xf, 0xf, false));
+    x += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x112, 0xf, 0xf, false));
+    x += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x114, 0xf, 0xf, false));
+    x += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x118, 0xf, 0xf, false));
+    x += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x142, 0xa, 0xf, false));
+    x += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x143, 0xc, 0xf, false));
+    return x;
+}
+
 // 16-byte streaming store
 __device__ __forceinline__ void st_nt(uint4* p, uint4 v) {
     u32x4_t w = {v.x, v.y, v.z, v.w};

@@ -10,7 +10,8 @@
 //   1. 16 lookups per lane in the LDS code table, replicated 32x as
 //      [letter][copy] (lane l reads copy l % 32: bank-conflict-free on any
 //      data);
-//   2. a wave-wide exclusive scan of the lanes' bit counts (DPP shuffles);
+//   2. a wave-wide exclusive scan of the lanes' bit counts (DPP row shifts
+//      and row broadcasts: no LDS round trips);
 //   3. each lane appends its codes to a 64-bit accumulator and emits 32-bit
 //      big-endian words into the wave's LDS staging image of the output: words
 //      wholly its own with ds_write, the two it shares with neighbours ds_or;
@@ -234,13 +235,8 @@ __global__ __launch_bounds__(kThreads) void k_pack(PackArgs a) {
                 bits += static_cast<uint32_t>(ent[k] & E::kMask);
             }
             // wave exclusive scan of the bit counts
-            uint32_t incl = bits;
-#pragma unroll
-            for (int d = 1; d < 64; d <<= 1) {
-                const uint32_t y = __shfl_up(incl, d, 64);
-                if (lane >= static_cast<uint32_t>(d)) incl += y;
-            }
-            const uint32_t tot = __shfl(incl, 63, 64);
+            const uint32_t incl = wave_scan_incl(bits);
+            const uint32_t tot = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(incl), 63));
             const uint32_t excl = incl - bits;
 
             if (a.sub_bit && nvalid > 0 && (s_in_chunk & (kSub - 1)) == 0)
