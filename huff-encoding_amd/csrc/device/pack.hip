@@ -6,19 +6,21 @@
 // (chunk_start = exclusive scan of per-chunk bit counts). Workgroups are
 // persistent (4 waves, grid sized to residency) so the code table is copied
 // into LDS once per workgroup; each wave then walks its chunks in rounds of
-// 1 KiB (64 lanes x 16 bytes) with no workgroup barrier:
-//   1. 16 lookups per lane in the LDS code table, replicated 32x as
+// 2 KiB (64 lanes x 32 consecutive bytes) with no workgroup barrier:
+//   1. 32 lookups per lane in the LDS code table, replicated 32x as
 //      [letter][copy] (lane l reads copy l % 32: bank-conflict-free on any
-//      data);
+//      data), summing the lane's bit count;
 //   2. a wave-wide exclusive scan of the lanes' bit counts (DPP row shifts
 //      and row broadcasts: no LDS round trips);
-//   3. each lane appends its codes to a 64-bit accumulator and emits 32-bit
-//      big-endian words into the wave's LDS staging image of the output: words
-//      wholly its own with ds_write, the two it shares with neighbours ds_or;
+//   3. codes <= 27 bits: groups of G codes (G * max_len <= 32) are joined in
+//      a register and ORed (ds_or) into the two 32-bit words of the wave's
+//      LDS staging image they can touch, each group at its own bit offset
+//      (no per-code branch, no serial dependence between groups). Codes
+//      > 27 bits: a 64-bit accumulator emitting whole words;
 //   4. complete 16-byte segments leave as one dwordx4 store per lane
 //      (byte-swapped: the stream is MSB-first); the partial last segment is
 //      carried to the next round.
-// Loads run 3 rounds (3 KiB per wave) ahead of the encoder.
+// Loads run 2 rounds (4 KiB per wave) ahead of the encoder.
 // A chunk's first output byte is shared with the previous chunk: the wave
 // recomputes the previous chunk's last <= 7 bits from the input bytes before
 // it (from prev_tail for the first chunk of a shard), so every output byte is
@@ -35,6 +37,13 @@ namespace {
 
 constexpr int kThreads = 256;
 constexpr int kWaves = kThreads / 64;
+constexpr uint32_t kBPL = kPackWaveRound / 64;  // consecutive input bytes per lane per round
+static_assert(kBPL % 16 == 0, "lanes load whole 16-byte pieces");
+constexpr int kPieces = kBPL / 16;
+
+struct LaneIn {
+    uint4 v[kPieces];
+};
 
 template <bool LONG>
 struct Entry;
@@ -55,7 +64,7 @@ struct Entry<true> {
 
 template <bool LONG>
 __device__ __forceinline__ void emit_codes(uint32_t* __restrict__ stage, uint64_t p,
-                                           const typename Entry<LONG>::T (&ent)[16]) {
+                                           const typename Entry<LONG>::T (&ent)[kBPL]) {
     using E = Entry<LONG>;
     uint32_t w = static_cast<uint32_t>(p >> 5);
     uint32_t nacc = static_cast<uint32_t>(p & 31);
@@ -75,7 +84,7 @@ __device__ __forceinline__ void emit_codes(uint32_t* __restrict__ stage, uint64_
         }
     };
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
+    for (int k = 0; k < static_cast<int>(kBPL); ++k) {
         const uint32_t len = static_cast<uint32_t>(ent[k] & E::kMask);
         const uint64_t code = static_cast<uint64_t>(ent[k] >> E::kShift);
         if (LONG && len > 32) {
@@ -100,12 +109,15 @@ __device__ __forceinline__ void emit_codes(uint32_t* __restrict__ stage, uint64_
 
 // short codes: groups of G consecutive codes (G * max_len <= 32) are joined
 // in a register and ORed into their (at most) two stage words at the group's
-// bit offset: no serial 64-bit accumulator, no per-code branch.
+// bit offset: no serial 64-bit accumulator, no per-code branch. An empty
+// entry past the chunk end has len 0 and code 0 and ORs zero. (Re-reading the
+// entries from the table here instead of keeping them live measured 30 %
+// slower.)
 template <int G>
-__device__ __forceinline__ void emit_codes_or(uint32_t* __restrict__ stage, uint32_t p, const uint32_t (&ent)[16]) {
+__device__ __forceinline__ void emit_codes_or(uint32_t* __restrict__ stage, uint32_t p, const uint32_t (&ent)[kBPL]) {
     uint32_t o = p;
 #pragma unroll
-    for (int k = 0; k < 16; k += G) {
+    for (int k = 0; k < static_cast<int>(kBPL); k += G) {
         uint32_t code = 0, len = 0;
 #pragma unroll
         for (int g = 0; g < G; ++g) {
@@ -115,7 +127,6 @@ __device__ __forceinline__ void emit_codes_or(uint32_t* __restrict__ stage, uint
         }
         const uint32_t s = o & 31u;
         // the group left-aligned at bit s of a 64-bit window starting at word o/32
-        // (an empty entry past the chunk end has len 0 and code 0: ORs zero)
         const uint64_t v = static_cast<uint64_t>(code) << ((64u - s - len) & 63u);
         uint32_t* w = stage + (o >> 5);
         __hip_atomic_fetch_or(w, static_cast<uint32_t>(v >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -181,10 +192,17 @@ __global__ __launch_bounds__(kThreads) void k_pack(PackArgs a) {
         const uint8_t* cin = a.in + sym0;
         const uint64_t cn = nsym;
 
-        // loads run 3 rounds ahead
-        uint4 v0 = load_lane(cin, cn, lane * 16);
-        uint4 v1 = nrounds > 1 ? load_lane(cin, cn, 1 * kPackWaveRound + lane * 16) : make_uint4(0, 0, 0, 0);
-        uint4 v2 = nrounds > 2 ? load_lane(cin, cn, 2 * kPackWaveRound + lane * 16) : make_uint4(0, 0, 0, 0);
+        // loads run 2 rounds ahead
+        auto load_round = [&](uint32_t r) {
+            LaneIn x;
+#pragma unroll
+            for (int q = 0; q < kPieces; ++q)
+                x.v[q] = r < nrounds ? load_lane(cin, cn, static_cast<uint64_t>(r) * kPackWaveRound + lane * kBPL + 16 * q)
+                                     : make_uint4(0, 0, 0, 0);
+            return x;
+        };
+        LaneIn v0 = load_round(0);
+        LaneIn v1 = load_round(1);
 
         // bits of the shared first byte that belong to the symbols before this chunk
         if (lane == 0 && (cs & 7)) {
@@ -217,21 +235,27 @@ __global__ __launch_bounds__(kThreads) void k_pack(PackArgs a) {
 
         uint64_t round_bit = cs;
         for (uint32_t r = 0; r < nrounds; ++r) {
-            const uint4 v = v0;
+            const LaneIn v = v0;
             v0 = v1;
-            v1 = v2;
-            if (r + 3 < nrounds) v2 = load_lane(cin, cn, static_cast<uint64_t>(r + 3) * kPackWaveRound + lane * 16);
-            const uint64_t s_in_chunk = static_cast<uint64_t>(r) * kPackWaveRound + lane * 16;
-            const int nvalid = s_in_chunk >= nsym ? 0 : (nsym - s_in_chunk >= 16 ? 16 : static_cast<int>(nsym - s_in_chunk));
+            if (r + 2 < nrounds) v1 = load_round(r + 2);
+            const uint64_t s_in_chunk = static_cast<uint64_t>(r) * kPackWaveRound + lane * kBPL;
+            const int nvalid = s_in_chunk >= nsym ? 0 : (nsym - s_in_chunk >= kBPL ? static_cast<int>(kBPL)
+                                                                                     : static_cast<int>(nsym - s_in_chunk));
 
-            T ent[16];
             uint32_t bits = 0;
-            const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+            uint32_t wv[4 * kPieces];
 #pragma unroll
-            for (int k = 0; k < 16; ++k) {
+            for (int q = 0; q < kPieces; ++q) {
+                wv[4 * q] = v.v[q].x;
+                wv[4 * q + 1] = v.v[q].y;
+                wv[4 * q + 2] = v.v[q].z;
+                wv[4 * q + 3] = v.v[q].w;
+            }
+            T ent[kBPL];
+#pragma unroll
+            for (int k = 0; k < static_cast<int>(kBPL); ++k) {
                 const uint32_t b = (wv[k >> 2] >> (8 * (k & 3))) & 0xFFu;
-                const T e = tab[(b << 5) | copy];
-                ent[k] = (k < nvalid) ? e : T(0);
+                ent[k] = (k < nvalid) ? tab[(b << 5) | copy] : T(0);
                 bits += static_cast<uint32_t>(ent[k] & E::kMask);
             }
             // wave exclusive scan of the bit counts

@@ -415,8 +415,9 @@ huff::Status huff_enc::pack(const huff_tree* t, uint64_t base, const uint8_t* pr
     a.sub_bit = static_cast<uint32_t*>(sub_bit.p);
     a.prev_tail = d_tab + 2304;
     a.prev_tail_len = static_cast<uint32_t>(prev_tail_len);
-    // one wave round is 1 KiB: <= 1024*maxlen bits + a < 128-bit carry
-    a.stage_words = (32 * std::max<uint32_t>(et.maxlen, 1) + 8 + 3) & ~3u;
+    // one wave round: <= kPackWaveRound*maxlen bits + a < 128-bit carry (+ the
+    // word after the last, which the OR emit may touch with zero)
+    a.stage_words = (huff::dev::kPackWaveRound / 32 * std::max<uint32_t>(et.maxlen, 1) + 8 + 3) & ~3u;
     a.max_len = et.maxlen;
     const size_t lds = huff::dev::pack_lds_bytes(ctx->tab_long, a.stage_words);
     const uint32_t per_cu = std::max<uint32_t>(1, std::min<uint32_t>(8, static_cast<uint32_t>((160 * 1024) / lds)));
