@@ -62,6 +62,10 @@ int huff_ctx_create(int device, huff_ctx** out) {
         // (where PyTorch allocates and fills tensors unless told otherwise)
         if (!st && hipStreamCreateWithFlags(&c->own, hipStreamDefault) != hipSuccess)
             st = huff::Status::err(HUFF_E_HIP, "hipStreamCreate failed");
+        if (!st && hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking) != hipSuccess)
+            st = huff::Status::err(HUFF_E_HIP, "hipStreamCreate failed");
+        if (!st && hipEventCreateWithFlags(&c->lut_free, hipEventDisableTiming) != hipSuccess)
+            st = huff::Status::err(HUFF_E_HIP, "hipEventCreate failed");
         if (st) {
             delete c;
             return st;
@@ -84,6 +88,11 @@ int huff_ctx_destroy(huff_ctx* ctx) {
         hipEventDestroy(p.b);
     }
     for (auto e : ctx->free_events) hipEventDestroy(e);
+    if (ctx->copy_stream) {
+        hipStreamSynchronize(ctx->copy_stream);
+        hipStreamDestroy(ctx->copy_stream);
+    }
+    if (ctx->lut_free) hipEventDestroy(ctx->lut_free);
     if (ctx->own) hipStreamDestroy(ctx->own);
     delete ctx;
     return HUFF_OK;

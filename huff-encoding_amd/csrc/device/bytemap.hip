@@ -47,7 +47,7 @@ __global__ __launch_bounds__(kThreads) void k_bytemap(BytemapArgs a) {
     }
     __builtin_amdgcn_sched_barrier(0);
     {  // lane t stages entry t into its 32 copies (one 128-B run)
-        const uint32_t e = (a.table[t] >> a.shift) & 0xFFu;
+        const uint32_t e = a.map[t];
         uint4* row = reinterpret_cast<uint4*>(tab + (t << 5));
 #pragma unroll
         for (int i = 0; i < 8; ++i) row[i] = make_uint4(e, e, e, e);

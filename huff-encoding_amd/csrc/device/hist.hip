@@ -10,8 +10,6 @@
 // chunk the 32 copies are summed (rotated reads, conflict-free) into the
 // per-chunk histogram row; the workgroup's totals go to one of 8 XCD-group
 // copies of the global weights with one atomic per bin.
-#include <cstdlib>
-
 #include "bitreader.hpp"
 
 namespace huff::dev {
@@ -112,7 +110,6 @@ __global__ __launch_bounds__(kThreads) void k_hist(const uint8_t* __restrict__ b
 // issued before the first count, the chunk's row is written, and the global
 // weights are summed from the rows afterwards (k_rows_sum) instead of with
 // per-workgroup atomics.
-template <int MODE>  // MODE 1: timing experiment only (no counting)
 __global__ __launch_bounds__(kThreads) void k_hist1(const uint8_t* __restrict__ base, uint64_t lo, uint64_t hi,
                                                     uint32_t* __restrict__ chunk_hist,
                                                     unsigned long long* __restrict__ gw) {
@@ -137,19 +134,12 @@ __global__ __launch_bounds__(kThreads) void k_hist1(const uint8_t* __restrict__ 
         // 16 loads stay in flight across it
         __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0), vmcnt/expcnt untouched
         __builtin_amdgcn_s_barrier();
-        if (MODE == 1) {
-            uint32_t x = 0;
 #pragma unroll
-            for (int r = 0; r < 16; ++r) x ^= v[r].x ^ v[r].y ^ v[r].z ^ v[r].w;
-            if (x == 0x9e3779b9u) h[t] = x;
-        } else {
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                count_word(h, v[r].x, lane32);
-                count_word(h, v[r].y, lane32);
-                count_word(h, v[r].z, lane32);
-                count_word(h, v[r].w, lane32);
-            }
+        for (int r = 0; r < 16; ++r) {
+            count_word(h, v[r].x, lane32);
+            count_word(h, v[r].y, lane32);
+            count_word(h, v[r].z, lane32);
+            count_word(h, v[r].w, lane32);
         }
     } else {
         __syncthreads();
@@ -194,7 +184,8 @@ __global__ __launch_bounds__(256) void k_rows_sum(const uint32_t* __restrict__ c
 
 // bits[c] = sum_b chunk_hist[c][b] * len[b]; one wave per chunk.
 __global__ __launch_bounds__(256) void k_chunk_bits(const uint32_t* __restrict__ chunk_hist, uint32_t nchunks,
-                                                    const uint8_t* __restrict__ len, uint64_t* __restrict__ bits) {
+                                                    CodeLens lens, uint64_t* __restrict__ bits) {
+    const uint8_t* len = lens.len;
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint32_t c = blockIdx.x * 4 + wave;
     if (c >= nchunks) return;
@@ -263,20 +254,7 @@ hipError_t launch_hist(const uint8_t* base, uint64_t lo, uint64_t hi, uint32_t n
                        unsigned long long* gw, hipStream_t s) {
     if (nchunks == 0) return hipSuccess;
     if (chunk_hist) {  // per-chunk rows wanted: one-shot grid, then the row sum
-        static const int mode = [] {
-            const char* e = std::getenv("HUFF_HIST_EXPERIMENT");
-            return e ? std::atoi(e) : 0;
-        }();
-        if (mode == 2) {
-            hipMemsetAsync(gw, 0, kHistCopies * 256 * 8, s);
-            uint32_t grid = nchunks < 1024 ? nchunks : 1024;
-            hipLaunchKernelGGL(k_hist, dim3(grid), dim3(kThreads), 0, s, base, lo, hi, nchunks, chunk_hist, gw);
-            return hipGetLastError();
-        }
-        if (mode == 1)
-            hipLaunchKernelGGL(k_hist1<1>, dim3(nchunks), dim3(kThreads), 0, s, base, lo, hi, chunk_hist, gw);
-        else
-            hipLaunchKernelGGL(k_hist1<0>, dim3(nchunks), dim3(kThreads), 0, s, base, lo, hi, chunk_hist, gw);
+        hipLaunchKernelGGL(k_hist1, dim3(nchunks), dim3(kThreads), 0, s, base, lo, hi, chunk_hist, gw);
         const uint32_t g = nchunks < 512 ? nchunks : 512;
         hipLaunchKernelGGL(k_rows_sum, dim3(g), dim3(256), 0, s, chunk_hist, nchunks, gw);
         return hipGetLastError();
@@ -288,7 +266,7 @@ hipError_t launch_hist(const uint8_t* base, uint64_t lo, uint64_t hi, uint32_t n
     return hipGetLastError();
 }
 
-hipError_t launch_chunk_bits(const uint32_t* chunk_hist, uint32_t nchunks, const uint8_t* len, uint64_t* bits,
+hipError_t launch_chunk_bits(const uint32_t* chunk_hist, uint32_t nchunks, const CodeLens& len, uint64_t* bits,
                              hipStream_t s) {
     if (nchunks == 0) return hipSuccess;
     hipLaunchKernelGGL(k_chunk_bits, dim3((nchunks + 3) / 4), dim3(256), 0, s, chunk_hist, nchunks, len, bits);

@@ -33,15 +33,23 @@ constexpr uint32_t kMsMaxBits = 12;
 constexpr uint32_t kMsSlow = 0x80000000u;
 
 
+// The code table travels in the kernel arguments (no upload copy on the
+// critical path between pass 1 and pass 2): u32 code << 5 | len for codes
+// <= 27 bits, u64 code << 6 | len up to 57 bits.
+union alignas(8) CodeTable {
+    uint32_t s[256];
+    uint64_t l[256];
+};
+
 struct PackArgs {
+    CodeTable table;
+    uint8_t prev_tail[8];         // right-aligned (prev_tail[7] precedes in[0])
     const uint8_t* in;
     uint64_t n;
-    const void* table;            // [256] u32 or u64 entries
     const uint64_t* chunk_start;  // [nchunks + 1], bits relative to out bit 0
     uint32_t nchunks;
     uint8_t* out;
     uint32_t* sub_bit;            // may be null
-    const uint8_t* prev_tail;     // 8 bytes, right-aligned (prev_tail[7] precedes in[0])
     uint32_t prev_tail_len;
     uint32_t stage_words;         // per wave
     uint32_t grid;                // persistent workgroups (4 waves each)
@@ -79,13 +87,12 @@ struct IndexlessArgs {
     uint64_t* c;                  // [nseg] symbol counts
 };
 
-// dst[i] = (table[src[i]] >> shift) & 0xFF (+ arithmetic restart index)
+// dst[i] = map[src[i]] (+ arithmetic restart index)
 struct BytemapArgs {
+    uint8_t map[256];
     const uint8_t* src;
     uint8_t* dst;
     uint64_t n;
-    const uint32_t* table;        // 256 entries
-    uint32_t shift;
     uint64_t* chunk_start;        // may be null
     uint32_t nchunks;
     uint64_t base_bits;
@@ -98,7 +105,10 @@ size_t decode_ms_lds_bytes(uint32_t mlut_bits, uint32_t rep_log2);
 
 hipError_t launch_hist(const uint8_t* base, uint64_t lo, uint64_t hi, uint32_t nchunks, uint32_t* chunk_hist,
                        unsigned long long* gw, hipStream_t s);
-hipError_t launch_chunk_bits(const uint32_t* chunk_hist, uint32_t nchunks, const uint8_t* len, uint64_t* bits,
+struct alignas(8) CodeLens {
+    uint8_t len[256];
+};
+hipError_t launch_chunk_bits(const uint32_t* chunk_hist, uint32_t nchunks, const CodeLens& len, uint64_t* bits,
                              hipStream_t s);
 hipError_t launch_scan(const uint64_t* bits, uint32_t nchunks, uint64_t base, uint64_t* start, hipStream_t s);
 hipError_t launch_pack(bool long_codes, const PackArgs& a, hipStream_t s);

@@ -171,7 +171,7 @@ __global__ __launch_bounds__(kThreads) void k_pack(PackArgs a) {
     uint32_t* stage = lds + E::kTableWords + wave * a.stage_words;
 
     // replicate the table: thread t writes copy t%32 of letters t/32 + 8i
-    const T* tg = reinterpret_cast<const T*>(a.table);
+    const T* tg = reinterpret_cast<const T*>(LONG ? static_cast<const void*>(a.table.l) : static_cast<const void*>(a.table.s));
 #pragma unroll 4
     for (int i = 0; i < 32; ++i) {
         const uint32_t e = (t >> 5) + 8 * i;

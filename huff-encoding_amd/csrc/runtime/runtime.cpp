@@ -250,38 +250,20 @@ huff::Status huff_ctx::sync() {
     return huff::Status::ok();
 }
 
-huff::Status huff_ctx::upload_enc_tables(const huff_tree* t, const uint8_t* prev_tail, size_t prev_tail_len) {
-    const huff::EncTables& et = t->enc_tables();
-    const bool long_codes = et.maxlen > huff::dev::kShortMaxLen;
-    HUFF_TRY(pin_tab.ensure(256 * 8 + 256 + 16));
-    uint8_t* h = static_cast<uint8_t*>(pin_tab.p);
-    if (long_codes) {
-        uint64_t* e = reinterpret_cast<uint64_t*>(h);
-        for (int b = 0; b < 256; ++b) e[b] = (et.code[b] << 6) | et.len[b];
-    } else {
-        uint32_t* e = reinterpret_cast<uint32_t*>(h);
-        for (int b = 0; b < 256; ++b) e[b] = static_cast<uint32_t>(et.code[b] << 5) | et.len[b];
-    }
-    std::memcpy(h + 2048, et.len, 256);
-    std::memset(h + 2304, 0, 8);
-    if (prev_tail_len) std::memcpy(h + 2304 + 8 - prev_tail_len, prev_tail, prev_tail_len);
-    HUFF_TRY(d_tab.ensure(2048 + 256 + 8));
-    HIP_TRY(hipMemcpyAsync(d_tab.p, h, 2048 + 256 + 8, hipMemcpyHostToDevice, stream));
-    HIP_TRY(hipEventRecord(pin_tab.ev, stream));
-    tab_tree_id = t->id;
-    tab_long = long_codes;
-    return huff::Status::ok();
-}
-
 huff::Status huff_ctx::upload_dec_tables(const huff_tree* t, const huff::DecTables** dt) {
     HUFF_TRY(t->dec_tables(dt));
     if (lut_tree_id == t->id) return huff::Status::ok();
     const size_t bytes = (*dt)->lut.size() * 4;
-    HUFF_TRY(pin_lut.ensure(bytes));
+    HUFF_TRY(pin_lut.ensure(bytes));  // waits until the previous upload has left it
     std::memcpy(pin_lut.p, (*dt)->lut.data(), bytes);
     HUFF_TRY(d_lut.ensure(bytes));
-    HIP_TRY(hipMemcpyAsync(d_lut.p, pin_lut.p, bytes, hipMemcpyHostToDevice, stream));
-    HIP_TRY(hipEventRecord(pin_lut.ev, stream));
+    // the copy runs on the side stream, beside what is already queued (the
+    // pack of this job), once the last kernel that read d_lut is done; the
+    // main stream waits for it before the next kernel
+    HIP_TRY(hipStreamWaitEvent(copy_stream, lut_free, 0));
+    HIP_TRY(hipMemcpyAsync(d_lut.p, pin_lut.p, bytes, hipMemcpyHostToDevice, copy_stream));
+    HIP_TRY(hipEventRecord(pin_lut.ev, copy_stream));
+    HIP_TRY(hipStreamWaitEvent(stream, pin_lut.ev, 0));
     lut_tree_id = t->id;
     return huff::Status::ok();
 }
@@ -372,9 +354,8 @@ huff::Status huff_enc::pack(const huff_tree* t, uint64_t base, const uint8_t* pr
     if (prev_tail_len > 8) return huff::Status::err(HUFF_E_INVALID_ARG, "prev_tail holds at most 8 bytes");
     HUFF_TRY(ctx->activate());
     hipStream_t s = ctx->stream;
-    HUFF_TRY(ctx->upload_enc_tables(t, prev_tail, prev_tail_len));
-    const uint8_t* d_tab = static_cast<const uint8_t*>(ctx->d_tab.p);
     const huff::EncTables& et = t->enc_tables();
+    const bool long_codes = et.maxlen > huff::dev::kShortMaxLen;
     if ((base & 7) == 0 && et.maxlen == 8 && !huff::fixed8_disabled()) {
         bool all8 = true;
         for (int b = 0; b < 256; ++b) all8 &= (w[b] == 0 || et.len[b] == 8);
@@ -383,8 +364,7 @@ huff::Status huff_enc::pack(const huff_tree* t, uint64_t base, const uint8_t* pr
             m.src = d_in;
             m.dst = d_out;
             m.n = n;
-            m.table = reinterpret_cast<const uint32_t*>(d_tab);
-            m.shift = 5;  // short entries are code << 5 | len
+            for (int b = 0; b < 256; ++b) m.map[b] = static_cast<uint8_t>(et.code[b]);
             m.chunk_start = static_cast<uint64_t*>(chunk_start.p);
             m.nchunks = nchunks;
             m.base_bits = 0;
@@ -397,8 +377,10 @@ huff::Status huff_enc::pack(const huff_tree* t, uint64_t base, const uint8_t* pr
             return huff::Status::ok();
         }
     }
+    huff::dev::CodeLens lens;
+    std::memcpy(lens.len, et.len, 256);
     HUFF_TRY(ctx->timed("chunk_bits", [&] {
-        return huff::dev::launch_chunk_bits(static_cast<const uint32_t*>(chunk_hist.p), nchunks, d_tab + 2048,
+        return huff::dev::launch_chunk_bits(static_cast<const uint32_t*>(chunk_hist.p), nchunks, lens,
                                             static_cast<uint64_t*>(chunk_bits.p), s);
     }));
     HUFF_TRY(ctx->timed("scan", [&] {
@@ -406,23 +388,26 @@ huff::Status huff_enc::pack(const huff_tree* t, uint64_t base, const uint8_t* pr
                                       static_cast<uint64_t*>(chunk_start.p), s);
     }));
     huff::dev::PackArgs a{};
+    if (long_codes)
+        for (int b = 0; b < 256; ++b) a.table.l[b] = (et.code[b] << 6) | et.len[b];
+    else
+        for (int b = 0; b < 256; ++b) a.table.s[b] = static_cast<uint32_t>(et.code[b] << 5) | et.len[b];
+    if (prev_tail_len) std::memcpy(a.prev_tail + 8 - prev_tail_len, prev_tail, prev_tail_len);
     a.in = d_in;
     a.n = n;
-    a.table = d_tab;
     a.chunk_start = static_cast<const uint64_t*>(chunk_start.p);
     a.nchunks = nchunks;
     a.out = d_out;
     a.sub_bit = static_cast<uint32_t*>(sub_bit.p);
-    a.prev_tail = d_tab + 2304;
     a.prev_tail_len = static_cast<uint32_t>(prev_tail_len);
     // one wave round: <= kPackWaveRound*maxlen bits + a < 128-bit carry (+ the
     // word after the last, which the OR emit may touch with zero)
     a.stage_words = (huff::dev::kPackWaveRound / 32 * std::max<uint32_t>(et.maxlen, 1) + 8 + 3) & ~3u;
     a.max_len = et.maxlen;
-    const size_t lds = huff::dev::pack_lds_bytes(ctx->tab_long, a.stage_words);
+    const size_t lds = huff::dev::pack_lds_bytes(long_codes, a.stage_words);
     const uint32_t per_cu = std::max<uint32_t>(1, std::min<uint32_t>(8, static_cast<uint32_t>((160 * 1024) / lds)));
     a.grid = std::max<uint32_t>(1, std::min<uint32_t>((nchunks + 3) / 4, ctx->cu_count * per_cu));
-    HUFF_TRY(ctx->timed("pack", [&] { return huff::dev::launch_pack(ctx->tab_long, a, s); }));
+    HUFF_TRY(ctx->timed("pack", [&] { return huff::dev::launch_pack(long_codes, a, s); }));
     packed = true;
     packed_tree_id = t->id;
     bit_base = base;
@@ -442,8 +427,7 @@ huff::Status huff_enc::decode(const huff_tree* t, const uint8_t* d_comp, uint64_
         m.src = d_comp;
         m.dst = d_out;
         m.n = n;
-        m.table = static_cast<const uint32_t*>(ctx->d_lut.p);  // entries (8 << 8) | letter
-        m.shift = 0;
+        for (int b = 0; b < 256; ++b) m.map[b] = static_cast<uint8_t>(dt->lut[b]);  // entries (8 << 8) | letter
         HUFF_TRY(ctx->timed("decode", [&] { return huff::dev::launch_bytemap(m, ctx->stream); }));
         return huff::Status::ok();
     }
@@ -479,6 +463,7 @@ huff::Status huff_enc::decode(const huff_tree* t, const uint8_t* d_comp, uint64_
     a.n = n;
     a.out = d_out;
     HUFF_TRY(ctx->timed("decode", [&] { return huff::dev::launch_decode(a, ctx->stream); }));
+    HIP_TRY(hipEventRecord(ctx->lut_free, ctx->stream));
     return huff::Status::ok();
 }
 
@@ -688,8 +673,7 @@ Status decode_indexless_dev(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_
         m.src = d_comp;
         m.dst = static_cast<uint8_t*>(out.p);
         m.n = nsym;
-        m.table = static_cast<const uint32_t*>(ctx->d_lut.p);
-        m.shift = 0;
+        for (int b = 0; b < 256; ++b) m.map[b] = static_cast<uint8_t>(dt->lut[b]);
         HIP_TRY(dev::launch_bytemap(m, ctx->stream));
         *nsym_out_alias = nsym;
         return Status::ok();
@@ -741,6 +725,7 @@ Status decode_indexless_dev(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_
     HUFF_TRY(ctx->sync());
     HUFF_TRY(out.ensure(total + 16));
     HIP_TRY(dev::launch_indexless_emit(a, static_cast<const uint64_t*>(off.p), static_cast<uint8_t*>(out.p), st));
+    HIP_TRY(hipEventRecord(ctx->lut_free, st));
     *nsym = total;
     return Status::ok();
 }

@@ -105,13 +105,13 @@ struct huff_ctx {
     int cu_count = 256;
     hipStream_t own = nullptr;
     hipStream_t stream = nullptr;
+    hipStream_t copy_stream = nullptr;  // table uploads beside the kernels
+    hipEvent_t lut_free = nullptr;      // after the last kernel that read d_lut
     PinnedBuf pin_w;     // weights readback
-    PinnedBuf pin_tab;   // code table / len table / prev tail upload
     PinnedBuf pin_lut;   // decode table upload
     DevBuf d_in, d_out;  // staging of the host-pointer API
-    DevBuf d_tab, d_len, d_tail, d_lut;
-    uint64_t tab_tree_id = 0, lut_tree_id = 0;
-    bool tab_long = false;
+    DevBuf d_lut;
+    uint64_t lut_tree_id = 0;
 
     // kernel timing
     struct Timed {
@@ -126,7 +126,6 @@ struct huff_ctx {
     huff::Status collect_timing();
 
     huff::Status activate() const;
-    huff::Status upload_enc_tables(const huff_tree* t, const uint8_t* prev_tail, size_t prev_tail_len);
     huff::Status upload_dec_tables(const huff_tree* t, const huff::DecTables** dt);
     huff::Status sync();
 };
