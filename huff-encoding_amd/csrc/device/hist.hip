@@ -198,38 +198,46 @@ __global__ __launch_bounds__(256) void k_chunk_bits(const uint32_t* __restrict__
     if (lane == 0) bits[c] = s;
 }
 
-// start[c] = base + sum_{c' < c} bits[c'], start[nchunks] = total end.
-__global__ __launch_bounds__(1024) void k_scan(const uint64_t* __restrict__ bits, uint32_t nchunks, uint64_t base,
-                                               uint64_t* __restrict__ start) {
-    // tiles of 1024 in index order; the next tile's values are loaded while
-    // the current one is scanned
-    __shared__ uint64_t wsum[2][16];
+// start[c] = base + sum_{c' < c} bits[c'], start[nchunks] = total end, in two
+// launches over tiles of 1024 chunks. A chunk has at most 65536 * 57 bits <
+// 2^22, so a tile's local prefix sums fit 32 bits and scan with DPP.
+// k_scan_tiles: tile-local exclusive prefix -> start[], tile total -> tsum[].
+__global__ __launch_bounds__(1024) void k_scan_tiles(const uint64_t* __restrict__ bits, uint32_t nchunks,
+                                                     uint64_t* __restrict__ start, uint64_t* __restrict__ tsum) {
+    __shared__ uint32_t wsum[16];
     const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
-    uint64_t carry = base;
-    uint64_t v_next = t < nchunks ? bits[t] : 0;
-    for (uint32_t tile = 0, k = 0; tile < nchunks; tile += 1024, k ^= 1) {
-        const uint64_t v = v_next;
-        const uint32_t i = tile + t;
-        v_next = (i + 1024 < nchunks) ? bits[i + 1024] : 0;
-        uint64_t incl = v;
+    const uint32_t i = blockIdx.x * 1024 + t;
+    const uint32_t v = i < nchunks ? static_cast<uint32_t>(bits[i]) : 0u;
+    const uint32_t incl = wave_scan_incl(v);
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    uint32_t pre = 0, tot = 0;
 #pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint64_t y = __shfl_up(incl, d, 64);
-            if (lane >= static_cast<uint32_t>(d)) incl += y;
-        }
-        if (lane == 63) wsum[k][wave] = incl;
-        __syncthreads();
-        uint64_t pre = carry, tot = 0;
-#pragma unroll
-        for (uint32_t w = 0; w < 16; ++w) {
-            const uint64_t x = wsum[k][w];
-            pre += (w < wave) ? x : 0;
-            tot += x;
-        }
-        if (i < nchunks) start[i] = pre + incl - v;
-        carry += tot;  // wsum[k] is rewritten only two tiles later, after a barrier
+    for (uint32_t w = 0; w < 16; ++w) {
+        pre += (w < wave) ? wsum[w] : 0u;
+        tot += wsum[w];
     }
-    if (t == 0) start[nchunks] = carry;
+    if (i < nchunks) start[i] = pre + incl - v;
+    if (t == 0) tsum[blockIdx.x] = tot;
+}
+
+// k_scan_fix: add base + the totals of the tiles before; the last tile also
+// writes start[nchunks]
+__global__ __launch_bounds__(1024) void k_scan_fix(uint32_t nchunks, uint64_t base, const uint64_t* __restrict__ tsum,
+                                                   uint64_t* __restrict__ start) {
+    __shared__ uint64_t off;
+    const uint32_t t = threadIdx.x;
+    if (t < 64) {  // one wave sums the tsum[q], q < blockIdx.x
+        uint64_t sum = 0;
+        for (uint32_t q = t; q < blockIdx.x; q += 64) sum += tsum[q];
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) sum += __shfl_down(sum, d, 64);
+        if (t == 0) off = base + sum;
+    }
+    __syncthreads();
+    const uint32_t i = blockIdx.x * 1024 + t;
+    if (i < nchunks) start[i] += off;
+    if (blockIdx.x == gridDim.x - 1 && t == 0) start[nchunks] = off + tsum[blockIdx.x];
 }
 
 // lowest index i with missing_mask[in[i]] != 0 (error path of compress_with_tree)
@@ -273,8 +281,11 @@ hipError_t launch_chunk_bits(const uint32_t* chunk_hist, uint32_t nchunks, const
     return hipGetLastError();
 }
 
-hipError_t launch_scan(const uint64_t* bits, uint32_t nchunks, uint64_t base, uint64_t* start, hipStream_t s) {
-    hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, s, bits, nchunks, base, start);
+hipError_t launch_scan(const uint64_t* bits, uint32_t nchunks, uint64_t base, uint64_t* start, uint64_t* tsum,
+                       hipStream_t s) {
+    const uint32_t tiles = nchunks ? (nchunks + 1023) / 1024 : 1;
+    hipLaunchKernelGGL(k_scan_tiles, dim3(tiles), dim3(1024), 0, s, bits, nchunks, start, tsum);
+    hipLaunchKernelGGL(k_scan_fix, dim3(tiles), dim3(1024), 0, s, nchunks, base, tsum, start);
     return hipGetLastError();
 }
 

@@ -110,7 +110,9 @@ struct alignas(8) CodeLens {
 };
 hipError_t launch_chunk_bits(const uint32_t* chunk_hist, uint32_t nchunks, const CodeLens& len, uint64_t* bits,
                              hipStream_t s);
-hipError_t launch_scan(const uint64_t* bits, uint32_t nchunks, uint64_t base, uint64_t* start, hipStream_t s);
+// tsum: scratch of ceil(nchunks / 1024) (>= 1) u64
+hipError_t launch_scan(const uint64_t* bits, uint32_t nchunks, uint64_t base, uint64_t* start, uint64_t* tsum,
+                       hipStream_t s);
 hipError_t launch_pack(bool long_codes, const PackArgs& a, hipStream_t s);
 hipError_t launch_decode(const DecodeArgs& a, hipStream_t s);
 hipError_t launch_decode_ring(const DecodeArgs& a, hipStream_t s);

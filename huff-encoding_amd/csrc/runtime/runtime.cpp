@@ -284,6 +284,7 @@ huff::Status huff_enc::init(huff_ctx* c, const uint8_t* d, uint64_t nbytes) {
     HUFF_TRY(gw.ensure(huff::dev::kHistCopies * 256 * 8));
     HUFF_TRY(chunk_bits.ensure(nc * 8));
     HUFF_TRY(chunk_start.ensure((nc + 1) * 8));
+    HUFF_TRY(tsum.ensure((nc / 1024 + 2) * 8));
     HUFF_TRY(sub_bit.ensure(((n + huff::dev::kSub - 1) / huff::dev::kSub + 1) * 4));
     HUFF_TRY(mask.ensure(256));
     HUFF_TRY(pos.ensure(8));
@@ -385,7 +386,7 @@ huff::Status huff_enc::pack(const huff_tree* t, uint64_t base, const uint8_t* pr
     }));
     HUFF_TRY(ctx->timed("scan", [&] {
         return huff::dev::launch_scan(static_cast<const uint64_t*>(chunk_bits.p), nchunks, base & 7,
-                                      static_cast<uint64_t*>(chunk_start.p), s);
+                                      static_cast<uint64_t*>(chunk_start.p), static_cast<uint64_t*>(tsum.p), s);
     }));
     huff::dev::PackArgs a{};
     if (long_codes)
@@ -718,8 +719,10 @@ Status decode_indexless_dev(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_
     }
     if (!settled) HIP_TRY(dev::launch_indexless_settle(a, xa, st));
     if (nseg > 0xFFFFFFFFull) return Status::err(HUFF_E_INVALID_ARG, "stream too long for one decode");
+    DevBuf tsum;
+    HUFF_TRY(tsum.ensure((nseg / 1024 + 2) * 8));
     HIP_TRY(dev::launch_scan(static_cast<const uint64_t*>(c.p), static_cast<uint32_t>(nseg), 0,
-                             static_cast<uint64_t*>(off.p), st));
+                             static_cast<uint64_t*>(off.p), static_cast<uint64_t*>(tsum.p), st));
     uint64_t total = 0;
     HIP_TRY(hipMemcpyAsync(&total, static_cast<uint64_t*>(off.p) + nseg, 8, hipMemcpyDeviceToHost, st));
     HUFF_TRY(ctx->sync());

@@ -135,7 +135,7 @@ struct huff_enc {
     const uint8_t* d_in = nullptr;
     uint64_t n = 0;
     uint32_t nchunks = 0;
-    DevBuf chunk_hist, gw, chunk_bits, chunk_start, sub_bit, mask, pos;
+    DevBuf chunk_hist, gw, chunk_bits, chunk_start, tsum, sub_bit, mask, pos;
     uint64_t w[256] = {};
     bool have_hist = false;
     // state of the last pack (for decode)
