@@ -77,6 +77,31 @@ def cpu_baseline(workload: str, target_s: float):
                       f"tree walk); oracle/huff_oracle.c restatement of huff_coding (Rust not buildable here)"}
 
 
+PHASE_KERNELS = {  # bench phase -> device kernels (names as in tools/summarize_prof.py)
+    "hist": ["k_hist1", "k_rows_sum"],
+    "chunk_bits": ["k_chunk_bits"],
+    "scan": ["k_scan_tiles", "k_scan_fix"],
+}
+
+
+def dominant_traffic(kind, phase, fixed8, dec_kernel):
+    """HBM bytes per launch of the dominant phase from the committed PMC
+    summary of this workload (profiles/traffic_<kind>.json, written by
+    tools/make_traffic.py from a rocprofv3 --pmc run of the same kernels)."""
+    path = os.path.join(ROOT, "profiles", f"traffic_{kind}.json")
+    if not os.path.exists(path):
+        return None, None
+    t = json.load(open(path))
+    names = PHASE_KERNELS.get(phase)
+    if phase == "pack":
+        names = ["k_bytemap"] if fixed8 else ["k_pack"]
+    elif phase == "decode":
+        names = ["k_bytemap"] if fixed8 else [dec_kernel or "k_decode_ring"]
+    if not names or not all(n in t for n in names):
+        return None, None
+    return int(sum(t[n]["hbm_bytes"] for n in names)), os.path.relpath(path, ROOT)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -165,6 +190,8 @@ def main():
     _, ln = tree.code_table()
     total = state["hists"].sum(axis=0, dtype=np.uint64)
     state["fixed8"] = bool((ln[total > 0] == 8).all()) and os.environ.get("HUFF_DISABLE_FIXED8", "0") in ("", "0")
+    maxlen = int(ln[total > 0].max())  # the decode kernel the runtime picks (runtime.cpp, huff_enc::decode)
+    state["dec_kernel"] = ("k_decode" if maxlen > 32 else "k_decode_ring" if bits < 7 * n else "k_decode_short")
     ms_per_step = elapsed * 1e3 / args.steps
     value = world * n / (elapsed / args.steps) / 1e9
     comp_bytes = (bits + 7) // 8
@@ -185,6 +212,7 @@ def main():
                           "GBps": round(b / (avg * 1e-3) / 1e9, 1)}
     dom = max(kernels, key=lambda k: kernels[k]["avg_ms"])
     ach = kernels[dom]["GBps"]
+    traffic, traffic_src = dominant_traffic(kind, dom, state.get("fixed8"), state.get("dec_kernel"))
     enc_ms = sum(kernels[k]["avg_ms"] for k in ("hist", "chunk_bits", "scan", "pack") if k in kernels)
     result = {
         "metric": METRIC,
@@ -204,7 +232,7 @@ def main():
                    "kernel_path": "fixed8 byte map (all codes 8 bits)" if state.get("fixed8") else "general bit pack/decode",
                    "parallelism": f"shard{world}", "collective": (f"all_gather int64[258] (weights + tail bytes) over {'RCCL' if args.dist_backend == 'nccl' else 'gloo (rehearsal)'}" if world > 1 else None)},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": ach, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                     "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": None},
+                     "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": traffic, "traffic_source": traffic_src},
         "kernels": kernels,
         "kernel_enc_GBps": round(n / (enc_ms * 1e-3) / 1e9, 1),
         "host_gap_ms": round(ms_per_step - sum(k["avg_ms"] for k in kernels.values()), 4),

@@ -1,7 +1,9 @@
 #!/usr/bin/env bash
-# One GPU-box session: parity tests, N=1 benches, a 2-rank rehearsal of the
-# N>1 path (gloo, both ranks on the one GPU), rocprofv3 profiles.
-#   tools/gpu_round.sh <tag> [skip-tests] [skip-prof]
+# One GPU-box session for the round's artifacts: parity tests, rocprofv3
+# profiles (kernel trace + separate PMC passes) per workload turned into
+# profiles/traffic_<w>.json, then the N=1 bench lines (with cpu_baseline) and a
+# 2-rank rehearsal of the N>1 path (gloo, both ranks on the one GPU).
+#   tools/gpu_round.sh <tag> [skip-tests]
 set -euo pipefail
 tag=${1:-dev}
 root=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -11,18 +13,18 @@ mkdir -p "$out"
 if [ "${2:-}" != "skip-tests" ]; then
   timeout -k 10 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider > "$out/gpu_tests.log" 2>&1
 fi
-timeout -k 10 400 python bench.py > "$out/bench_uniform.json" 2> "$out/bench_uniform.err"
-for w in zipf text; do
-  timeout -k 10 300 python bench.py --workload $w --no-cpu-baseline > "$out/bench_$w.json" 2> "$out/bench_$w.err"
+for w in uniform zipf text; do
+  bash tools/profile.sh all $w "${tag}_all_$w" > /dev/null
+  python tools/summarize_prof.py "gpurun_out/prof/${tag}_all_$w" > "$out/prof_all_$w.json"
+  python tools/make_traffic.py "$out/prof_all_$w.json" $w > /dev/null
+  cp "gpurun_out/prof/${tag}_all_$w/trace/run_kernel_stats.csv" "$out/kernel_stats_all_$w.csv"
+done
+for w in uniform zipf text; do
+  timeout -k 10 400 python bench.py --workload $w > "$out/bench_$w.json" 2> "$out/bench_$w.err"
 done
 HUFF_DISABLE_FIXED8=1 timeout -k 10 300 python bench.py --no-cpu-baseline > "$out/bench_uniform_general.json" 2> "$out/bench_uniform_general.err"
 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
   --master-port 29533 bench.py --gpus 2 --steps 5 --warmup 2 --workload text --bytes-per-gpu $((1<<28)) \
   --dist-backend gloo > "$out/bench_2rank_gloo.json" 2> "$out/bench_2rank_gloo.err"
-if [ "${3:-}" != "skip-prof" ]; then
-  for w in uniform zipf; do
-    bash tools/profile.sh all $w "${tag}_all_$w" > /dev/null
-    python tools/summarize_prof.py "gpurun_out/prof/${tag}_all_$w" > "$out/prof_all_$w.json"
-  done
-fi
+mkdir -p "$out/profiles_copy" && cp profiles/traffic_*.json "$out/profiles_copy/"
 echo "gpu_round $tag done"

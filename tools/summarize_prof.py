@@ -9,14 +9,16 @@ import csv
 import glob
 import json
 import os
+import re
 import sys
 from collections import defaultdict
 
 
 def short(name: str) -> str:
-    for k in ("k_hist", "k_chunk_bits", "k_scan", "k_pack", "k_decode", "k_spec", "k_fix", "k_emit", "k_gen", "k_bytemap", "k_settle", "k_find_first"):
-        if k in name:
-            return k + ("<long>" if "ILb1E" in name else "")
+    """the kernel's function name (k_hist1, k_decode_ring, ...), else a prefix"""
+    m = re.search(r"\b(k_[A-Za-z0-9_]+)", name)
+    if m:
+        return m.group(1) + ("<long>" if "<true" in name or "ILb1E" in name else "")
     return name[:40]
 
 
