@@ -20,23 +20,25 @@ constexpr int kThreads = 256;
 constexpr int kCopies = 32;
 
 
-__device__ __forceinline__ void count_word(uint32_t* h, uint32_t w, uint32_t lane32) {
+template <int LOGC = 5>
+__device__ __forceinline__ void count_word(uint32_t* h, uint32_t w, uint32_t lane_c) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         uint32_t b = (w >> (8 * k)) & 0xFFu;
-        __hip_atomic_fetch_add(&h[(b << 5) | lane32], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_fetch_add(&h[(b << LOGC) | lane_c], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
 }
 
+template <int LOGC = 5>
 __device__ __forceinline__ void count_masked(uint32_t* h, uint4 v, uint64_t off, uint64_t lo, uint64_t hi,
-                                             uint32_t lane32) {
+                                             uint32_t lane_c) {
     uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
         uint64_t g = off + k;
         if (g >= lo && g < hi) {
             uint32_t b = (w[k >> 2] >> (8 * (k & 3))) & 0xFFu;
-            __hip_atomic_fetch_add(&h[(b << 5) | lane32], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_fetch_add(&h[(b << LOGC) | lane_c], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
     }
 }
@@ -110,57 +112,59 @@ __global__ __launch_bounds__(kThreads) void k_hist(const uint8_t* __restrict__ b
 // issued before the first count, the chunk's row is written, and the global
 // weights are summed from the rows afterwards (k_rows_sum) instead of with
 // per-workgroup atomics.
+template <int LOGC>
 __global__ __launch_bounds__(kThreads) void k_hist1(const uint8_t* __restrict__ base, uint64_t lo, uint64_t hi,
                                                     uint32_t* __restrict__ chunk_hist,
                                                     unsigned long long* __restrict__ gw) {
+    constexpr uint32_t C = 1u << LOGC;  // LDS copies of the histogram
     if (blockIdx.x == 0)  // k_rows_sum (next on the stream) accumulates into gw
         for (uint32_t i = threadIdx.x; i < kHistCopies * 256; i += kThreads) gw[i] = 0;
-    __shared__ __attribute__((aligned(16))) uint32_t h[256 * kCopies];
+    __shared__ __attribute__((aligned(16))) uint32_t h[256 * C];
     const uint32_t t = threadIdx.x;
-    const uint32_t lane32 = t & 31;
-    uint4* h4 = reinterpret_cast<uint4*>(h);
-#pragma unroll
-    for (int i = 0; i < 256 * kCopies / 4 / kThreads; ++i) h4[t + i * kThreads] = make_uint4(0, 0, 0, 0);
+    const uint32_t lane_c = t & (C - 1);
     const uint32_t c = blockIdx.x;
     const uint64_t cbeg = static_cast<uint64_t>(c) * kChunk;
     const bool full = cbeg >= lo && cbeg + kChunk <= hi;
+    uint4 v[16];
     if (full) {
         const uint4* p = reinterpret_cast<const uint4*>(base + cbeg) + t;
-        uint4 v[16];
 #pragma unroll
         for (int r = 0; r < 16; ++r) v[r] = ld_nt(p + r * kThreads);
-        __builtin_amdgcn_sched_barrier(0);  // no use of v[] hoisted above the last load
-        // LDS zeroing done everywhere; a bare barrier (no fence) so the
-        // 16 loads stay in flight across it
-        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0), vmcnt/expcnt untouched
-        __builtin_amdgcn_s_barrier();
+    }
+    __builtin_amdgcn_sched_barrier(0);  // loads first, no use of v[] hoisted above them
+    uint4* h4 = reinterpret_cast<uint4*>(h);
+#pragma unroll
+    for (uint32_t i = 0; i < 256 * C / 4 / kThreads; ++i) h4[t + i * kThreads] = make_uint4(0, 0, 0, 0);
+    // a bare barrier (no fence): the LDS zeroing is complete, the loads stay in flight
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0), vmcnt/expcnt untouched
+    __builtin_amdgcn_s_barrier();
+    if (full) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-            count_word(h, v[r].x, lane32);
-            count_word(h, v[r].y, lane32);
-            count_word(h, v[r].z, lane32);
-            count_word(h, v[r].w, lane32);
+            count_word<LOGC>(h, v[r].x, lane_c);
+            count_word<LOGC>(h, v[r].y, lane_c);
+            count_word<LOGC>(h, v[r].z, lane_c);
+            count_word<LOGC>(h, v[r].w, lane_c);
         }
     } else {
-        __syncthreads();
         for (int r = 0; r < 16; ++r) {
             const uint64_t off = cbeg + static_cast<uint64_t>(r) * kRound + t * 16;
             if (off + 16 <= lo || off >= hi) continue;
-            uint4 v;
+            uint4 x;
             if (off + 16 <= hi) {
-                v = *reinterpret_cast<const uint4*>(base + off);
+                x = *reinterpret_cast<const uint4*>(base + off);
             } else {  // never read past hi
                 uint32_t w[4] = {0, 0, 0, 0};
                 for (int k = 0; off + k < hi; ++k) w[k >> 2] |= static_cast<uint32_t>(base[off + k]) << (8 * (k & 3));
-                v = make_uint4(w[0], w[1], w[2], w[3]);
+                x = make_uint4(w[0], w[1], w[2], w[3]);
             }
-            count_masked(h, v, off, lo, hi, lane32);
+            count_masked<LOGC>(h, x, off, lo, hi, lane_c);
         }
     }
     __syncthreads();
     uint32_t s = 0;
 #pragma unroll 8
-    for (int j = 0; j < kCopies; ++j) s += h[(t << 5) | ((j + t) & 31)];
+    for (uint32_t j = 0; j < C; ++j) s += h[(t << LOGC) | ((j + t) & (C - 1))];
     chunk_hist[static_cast<uint64_t>(c) * 256 + t] = s;
 }
 
@@ -262,7 +266,9 @@ hipError_t launch_hist(const uint8_t* base, uint64_t lo, uint64_t hi, uint32_t n
                        unsigned long long* gw, hipStream_t s) {
     if (nchunks == 0) return hipSuccess;
     if (chunk_hist) {  // per-chunk rows wanted: one-shot grid, then the row sum
-        hipLaunchKernelGGL(k_hist1, dim3(nchunks), dim3(kThreads), 0, s, base, lo, hi, chunk_hist, gw);
+        // 32 copies: 16 measured equal on uniform bytes and 20 % slower on
+        // Zipf (same-address conflicts between lanes l and l + 16)
+        hipLaunchKernelGGL(k_hist1<5>, dim3(nchunks), dim3(kThreads), 0, s, base, lo, hi, chunk_hist, gw);
         const uint32_t g = nchunks < 512 ? nchunks : 512;
         hipLaunchKernelGGL(k_rows_sum, dim3(g), dim3(256), 0, s, chunk_hist, nchunks, gw);
         return hipGetLastError();

@@ -291,6 +291,43 @@ def test_shard_stitching_on_one_gpu(H, O, ctx):
     assert base == total and got.size == want.size and (got == want).all()
 
 
+def test_back_to_back_jobs_different_trees(H, O, ctx):
+    """several encode/decode jobs with different trees queued on one context
+    without host synchronisation in between: the decode tables (uploaded on a
+    side stream while the pack runs) must never be overwritten under a decode
+    that still reads them"""
+    import torch
+
+    rng = np.random.default_rng(12)
+    n = 3 * 65536 + 777
+    datas = [np.minimum(rng.geometric(p, n), 255).astype(np.uint8) for p in (0.05, 0.3, 0.6, 0.12)]
+    datas.append(rng.integers(0, 256, n, dtype=np.uint8))  # all-8-bit codes: byte map
+    xs, outs, decs, jobs, trees = [], [], [], [], []
+    for d in datas:
+        x = torch.from_numpy(d).cuda()
+        xs.append(x)
+        job = H.EncodeJob(ctx, x.data_ptr(), n)
+        jobs.append(job)
+    # pass 1 for all (host waits for weights), then pass 2 + decode for all, no sync
+    hists = [job.hist() for job in jobs]
+    for job, w in zip(jobs, hists):
+        out = torch.zeros(2 * n + 128, dtype=torch.uint8, device="cuda")
+        tree, _, bits = job.pack_shards(w[None, :], 0, [b""], out.data_ptr(), out.numel())
+        dec = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
+        job.decode(tree, out.data_ptr(), dec.data_ptr())
+        outs.append((out, bits))
+        decs.append(dec)
+        trees.append(tree)
+    torch.cuda.synchronize()
+    for d, (out, bits), dec, w in zip(datas, outs, decs, hists):
+        ot = O.Tree.from_weights(O.weights_from_array(w))
+        code, ln = ot.code_table()
+        want, wb = O.fast_encode(d, code, ln, threads=4)
+        assert wb == bits
+        assert (out[: (bits + 7) // 8].cpu().numpy() == want).all()
+        assert (dec[:n].cpu().numpy() == d).all()
+
+
 def test_pack_shards_on_one_gpu(H, O, ctx):
     """huff_enc_pack_shards (native tree + bit base + tail, then pack) for 4
     shards, one of them shorter than 8 bytes: the owned bytes concatenate to
