@@ -105,8 +105,8 @@ def dominant_traffic(kind, phase, fixed8, dec_kernel):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="uniform", choices=sorted(WORKLOADS))
     ap.add_argument("--bytes-per-gpu", type=int, default=1 << 30)
     ap.add_argument("--no-cpu-baseline", action="store_true")

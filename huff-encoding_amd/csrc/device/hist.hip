@@ -186,6 +186,19 @@ __global__ __launch_bounds__(256) void k_rows_sum(const uint32_t* __restrict__ c
     if (s) atomicAdd(&gw[(blockIdx.x % kHistCopies) * 256 + t], static_cast<unsigned long long>(s));
 }
 
+// Pass 1's result straight to pinned host memory: word b = total of bin b
+// with the launch's 16-bit sequence tag in bits 48..63 (totals < 2^48). Each
+// word is one 8-byte store, so the host, polling until all 256 tags match,
+// needs no fence, no flag and no device-to-host copy.
+__global__ __launch_bounds__(256) void k_hist_publish(const unsigned long long* __restrict__ gw,
+                                                      unsigned long long* host, uint64_t tag) {
+    const uint32_t t = threadIdx.x;
+    uint64_t tot = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kHistCopies; ++k) tot += gw[k * 256 + t];
+    __hip_atomic_store(&host[t], (tag << 48) | tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // bits[c] = sum_b chunk_hist[c][b] * len[b]; one wave per chunk.
 __global__ __launch_bounds__(256) void k_chunk_bits(const uint32_t* __restrict__ chunk_hist, uint32_t nchunks,
                                                     CodeLens lens, uint64_t* __restrict__ bits) {
@@ -263,7 +276,7 @@ __global__ __launch_bounds__(256) void k_find_first(const uint8_t* __restrict__ 
 }  // namespace
 
 hipError_t launch_hist(const uint8_t* base, uint64_t lo, uint64_t hi, uint32_t nchunks, uint32_t* chunk_hist,
-                       unsigned long long* gw, hipStream_t s) {
+                       unsigned long long* gw, hipStream_t s, HistDone done) {
     if (nchunks == 0) return hipSuccess;
     if (chunk_hist) {  // per-chunk rows wanted: one-shot grid, then the row sum
         // 32 copies: 16 measured equal on uniform bytes and 20 % slower on
@@ -271,6 +284,7 @@ hipError_t launch_hist(const uint8_t* base, uint64_t lo, uint64_t hi, uint32_t n
         hipLaunchKernelGGL(k_hist1<5>, dim3(nchunks), dim3(kThreads), 0, s, base, lo, hi, chunk_hist, gw);
         const uint32_t g = nchunks < 512 ? nchunks : 512;
         hipLaunchKernelGGL(k_rows_sum, dim3(g), dim3(256), 0, s, chunk_hist, nchunks, gw);
+        if (done.host) hipLaunchKernelGGL(k_hist_publish, dim3(1), dim3(256), 0, s, gw, done.host, done.tag);
         return hipGetLastError();
     }
     uint32_t grid = nchunks < 1024 ? nchunks : 1024;

@@ -103,8 +103,14 @@ size_t pack_lds_bytes(bool long_codes, uint32_t stage_words);
 size_t decode_lds_bytes(uint32_t lut_bits, uint32_t rep_log2);
 size_t decode_ms_lds_bytes(uint32_t mlut_bits, uint32_t rep_log2);
 
+// Pass 1's totals straight to pinned host memory (device-visible pointer):
+// host[b] = (tag << 48) | total_b. host == nullptr: the totals stay in gw.
+struct HistDone {
+    unsigned long long* host = nullptr;
+    uint64_t tag = 0;  // 16 bits
+};
 hipError_t launch_hist(const uint8_t* base, uint64_t lo, uint64_t hi, uint32_t nchunks, uint32_t* chunk_hist,
-                       unsigned long long* gw, hipStream_t s);
+                       unsigned long long* gw, hipStream_t s, HistDone done = HistDone{});
 struct alignas(8) CodeLens {
     uint8_t len[256];
 };

@@ -274,6 +274,8 @@ huff::Status huff_ctx::upload_dec_tables(const huff_tree* t, const huff::DecTabl
 huff::Status huff_enc::init(huff_ctx* c, const uint8_t* d, uint64_t nbytes) {
     if (reinterpret_cast<uintptr_t>(d) & 15)
         return huff::Status::err(HUFF_E_INVALID_ARG, "device input must be 16-byte aligned");
+    if (nbytes >= (1ull << 48))  // pass 1 publishes 48-bit totals (hist.hip, k_hist_publish)
+        return huff::Status::err(HUFF_E_INVALID_ARG, "one job holds fewer than 2^48 bytes");
     ctx = c;
     d_in = d;
     n = nbytes;
@@ -282,6 +284,7 @@ huff::Status huff_enc::init(huff_ctx* c, const uint8_t* d, uint64_t nbytes) {
     const size_t nc = std::max<uint32_t>(nchunks, 1);
     HUFF_TRY(chunk_hist.ensure(nc * 256 * 4));
     HUFF_TRY(gw.ensure(huff::dev::kHistCopies * 256 * 8));
+
     HUFF_TRY(chunk_bits.ensure(nc * 8));
     HUFF_TRY(chunk_start.ensure((nc + 1) * 8));
     HUFF_TRY(tsum.ensure((nc / 1024 + 2) * 8));
@@ -294,19 +297,40 @@ huff::Status huff_enc::init(huff_ctx* c, const uint8_t* d, uint64_t nbytes) {
 huff::Status huff_enc::hist() {
     HUFF_TRY(ctx->activate());
     hipStream_t s = ctx->stream;
+    if (nchunks == 0) {
+        for (int b = 0; b < 256; ++b) w[b] = 0;
+        have_hist = true;
+        packed = false;
+        return huff::Status::ok();
+    }
+    HUFF_TRY(ctx->pin_w.ensure(256 * 8));
+    if (!ctx->pin_w_dev) {
+        std::memset(ctx->pin_w.p, 0, 256 * 8);
+        HIP_TRY(hipHostGetDevicePointer(&ctx->pin_w_dev, ctx->pin_w.p, 0));
+    }
+    huff::dev::HistDone done;
+    done.host = static_cast<unsigned long long*>(ctx->pin_w_dev);
+    ctx->hist_seq = (ctx->hist_seq % 0xFFFF) + 1;  // 1..65535: never the zeroed buffer's tag
+    done.tag = ctx->hist_seq;
+    const uint64_t* hw = static_cast<const uint64_t*>(ctx->pin_w.p);
     HUFF_TRY(ctx->timed("hist", [&] {
         return huff::dev::launch_hist(d_in, 0, n, nchunks, static_cast<uint32_t*>(chunk_hist.p),
-                                      static_cast<unsigned long long*>(gw.p), s);
+                                      static_cast<unsigned long long*>(gw.p), s, done);
     }));
-    HUFF_TRY(ctx->pin_w.ensure(huff::dev::kHistCopies * 256 * 8));
-    HIP_TRY(hipMemcpyAsync(ctx->pin_w.p, gw.p, huff::dev::kHistCopies * 256 * 8, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipEventRecord(ctx->pin_w.ev, s));
-    HUFF_TRY(ctx->pin_w.wait());
-    const uint64_t* h = static_cast<const uint64_t*>(ctx->pin_w.p);
-    for (int b = 0; b < 256; ++b) {
-        uint64_t s8 = 0;
-        for (uint32_t k = 0; k < huff::dev::kHistCopies; ++k) s8 += h[k * 256 + b];
-        w[b] = s8;
+    // every word carries the launch's tag once written (k_hist_publish)
+    int b = 0;
+    for (uint64_t spin = 0; b < 256; ++spin) {
+        const uint64_t v = __atomic_load_n(&hw[b], __ATOMIC_ACQUIRE);
+        if ((v >> 48) == done.tag) {
+            w[b++] = v & ((1ull << 48) - 1);
+            continue;
+        }
+        if ((spin & 1023) == 1023) {
+            const hipError_t q = hipStreamQuery(s);
+            if (q == hipSuccess && (__atomic_load_n(&hw[b], __ATOMIC_ACQUIRE) >> 48) != done.tag)
+                return huff::Status::err(HUFF_E_HIP, "pass 1 finished without publishing its weights");
+            if (q != hipSuccess && q != hipErrorNotReady) HIP_TRY(q);
+        }
     }
     have_hist = true;
     packed = false;

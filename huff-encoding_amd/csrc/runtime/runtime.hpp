@@ -107,7 +107,9 @@ struct huff_ctx {
     hipStream_t stream = nullptr;
     hipStream_t copy_stream = nullptr;  // table uploads beside the kernels
     hipEvent_t lut_free = nullptr;      // after the last kernel that read d_lut
-    PinnedBuf pin_w;     // weights readback
+    PinnedBuf pin_w;     // weights readback: 256 tagged totals written by pass 1
+    void* pin_w_dev = nullptr;
+    uint64_t hist_seq = 0;
     PinnedBuf pin_lut;   // decode table upload
     DevBuf d_in, d_out;  // staging of the host-pointer API
     DevBuf d_lut;
