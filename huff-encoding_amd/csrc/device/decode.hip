@@ -25,7 +25,6 @@ namespace {
 constexpr int kThreads = 256;
 constexpr uint32_t kPhase = 64;                    // symbols per lane per phase
 constexpr uint32_t kStageStride = kPhase / 4 + 1;  // words per lane row (+1: bank spread)
-constexpr uint32_t kInStride = 17;                 // k_decode_ms input row: 16 dwords + 1
 
 // one 16-byte slot of the stream (zero past the end, never read past it)
 __device__ __forceinline__ uint4 load_slot(const uint8_t* __restrict__ comp, uint64_t nbytes, uint64_t s) {
@@ -41,37 +40,6 @@ __device__ __forceinline__ uint4 load_slot(const uint8_t* __restrict__ comp, uin
         else w |= v;
     }
     return make_uint4(x, y, z, w);
-}
-
-// one 64-byte unit of the stream as 4 x 16 B. Fast path: the whole unit is
-// inside the stream. Otherwise dword-granular: dwords that start inside the
-// stream are read (the stream is 4-B aligned, so a dword never crosses the
-// end of its allocation), bytes past the end may hold anything: the decoder
-// never turns bits past the last symbol into output.
-struct Unit {
-    uint4 a, b, c, d;
-};
-
-__device__ __forceinline__ Unit load_unit(const uint8_t* __restrict__ comp, uint64_t nbytes, uint64_t u) {
-    const uint64_t b = u * 64;
-    const uint4* p = reinterpret_cast<const uint4*>(comp + b);
-    Unit r;
-    if (b + 64 <= nbytes) {
-        r.a = p[0];
-        r.b = p[1];
-        r.c = p[2];
-        r.d = p[3];
-    } else {
-        uint32_t w[16];
-        const uint32_t* q = reinterpret_cast<const uint32_t*>(comp + b);
-#pragma unroll
-        for (int i = 0; i < 16; ++i) w[i] = (b + 4 * i < nbytes) ? q[i] : 0u;
-        r.a = make_uint4(w[0], w[1], w[2], w[3]);
-        r.b = make_uint4(w[4], w[5], w[6], w[7]);
-        r.c = make_uint4(w[8], w[9], w[10], w[11]);
-        r.d = make_uint4(w[12], w[13], w[14], w[15]);
-    }
-    return r;
 }
 
 // Generic variant (any code length <= 57): per-lane 4 x 16-B ring, global
@@ -325,278 +293,6 @@ __global__ __launch_bounds__(kThreads) void k_decode_short(DecodeArgs a) {
 }
 
 
-// Multi-symbol variant (every code <= 32 bits; the default). Per lane:
-//  - one lookup of the top K (= 12) window bits in a multi-symbol table in
-//    LDS yields up to 3 letters and the bits they use (a K-bit walk of the
-//    tree from the root, restarting after each leaf); only a code longer than
-//    K bits falls back to the single-symbol tables (global, L2-resident);
-//  - two lookups per refill check: after a refill the window holds >= 32
-//    bits, enough for two K-bit lookups;
-//  - input: 64-byte units; the current unit sits in a lane-private LDS row
-//    and the next one in registers (loaded a unit ahead), so a refill is one
-//    ds_read of the dword after the one just consumed, prefetched a refill
-//    ahead;
-//  - output: letters gather in a 64-bit accumulator, whole dwords go to a
-//    lane-private LDS row, which leaves as whole 4*OUTDW-byte pieces.
-template <uint32_t OUTDW>
-__global__ __launch_bounds__(kThreads) void k_decode_ms(DecodeArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    const uint32_t K = a.mlut_bits;
-    const uint32_t LR = a.lut_rep_log2;
-    const uint32_t nent = (1u << K) << LR;
-    uint32_t* mlut = lds;
-    uint32_t* inrows = lds + ((nent + 3) & ~3u);
-    uint32_t* outrows = inrows + kThreads * kInStride;
-    const uint32_t t = threadIdx.x;
-    for (uint32_t i = t; i < nent; i += kThreads) mlut[i] = a.mlut[i >> LR];
-    __syncthreads();
-
-    const uint32_t rep = t & ((1u << LR) - 1);
-    const uint32_t c = blockIdx.x;
-    const uint64_t sym0 = static_cast<uint64_t>(c) * kChunk;
-    const uint64_t nsym = (a.n - sym0 < kChunk) ? a.n - sym0 : kChunk;
-    const uint64_t lsym0 = static_cast<uint64_t>(t) * kSub;
-    const uint32_t cnt = lsym0 >= nsym ? 0u : static_cast<uint32_t>(nsym - lsym0 < kSub ? nsym - lsym0 : kSub);
-    if (cnt == 0) return;  // no barrier follows
-
-    const uint64_t pos = a.chunk_start[c] + a.sub_bit[(sym0 + lsym0) / kSub];
-    uint8_t* dst = a.out + sym0 + lsym0;
-    uint32_t* irow = inrows + t * kInStride;
-    uint32_t* orow = outrows + t * (OUTDW + 1);
-    const uint32_t Ks = a.lut_bits;
-    const uint32_t* glut = a.lut;
-
-    uint64_t unit = pos >> 9;  // 64-byte units
-    {
-        const Unit A = load_unit(a.comp, a.comp_bytes, unit);
-        irow[0] = A.a.x; irow[1] = A.a.y; irow[2] = A.a.z; irow[3] = A.a.w;
-        irow[4] = A.b.x; irow[5] = A.b.y; irow[6] = A.b.z; irow[7] = A.b.w;
-        irow[8] = A.c.x; irow[9] = A.c.y; irow[10] = A.c.z; irow[11] = A.c.w;
-        irow[12] = A.d.x; irow[13] = A.d.y; irow[14] = A.d.z; irow[15] = A.d.w;
-    }
-    Unit B = load_unit(a.comp, a.comp_bytes, unit + 1);
-    const uint32_t drop = static_cast<uint32_t>(pos & 511);
-    uint32_t wi = drop >> 5;
-    uint32_t nextw = irow[wi];
-    uint64_t buf = 0;
-    uint32_t nb = 0;
-
-#define MS_ADVANCE()                                                                   \
-    do {                                                                               \
-        if (++wi == 16) {                                                              \
-            irow[0] = B.a.x; irow[1] = B.a.y; irow[2] = B.a.z; irow[3] = B.a.w;        \
-            irow[4] = B.b.x; irow[5] = B.b.y; irow[6] = B.b.z; irow[7] = B.b.w;        \
-            irow[8] = B.c.x; irow[9] = B.c.y; irow[10] = B.c.z; irow[11] = B.c.w;      \
-            irow[12] = B.d.x; irow[13] = B.d.y; irow[14] = B.d.z; irow[15] = B.d.w;    \
-            ++unit;                                                                    \
-            B = load_unit(a.comp, a.comp_bytes, unit + 1);                             \
-            wi = 0;                                                                    \
-        }                                                                              \
-        nextw = irow[wi];                                                              \
-    } while (0)
-
-#define MS_REFILL()                                                                    \
-    do {                                                                               \
-        if (nb < 32) {                                                                 \
-            buf |= static_cast<uint64_t>(__builtin_bswap32(nextw)) << (32 - nb);       \
-            nb += 32;                                                                  \
-            MS_ADVANCE();                                                              \
-        }                                                                              \
-    } while (0)
-
-    MS_REFILL();
-    {
-        const uint32_t sh = drop & 31;
-        buf <<= sh;
-        nb -= sh;
-    }
-    uint64_t acc = 0;
-    uint32_t fill = 0, dwn = 0, j = 0;
-
-#define MS_STEP()                                                                      \
-    do {                                                                               \
-        if (j < cnt) {                                                                 \
-            uint32_t e = mlut[(static_cast<uint32_t>(buf >> (64 - K)) << LR) | rep];   \
-            uint32_t used, cn, syms;                                                   \
-            if (e & kMsSlow) {                                                         \
-                MS_REFILL();                                                           \
-                uint32_t e1 = glut[static_cast<uint32_t>(buf >> (64 - Ks))];           \
-                uint32_t d = Ks;                                                       \
-                while (e1 & kLutPtr) {                                                 \
-                    const uint32_t idx = static_cast<uint32_t>((buf >> (56 - d)) & 0xFFu); \
-                    e1 = glut[(e1 & ~kLutPtr) + idx];                                  \
-                    d += 8;                                                            \
-                }                                                                      \
-                used = (e1 >> 8) & 0xFFu;                                              \
-                cn = 1;                                                                \
-                syms = e1 & 0xFFu;                                                     \
-            } else {                                                                   \
-                used = (e >> 24) & 31u;                                                \
-                cn = (e >> 29) & 3u;                                                   \
-                syms = e & 0xFFFFFFu;                                                  \
-            }                                                                          \
-            buf <<= used;                                                              \
-            nb -= used;                                                                \
-            const uint32_t rem = cnt - j;                                              \
-            if (cn > rem) {                                                            \
-                cn = rem;                                                              \
-                syms &= (1u << (8 * cn)) - 1u;                                         \
-            }                                                                          \
-            acc |= static_cast<uint64_t>(syms) << (8 * fill);                          \
-            fill += cn;                                                                \
-            j += cn;                                                                   \
-            if (fill >= 4) {                                                           \
-                orow[dwn & (OUTDW - 1)] = static_cast<uint32_t>(acc);                  \
-                acc >>= 32;                                                            \
-                fill -= 4;                                                             \
-                ++dwn;                                                                 \
-                if ((dwn & (OUTDW - 1)) == 0) {                                        \
-                    uint4* d4 = reinterpret_cast<uint4*>(dst + (dwn - OUTDW) * 4);     \
-                    _Pragma("unroll") for (uint32_t q = 0; q < OUTDW / 4; ++q)         \
-                        d4[q] = make_uint4(orow[4 * q], orow[4 * q + 1], orow[4 * q + 2], orow[4 * q + 3]); \
-                }                                                                      \
-            }                                                                          \
-        }                                                                              \
-    } while (0)
-
-    while (j < cnt) {
-        MS_REFILL();
-        MS_STEP();
-        MS_STEP();
-    }
-#undef MS_STEP
-#undef MS_REFILL
-#undef MS_ADVANCE
-    // ragged end (only a lane with cnt < 256): bytes [(dwn & ~(OUTDW-1)) * 4, j)
-    for (uint32_t i = (dwn & ~(OUTDW - 1)) * 4; i < j; ++i) {
-        const uint32_t v = i < 4 * dwn ? orow[(i >> 2) & (OUTDW - 1)] >> (8 * (i & 3))
-                                       : static_cast<uint32_t>(acc >> (8 * (i - 4 * dwn)));
-        dst[i] = static_cast<uint8_t>(v);
-    }
-}
-
-__device__ __forceinline__ uint32_t sel4(const uint4& v, uint32_t i) {
-    const uint32_t lo = (i & 1) ? v.y : v.x;
-    const uint32_t hi = (i & 1) ? v.w : v.z;
-    return (i & 2) ? hi : lo;
-}
-
-__device__ __forceinline__ uint32_t sel16(const Unit& u, uint32_t i) {
-    const uint32_t a = sel4(u.a, i), b = sel4(u.b, i), c = sel4(u.c, i), d = sel4(u.d, i);
-    const uint32_t lo = (i & 4) ? b : a;
-    const uint32_t hi = (i & 4) ? d : c;
-    return (i & 8) ? hi : lo;
-}
-
-// Multi-symbol variant with register-resident input (LDS only for the table
-// and a short output row, so more waves fit per CU). CPB chunks per
-// workgroup (256 lanes each) share one copy of the table.
-template <uint32_t OUTDW, uint32_t CPB>
-__global__ __launch_bounds__(256 * CPB) void k_decode_ms2(DecodeArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    const uint32_t K = a.mlut_bits;
-    const uint32_t nent = 1u << K;
-    uint32_t* mlut = lds;
-    uint32_t* outrows = lds + ((nent + 3) & ~3u);
-    const uint32_t tid = threadIdx.x;
-    for (uint32_t i = tid; i < nent; i += 256 * CPB) mlut[i] = a.mlut[i];
-    __syncthreads();
-
-    const uint32_t c = blockIdx.x * CPB + tid / 256;
-    const uint32_t t = tid % 256;
-    if (c >= a.nchunks) return;
-    const uint64_t sym0 = static_cast<uint64_t>(c) * kChunk;
-    const uint64_t nsym = (a.n - sym0 < kChunk) ? a.n - sym0 : kChunk;
-    const uint64_t lsym0 = static_cast<uint64_t>(t) * kSub;
-    const uint32_t cnt = lsym0 >= nsym ? 0u : static_cast<uint32_t>(nsym - lsym0 < kSub ? nsym - lsym0 : kSub);
-    if (cnt == 0) return;  // no barrier follows
-
-    const uint64_t pos = a.chunk_start[c] + a.sub_bit[(sym0 + lsym0) / kSub];
-    uint8_t* dst = a.out + sym0 + lsym0;
-    uint32_t* orow = outrows + tid * (OUTDW + 1);
-    const uint32_t Ks = a.lut_bits;
-    const uint32_t* glut = a.lut;
-
-    uint64_t unit = pos >> 9;  // 64-byte units
-    Unit A = load_unit(a.comp, a.comp_bytes, unit);
-    Unit B = load_unit(a.comp, a.comp_bytes, unit + 1);
-    const uint32_t drop = static_cast<uint32_t>(pos & 511);
-    uint32_t wi = drop >> 5;
-    uint64_t buf = 0;
-    uint32_t nb = 0;
-
-#define MS2_REFILL()                                                                   \
-    do {                                                                               \
-        if (nb < 32) {                                                                 \
-            const uint32_t w_ = sel16(A, wi);                                          \
-            buf |= static_cast<uint64_t>(__builtin_bswap32(w_)) << (32 - nb);          \
-            nb += 32;                                                                  \
-            if (++wi == 16) {                                                          \
-                A = B;                                                                 \
-                ++unit;                                                                \
-                B = load_unit(a.comp, a.comp_bytes, unit + 1);                         \
-                wi = 0;                                                                \
-            }                                                                          \
-        }                                                                              \
-    } while (0)
-
-    MS2_REFILL();
-    {
-        const uint32_t sh = drop & 31;
-        buf <<= sh;
-        nb -= sh;
-    }
-    uint64_t acc = 0;
-    uint32_t fill = 0, dwn = 0, j = 0;
-
-#define MS2_STEP()                                                                     \
-    do {                                                                               \
-        uint32_t e = mlut[static_cast<uint32_t>(buf >> (64 - K))];                     \
-        if (e & kMsSlow) {                                                             \
-            MS2_REFILL();                                                              \
-            uint32_t e1 = glut[static_cast<uint32_t>(buf >> (64 - Ks))];               \
-            uint32_t d = Ks;                                                           \
-            while (e1 & kLutPtr) {                                                     \
-                const uint32_t idx = static_cast<uint32_t>((buf >> (56 - d)) & 0xFFu); \
-                e1 = glut[(e1 & ~kLutPtr) + idx];                                      \
-                d += 8;                                                                \
-            }                                                                          \
-            e = (e1 & 0xFFu) | (((e1 >> 8) & 0xFFu) << 24) | (1u << 29);               \
-        }                                                                              \
-        const uint32_t used = (e >> 24) & 31u;                                         \
-        const uint32_t cn = min((e >> 29) & 3u, cnt - j);                              \
-        const uint32_t syms = __builtin_amdgcn_ubfe(e, 0, 8 * cn);                     \
-        buf <<= used;                                                                  \
-        nb -= used;                                                                    \
-        acc |= static_cast<uint64_t>(syms) << (8 * fill);                              \
-        fill += cn;                                                                    \
-        j += cn;                                                                       \
-        orow[dwn & (OUTDW - 1)] = static_cast<uint32_t>(acc);                          \
-        if (fill >= 4) {                                                               \
-            acc >>= 32;                                                                \
-            fill -= 4;                                                                 \
-            ++dwn;                                                                     \
-            if ((dwn & (OUTDW - 1)) == 0) {                                            \
-                uint4* d4 = reinterpret_cast<uint4*>(dst + (dwn - OUTDW) * 4);         \
-                _Pragma("unroll") for (uint32_t q = 0; q < OUTDW / 4; ++q)             \
-                    d4[q] = make_uint4(orow[4 * q], orow[4 * q + 1], orow[4 * q + 2], orow[4 * q + 3]); \
-            }                                                                          \
-        }                                                                              \
-    } while (0)
-
-    while (j < cnt) {
-        MS2_REFILL();
-        MS2_STEP();
-        MS2_STEP();
-    }
-#undef MS2_STEP
-#undef MS2_REFILL
-    for (uint32_t i = (dwn & ~(OUTDW - 1)) * 4; i < j; ++i) {
-        const uint32_t v = i < 4 * dwn ? orow[(i >> 2) & (OUTDW - 1)] >> (8 * (i & 3))
-                                       : static_cast<uint32_t>(acc >> (8 * (i - 4 * dwn)));
-        dst[i] = static_cast<uint8_t>(v);
-    }
-}
 }  // namespace
 
 size_t decode_lds_bytes(uint32_t lut_bits, uint32_t rep_log2) {
@@ -604,36 +300,15 @@ size_t decode_lds_bytes(uint32_t lut_bits, uint32_t rep_log2) {
     return static_cast<size_t>(nprim + kThreads * kStageStride) * 4;
 }
 
-size_t decode_ms_lds_bytes(uint32_t mlut_bits, uint32_t rep_log2, uint32_t outdw) {
-    const uint32_t nent = (((1u << mlut_bits) << rep_log2) + 3) & ~3u;
-    return static_cast<size_t>(nent + kThreads * kInStride + kThreads * (outdw + 1)) * 4;
-}
-
-size_t decode_ms_lds_bytes(uint32_t mlut_bits, uint32_t rep_log2) { return decode_ms_lds_bytes(mlut_bits, rep_log2, 16); }
-
 hipError_t launch_decode(const DecodeArgs& a, hipStream_t s) {
     if (a.nchunks == 0) return hipSuccess;
     if (a.max_len > 32) {
         hipLaunchKernelGGL(k_decode<true>, dim3(a.nchunks), dim3(kThreads), decode_lds_bytes(a.lut_bits, 0), s, a);
-    } else if (a.variant == 1 || !a.mlut) {
+    } else if (a.variant == kDecodeRing && a.mlut) {
+        return launch_decode_ring(a, s);
+    } else {
         hipLaunchKernelGGL(k_decode_short, dim3(a.nchunks), dim3(kThreads),
                            decode_lds_bytes(a.lut_bits, a.lut_rep_log2), s, a);
-    } else if (a.variant == 7) {
-        return launch_decode_ring(a, s);
-    } else if (a.variant >= 3 && a.variant <= 6) {
-        const uint32_t nent = ((1u << a.mlut_bits) + 3) & ~3u;
-        switch (a.variant) {
-            case 3: hipLaunchKernelGGL((k_decode_ms2<8, 1>), dim3(a.nchunks), dim3(256), (nent + 256 * 9) * 4, s, a); break;
-            case 4: hipLaunchKernelGGL((k_decode_ms2<8, 2>), dim3((a.nchunks + 1) / 2), dim3(512), (nent + 512 * 9) * 4, s, a); break;
-            case 5: hipLaunchKernelGGL((k_decode_ms2<16, 1>), dim3(a.nchunks), dim3(256), (nent + 256 * 17) * 4, s, a); break;
-            default: hipLaunchKernelGGL((k_decode_ms2<16, 2>), dim3((a.nchunks + 1) / 2), dim3(512), (nent + 512 * 17) * 4, s, a); break;
-        }
-    } else if (a.variant == 2) {
-        hipLaunchKernelGGL(k_decode_ms<8>, dim3(a.nchunks), dim3(kThreads),
-                           decode_ms_lds_bytes(a.mlut_bits, a.lut_rep_log2, 8), s, a);
-    } else {
-        hipLaunchKernelGGL(k_decode_ms<16>, dim3(a.nchunks), dim3(kThreads),
-                           decode_ms_lds_bytes(a.mlut_bits, a.lut_rep_log2, 16), s, a);
     }
     return hipGetLastError();
 }

@@ -69,7 +69,7 @@ struct DecodeArgs {
     uint32_t lut_rep_log2;        // primary table copies in LDS (bank spread)
     const uint32_t* mlut;         // multi-symbol table [1 << mlut_bits] (null: none)
     uint32_t mlut_bits;
-    uint32_t variant;             // kernel choice for experiments (0 = default)
+    uint32_t variant;             // kDecodeRing or kDecodeSingle (codes <= 32 bits)
     uint64_t n;
     uint8_t* out;
 };
@@ -101,7 +101,8 @@ struct BytemapArgs {
 
 size_t pack_lds_bytes(bool long_codes, uint32_t stage_words);
 size_t decode_lds_bytes(uint32_t lut_bits, uint32_t rep_log2);
-size_t decode_ms_lds_bytes(uint32_t mlut_bits, uint32_t rep_log2);
+constexpr uint32_t kDecodeSingle = 1;  // decode.hip k_decode_short
+constexpr uint32_t kDecodeRing = 7;    // decode_ring.hip k_decode_ring
 
 // Pass 1's totals straight to pinned host memory (device-visible pointer):
 // host[b] = (tag << 48) | total_b. host == nullptr: the totals stay in gw.

@@ -51,11 +51,9 @@ bool fixed8_disabled() {
     return e && *e && *e != '0';
 }
 
-static uint32_t ms_bits() {  // HUFF_DEC_MS_BITS: experiments only
-    const char* e = std::getenv("HUFF_DEC_MS_BITS");
-    const int v = e ? std::atoi(e) : static_cast<int>(dev::kMsMaxBits);
-    return static_cast<uint32_t>(std::max(4, std::min(static_cast<int>(dev::kMsMaxBits), v)));
-}
+// multi-symbol table index bits: 12 (16 KiB); 11 and 10 measured slower on
+// Zipf (its 12-bit codes fall to the single-symbol path) and no faster on text
+static uint32_t ms_bits() { return dev::kMsMaxBits; }
 
 void build_multi_table(const HuffTree& t, uint32_t mbits, DecTables& out) {
     // entry i: walk the tree from the root over the mbits bits of i (MSB
@@ -466,25 +464,21 @@ huff::Status huff_enc::decode(const huff_tree* t, const uint8_t* d_comp, uint64_
     a.sub_bit = static_cast<const uint32_t*>(sub_bit.p);
     a.nchunks = nchunks;
     a.max_len = dt->maxdepth;
-    // replicate the primary table up to 4 KiB of LDS (fewer bank conflicts,
-    // occupancy kept); HUFF_DEC_LUT_REP_LOG2 overrides for experiments
-    {
-        int rep = std::max(0, std::min(5, 10 - static_cast<int>(dt->bits)));
-        if (const char* env = std::getenv("HUFF_DEC_LUT_REP_LOG2")) rep = std::max(0, std::min(5, std::atoi(env)));
-        a.lut_rep_log2 = static_cast<uint32_t>(rep);
+    // single-symbol kernel: primary table replicated up to 4 KiB of LDS
+    // (fewer bank conflicts, occupancy kept)
+    a.lut_rep_log2 = static_cast<uint32_t>(std::max(0, std::min(5, 10 - static_cast<int>(dt->bits))));
+    // kernel choice: the multi-symbol ring decoder pays off when lookups
+    // return more than one letter (mean code length well under the 12-bit
+    // table index); near-8-bit codes run the single-symbol kernel.
+    // HUFF_DEC_VARIANT=1|7 forces one (tests, measurements).
+    a.variant = (total_bits < 7 * n) ? huff::dev::kDecodeRing : huff::dev::kDecodeSingle;
+    if (const char* env = std::getenv("HUFF_DEC_VARIANT")) {
+        const int v = std::atoi(env);
+        if (v == static_cast<int>(huff::dev::kDecodeRing) || v == static_cast<int>(huff::dev::kDecodeSingle))
+            a.variant = static_cast<uint32_t>(v);
     }
     a.mlut = static_cast<const uint32_t*>(ctx->d_lut.p) + dt->moff;
     a.mlut_bits = dt->mbits;
-    // kernel choice: the multi-symbol ring decoder pays off when lookups
-    // return more than one letter (mean code length well under the 12-bit
-    // table index); near-8-bit codes run the single-symbol kernel
-    a.variant = (total_bits < 7 * n) ? 7u : 1u;
-    if (const char* env = std::getenv("HUFF_DEC_VARIANT")) a.variant = static_cast<uint32_t>(std::atoi(env));
-    if (a.variant == 0 || a.variant == 7) {  // multi-symbol kernels: no table replication
-        a.lut_rep_log2 = 0;
-        if (const char* env = std::getenv("HUFF_DEC_MS_REP_LOG2"))
-            a.lut_rep_log2 = static_cast<uint32_t>(std::max(0, std::min(3, std::atoi(env))));
-    }
     a.n = n;
     a.out = d_out;
     HUFF_TRY(ctx->timed("decode", [&] { return huff::dev::launch_decode(a, ctx->stream); }));

@@ -160,9 +160,16 @@ def _device_gen(H, ctx, kind, seed, n):
     return x
 
 
+@pytest.mark.parametrize("dec", ["auto", "1", "7"], ids=["dec-auto", "dec-single", "dec-ring"])
 @pytest.mark.parametrize("kind,seed", [("uniform", 0x5EED0001), ("zipf", 0x5EED0002), ("text", 0x5EED0005)])
-def test_device_job_medium(H, O, ctx, kind, seed):
+def test_device_job_medium(H, O, ctx, kind, seed, dec, monkeypatch):
+    """16 MiB + ragged tail of each workload; decode through the kernel the
+    runtime picks and through each decode kernel forced (HUFF_DEC_VARIANT)"""
     import torch
+
+    if dec != "auto":
+        monkeypatch.setenv("HUFF_DEC_VARIANT", dec)
+        monkeypatch.setenv("HUFF_DISABLE_FIXED8", "1")
 
     n = (1 << 24) + 12345  # 16 MiB + a ragged tail
     x = _device_gen(H, ctx, kind, seed, n)
