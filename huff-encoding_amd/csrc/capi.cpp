@@ -381,23 +381,13 @@ int huff_enc_pack_shards(huff_enc* e, const uint64_t* hists, uint32_t world, uin
     if (reinterpret_cast<uintptr_t>(d_out) & 15) return fail(HUFF_E_INVALID_ARG, "d_out must be 16-byte aligned");
     *tree_out = nullptr;
     return guarded([&]() -> huff::Status {
-        huff::ByteWeights g;  // from_bytes of the concatenation: plain per-bin sums
-        for (uint32_t q = 0; q < world; ++q)
-            for (int b = 0; b < 256; ++b) g.weights[b] += hists[static_cast<size_t>(q) * 256 + b];
-        g.len = 0;
-        for (int b = 0; b < 256; ++b) g.len += g.weights[b] != 0;
         auto t = std::make_unique<huff_tree>();
-        HUFF_TRY(huff::HuffTree::from_weights(g, t->t));
+        HUFF_TRY(huff::HuffTree::from_weights(huff::shard_weights(hists, world), t->t));
         const huff::EncTables& et = t->enc_tables();
-        uint64_t base = 0;
-        for (uint32_t q = 0; q < rank; ++q)
-            for (int b = 0; b < 256; ++b) base += hists[static_cast<size_t>(q) * 256 + b] * et.len[b];
+        const uint64_t base = huff::shard_bit_base(hists, rank, et.len);
         uint8_t prev[8];
         size_t np = 0;
-        for (uint32_t q = rank; q-- > 0 && np < 8;) {  // last <= 8 bytes before this shard
-            const size_t tl = tail_lens[q] > 8 ? 8 : tail_lens[q];
-            for (size_t k = tl; k-- > 0 && np < 8;) prev[7 - np++] = tails[static_cast<size_t>(q) * 8 + k];
-        }
+        if (rank) huff::shard_prev_tail(tails, tail_lens, rank, prev, &np);
         if (bit_base_out) *bit_base_out = base;
         uint64_t bits = 0;
         huff::Status st = e->pack(t.get(), base, prev + 8 - np, np, d_out, out_cap, &bits);

@@ -89,6 +89,18 @@ private:
 };
 
 // ---------------------------------------------------------------------------
+// Sharded encode: shard `rank` of `world` contiguous shards.
+// hists = world x 256 per-shard weights; tails[q*8 ..] holds shard q's last
+// tail_lens[q] (<= 8) bytes. Fills the summed weights (ByteWeights::from_bytes
+// of the whole stream: plain sums), and after the tree is known, the shard's
+// first global bit (sum of the earlier shards' bits) and the <= 8 input bytes
+// right before it (right-aligned in prev[8], count in *np).
+// ---------------------------------------------------------------------------
+ByteWeights shard_weights(const uint64_t* hists, uint32_t world);
+uint64_t shard_bit_base(const uint64_t* hists, uint32_t rank, const uint8_t len[256]);
+void shard_prev_tail(const uint8_t* tails, const uint8_t* tail_lens, uint32_t rank, uint8_t prev[8], size_t* np);
+
+// ---------------------------------------------------------------------------
 // CompressData container — huff_coding/src/comp.rs:40-184, 279-300
 // ---------------------------------------------------------------------------
 // Byte layout of to_bytes (comp.rs:279-300, huff/README.md):

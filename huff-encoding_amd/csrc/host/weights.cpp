@@ -68,4 +68,29 @@ std::vector<std::pair<size_t, size_t>> ration_bounds(size_t n, size_t ration_cou
     return r;
 }
 
+ByteWeights shard_weights(const uint64_t* hists, uint32_t world) {
+    ByteWeights g;
+    for (uint32_t q = 0; q < world; ++q)
+        for (int b = 0; b < 256; ++b) g.weights[b] += hists[static_cast<size_t>(q) * 256 + b];
+    g.len = 0;
+    for (int b = 0; b < 256; ++b) g.len += g.weights[b] != 0;
+    return g;
+}
+
+uint64_t shard_bit_base(const uint64_t* hists, uint32_t rank, const uint8_t len[256]) {
+    uint64_t base = 0;
+    for (uint32_t q = 0; q < rank; ++q)
+        for (int b = 0; b < 256; ++b) base += hists[static_cast<size_t>(q) * 256 + b] * len[b];
+    return base;
+}
+
+void shard_prev_tail(const uint8_t* tails, const uint8_t* tail_lens, uint32_t rank, uint8_t prev[8], size_t* np) {
+    size_t k = 0;
+    for (uint32_t q = rank; q-- > 0 && k < 8;) {  // walk back over the earlier shards
+        const size_t tl = tail_lens[q] > 8 ? 8 : tail_lens[q];
+        for (size_t i = tl; i-- > 0 && k < 8;) prev[7 - k++] = tails[static_cast<size_t>(q) * 8 + i];
+    }
+    *np = k;
+}
+
 }  // namespace huff

@@ -1,6 +1,7 @@
 // test_host.cpp — the reference's own tests, restated against the product's
 // C++ host code (huff_coding/tests/*.rs and the weights/tree doctests).
 // Host only: no GPU call.
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -125,7 +126,51 @@ static void byte_weights_doctests() {
     CHECK(a.weights['a'] == 5 && a.weights['b'] == 5 && a.weights['c'] == 1);
 }
 
+// shard plan vs the single stream: random shard cuts (empty and < 8-byte
+// shards included) of a random byte string
+static void shard_plan_matches_single_stream() {
+    uint64_t rng = 0x1234567u;
+    auto next = [&] { rng = rng * 6364136223846793005ull + 1442695040888963407ull; return rng >> 33; };
+    for (int trial = 0; trial < 200; ++trial) {
+        const size_t n = next() % 200;
+        std::vector<uint8_t> data(n);
+        for (auto& x : data) x = static_cast<uint8_t>(next() % 7);
+        const uint32_t world = 1 + next() % 6;
+        std::vector<size_t> cut{0};
+        for (uint32_t q = 1; q < world; ++q) cut.push_back(n ? next() % (n + 1) : 0);
+        cut.push_back(n);
+        std::sort(cut.begin(), cut.end());
+        std::vector<uint64_t> hists(world * 256, 0);
+        std::vector<uint8_t> tails(world * 8, 0), tl(world, 0);
+        for (uint32_t q = 0; q < world; ++q) {
+            for (size_t i = cut[q]; i < cut[q + 1]; ++i) ++hists[q * 256 + data[i]];
+            const size_t len = std::min<size_t>(8, cut[q + 1] - cut[q]);
+            tl[q] = static_cast<uint8_t>(len);
+            for (size_t k = 0; k < len; ++k) tails[q * 8 + k] = data[cut[q + 1] - len + k];
+        }
+        const ByteWeights g = shard_weights(hists.data(), world);
+        for (int b = 0; b < 256; ++b) {
+            uint64_t c = 0;
+            for (uint8_t x : data) c += x == b;
+            CHECK(g.weights[b] == c);
+        }
+        uint8_t len[256];
+        for (int b = 0; b < 256; ++b) len[b] = static_cast<uint8_t>(1 + b % 5);
+        for (uint32_t r = 0; r < world; ++r) {
+            uint64_t want = 0;
+            for (size_t i = 0; i < cut[r]; ++i) want += len[data[i]];
+            CHECK(shard_bit_base(hists.data(), r, len) == want);
+            uint8_t prev[8];
+            size_t np = 0;
+            shard_prev_tail(tails.data(), tl.data(), r, prev, &np);
+            CHECK(np == std::min<size_t>(8, cut[r]));
+            for (size_t k = 0; k < np; ++k) CHECK(prev[8 - np + k] == data[cut[r] - np + k]);
+        }
+    }
+}
+
 int main() {
+    shard_plan_matches_single_stream();
     tree_normal_init();
     tree_single_branch();
     tree_invalid_weights();
