@@ -406,6 +406,22 @@ int huff_enc_decode(huff_enc* e, const huff_tree* t, const uint8_t* d_comp, uint
     });
 }
 
+int huff_dev_decompress(huff_ctx* ctx, const huff_tree* t, const uint8_t* d_comp, size_t comp_bytes,
+                        uint8_t padding, uint8_t* d_out, size_t out_cap, size_t* n_out) {
+    if (!ctx || !t || !n_out || (!d_comp && comp_bytes)) return fail(HUFF_E_INVALID_ARG, "null argument");
+    if (padding > 7) return fail(HUFF_E_PADDING, "padding bits > 7");
+    *n_out = 0;
+    return guarded([&]() -> huff::Status {
+        const uint64_t valid = comp_bytes ? comp_bytes * 8 - padding : 0;
+        DevBuf unused;
+        uint64_t n = 0;
+        huff::Status st = huff::decode_indexless_dev(ctx, d_comp, comp_bytes, valid, t, unused, &n,
+                                                     d_out ? d_out : reinterpret_cast<uint8_t*>(1), d_out ? out_cap : 0);
+        *n_out = n;
+        return st;
+    });
+}
+
 int huff_dev_generate(huff_ctx* ctx, int kind, uint64_t seed, uint64_t offset, const uint64_t* cdf, uint8_t* d_out,
                       size_t n) {
     if (!ctx || (!d_out && n) || (kind == 1 && !cdf)) return fail(HUFF_E_INVALID_ARG, "null argument");

@@ -15,7 +15,12 @@
 //           one or two rounds settle; a bounded host loop falls back to a
 //           sequential sweep (k_settle) for codes that never synchronise.
 //  scan   : exclusive scan of c[] -> output offsets (k_scan, hist.hip).
-//  k_emit : lane i decodes c[i] symbols from its settled start.
+//  k_mark : (codes <= 32 bits) lane i walks its settled segment once more and
+//           records the start bit of every symbol whose index is a multiple
+//           of 256: the restart index the ring decoder (decode_ring.hip) then
+//           decodes from, as it does for streams this encoder wrote.
+//  k_emit : (longer codes) lane i decodes c[i] symbols from its settled start.
+// k_spec and k_mark stage each workgroup's 256 segments in LDS (k_*_lds).
 // A codeword that would cross B is dropped, as the reference's walk drops an
 // incomplete final code (comp.rs:493-516).
 #include "bitreader.hpp"
@@ -173,10 +178,169 @@ Seg make_seg(const IndexlessArgs& a) {
     return Seg{a.comp, a.comp_bytes, a.valid_bits, a.seg_bits, a.nseg, a.lut, a.lut_bits};
 }
 
+// ---- LDS-staged variants (every code <= 32 bits) ---------------------------
+// A workgroup's 256 consecutive segments are one contiguous bit range: it is
+// staged in LDS once with coalesced dword loads (plus 32 bytes of lookahead
+// for the code that crosses the last segment end), and each lane then reads
+// its bits from LDS: a 64-bit window refilled 32 bits at a time, multi-symbol
+// lookups (top 12 bits -> up to 3 letters) while the whole entry stays inside
+// the lane's range, single codes otherwise.
+
+struct Staged {
+    const uint32_t* w;
+    uint64_t base;  // bit position of w[0]'s most significant bit
+};
+
+__device__ Staged stage_block(const IndexlessArgs& a, uint32_t* w) {
+    const uint64_t seg0 = static_cast<uint64_t>(blockIdx.x) * kThreads;
+    const uint64_t bit_lo = seg0 * a.seg_bits;
+    const uint64_t seg_end = seg0 + kThreads < a.nseg ? seg0 + kThreads : a.nseg;
+    const uint64_t bit_hi = seg_end * a.seg_bits < a.valid_bits ? seg_end * a.seg_bits : a.valid_bits;
+    const uint64_t byte_lo = (bit_lo >> 3) & ~3ull;
+    uint64_t byte_hi = ((bit_hi + 7) >> 3) + 32;
+    if (byte_hi > a.comp_bytes) byte_hi = a.comp_bytes;
+    const uint32_t nw = static_cast<uint32_t>((byte_hi - byte_lo + 3) / 4);
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(a.comp + byte_lo);
+    for (uint32_t i = threadIdx.x; i < nw + 2; i += blockDim.x) w[i] = i < nw ? src[i] : 0u;
+    return Staged{w, byte_lo * 8};
+}
+
+struct LaneBits {
+    const uint32_t* w;
+    uint64_t buf;
+    uint32_t nb, rp;
+    uint64_t pos;
+    __device__ __forceinline__ void init(const Staged& st, uint64_t p) {
+        w = st.w;
+        pos = p;
+        const uint64_t off = p - st.base;
+        rp = static_cast<uint32_t>(off >> 5);
+        const uint32_t sh = static_cast<uint32_t>(off & 31);
+        buf = (static_cast<uint64_t>(__builtin_bswap32(w[rp])) << 32) | __builtin_bswap32(w[rp + 1]);
+        buf <<= sh;
+        nb = 64 - sh;
+        rp += 2;
+    }
+    __device__ __forceinline__ void refill() {
+        if (nb < 32) {
+            buf |= static_cast<uint64_t>(__builtin_bswap32(w[rp++])) << (32 - nb);
+            nb += 32;
+        }
+    }
+    __device__ __forceinline__ void consume(uint32_t len) {
+        buf <<= len;
+        nb -= len;
+        pos += len;
+    }
+};
+
+// one code from the single-symbol tables (global, L2-resident: only segment
+// ends and codes longer than the multi table's index take this path)
+__device__ __forceinline__ uint32_t single_code(const LaneBits& r, const uint32_t* glut, uint32_t Ks) {
+    uint32_t e = glut[static_cast<uint32_t>(r.buf >> (64 - Ks))];
+    uint32_t d = Ks;
+    while (e & kLutPtr) {
+        const uint32_t idx = static_cast<uint32_t>((r.buf >> (56 - d)) & 0xFFu);
+        e = glut[(e & ~kLutPtr) + idx];
+        d += 8;
+    }
+    return e;  // (len << 8) | letter
+}
+
+// LDS: [multi table 1 << K][staged input]
+__global__ __launch_bounds__(kThreads) void k_spec_lds(IndexlessArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    const uint32_t K = a.mlut_bits, Ks = a.lut_bits;
+    uint32_t* mlut = lds;
+    for (uint32_t i = threadIdx.x; i < (1u << K); i += blockDim.x) mlut[i] = a.mlut[i];
+    const Staged st = stage_block(a, mlut + (1u << K));
+    __syncthreads();
+    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= a.nseg) return;
+    const uint64_t B = a.valid_bits;
+    const uint64_t start = i * a.seg_bits;
+    const uint64_t end = (i + 1 == a.nseg) ? B : (start + a.seg_bits < B ? start + a.seg_bits : B);
+    LaneBits r;
+    r.init(st, start);
+    uint64_t cnt = 0;
+    while (r.pos < end) {
+        r.refill();
+        const uint32_t e = mlut[static_cast<uint32_t>(r.buf >> (64 - K))];
+        const uint32_t used = (e >> 24) & 31u;
+        if (!(e & kMsSlow) && r.pos + used < end) {  // every code of the entry ends before `end`
+            r.consume(used);
+            cnt += e >> 29;
+            continue;
+        }
+        const uint32_t len = (single_code(r, a.lut, Ks) >> 8) & 0xFFu;
+        if (r.pos + len > B) {  // an incomplete final code is dropped (comp.rs:493-516)
+            r.pos = B;
+            break;
+        }
+        r.consume(len);
+        ++cnt;
+    }
+    a.s[i] = start;
+    a.x[i] = r.pos;
+    a.c[i] = cnt;
+}
+
+// sub_abs[g] = start bit of symbol 256 g, from the settled segments
+__global__ __launch_bounds__(kThreads) void k_mark_lds(IndexlessArgs a, const uint64_t* __restrict__ off,
+                                                       uint64_t* __restrict__ sub_abs) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    const uint32_t K = a.mlut_bits, Ks = a.lut_bits;
+    uint32_t* mlut = lds;
+    for (uint32_t i = threadIdx.x; i < (1u << K); i += blockDim.x) mlut[i] = a.mlut[i];
+    const Staged st = stage_block(a, mlut + (1u << K));
+    __syncthreads();
+    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= a.nseg) return;
+    uint64_t j = off[i];
+    const uint64_t jend = j + a.c[i];
+    if (j == jend) return;
+    LaneBits r;
+    r.init(st, a.s[i]);
+    while (j < jend) {
+        if ((j & 255) == 0) sub_abs[j >> 8] = r.pos;
+        r.refill();
+        const uint32_t e = mlut[static_cast<uint32_t>(r.buf >> (64 - K))];
+        const uint32_t cn = e >> 29;
+        if (!(e & kMsSlow) && (j & 255) + cn <= 256 && j + cn <= jend) {  // no mark inside the entry
+            r.consume((e >> 24) & 31u);
+            j += cn;
+            continue;
+        }
+        r.consume((single_code(r, a.lut, Ks) >> 8) & 0xFFu);
+        ++j;
+    }
+}
+
 }  // namespace
+
+static size_t lds_staged_bytes(const IndexlessArgs& a) {
+    return static_cast<size_t>(1u << a.mlut_bits) * 4 + ((kThreads * a.seg_bits + 7) / 8 + 64 + 8 + 3) / 4 * 4;
+}
+
+static bool use_staged(const IndexlessArgs& a) { return a.mlut && a.max_len <= 32 && lds_staged_bytes(a) <= 160 * 1024; }
+
+hipError_t launch_indexless_mark(const IndexlessArgs& a, const uint64_t* off, uint64_t* sub_abs, hipStream_t st) {
+    if (a.nseg == 0) return hipSuccess;
+    if (!use_staged(a)) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_mark_lds, dim3((a.nseg + kThreads - 1) / kThreads), dim3(kThreads), lds_staged_bytes(a), st,
+                       a, off, sub_abs);
+    return hipGetLastError();
+}
+
+bool indexless_staged(const IndexlessArgs& a) { return use_staged(a); }
 
 hipError_t launch_indexless_spec(const IndexlessArgs& a, hipStream_t st) {
     if (a.nseg == 0) return hipSuccess;
+    if (use_staged(a)) {
+        hipLaunchKernelGGL(k_spec_lds, dim3((a.nseg + kThreads - 1) / kThreads), dim3(kThreads), lds_staged_bytes(a),
+                           st, a);
+        return hipGetLastError();
+    }
     const Seg g = make_seg(a);
     const size_t lds = (1u << a.lut_bits) * 4;
     hipLaunchKernelGGL(k_spec, dim3((a.nseg + kThreads - 1) / kThreads), dim3(kThreads), lds, st, g, a.s, a.x,

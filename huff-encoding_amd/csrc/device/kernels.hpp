@@ -67,6 +67,8 @@ struct DecodeArgs {
     uint32_t nchunks;
     uint32_t max_len;             // longest code (> 32: window slow path)
     uint32_t lut_rep_log2;        // primary table copies in LDS (bank spread)
+    const uint64_t* sub_abs;      // non-null: absolute start bit of every 256-symbol run
+                                  // (index-free decode), instead of chunk_start + sub_bit
     const uint32_t* mlut;         // multi-symbol table [1 << mlut_bits] (null: none)
     uint32_t mlut_bits;
     uint32_t variant;             // kDecodeRing or kDecodeSingle (codes <= 32 bits)
@@ -85,6 +87,9 @@ struct IndexlessArgs {
     uint64_t* s;                  // [nseg] settled segment starts
     uint64_t* x;                  // [nseg] exits
     uint64_t* c;                  // [nseg] symbol counts
+    const uint32_t* mlut;         // multi-symbol table (codes <= 32 bits: the LDS-staged kernels)
+    uint32_t mlut_bits;
+    uint32_t max_len;
 };
 
 // dst[i] = map[src[i]] (+ arithmetic restart index)
@@ -129,6 +134,9 @@ hipError_t launch_indexless_fix(const IndexlessArgs& a, const uint64_t* xin, uin
                                 hipStream_t s);
 hipError_t launch_indexless_settle(const IndexlessArgs& a, uint64_t* x, hipStream_t s);
 hipError_t launch_indexless_emit(const IndexlessArgs& a, const uint64_t* off, uint8_t* out, hipStream_t s);
+// restart index for the ring decoder: sub_abs[g] = start bit of symbol 256 g
+hipError_t launch_indexless_mark(const IndexlessArgs& a, const uint64_t* off, uint64_t* sub_abs, hipStream_t s);
+bool indexless_staged(const IndexlessArgs& a);  // k_spec/k_mark LDS variants apply
 hipError_t launch_bytemap(const BytemapArgs& a, hipStream_t s);
 hipError_t launch_find_first(const uint8_t* in, uint64_t n, const uint8_t* missing_mask, unsigned long long* pos,
                              hipStream_t s);

@@ -676,8 +676,18 @@ Status parse_block_size(const char* s, size_t* out) {
 namespace huff {
 
 Status decode_indexless_dev(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_bytes, uint64_t valid_bits,
-                            const huff_tree* t, DevBuf& out, uint64_t* nsym) {
+                            const huff_tree* t, DevBuf& out, uint64_t* nsym, uint8_t* d_user, size_t user_cap) {
     *nsym = 0;
+    // the output goes to d_user when given (capacity checked once the count
+    // is known), else into `out`
+    auto out_ptr = [&](uint64_t need) -> Status {
+        if (d_user) {
+            if (need > user_cap) return Status::err(HUFF_E_BUFFER_TOO_SMALL, "output buffer too small");
+            return Status::ok();
+        }
+        return out.ensure(need + 16);
+    };
+    auto out_at = [&]() { return d_user ? d_user : static_cast<uint8_t*>(out.p); };
     uint64_t* nsym_out_alias = nsym;
     if (valid_bits == 0) return Status::ok();
     if (reinterpret_cast<uintptr_t>(d_comp) & 3)
@@ -687,10 +697,11 @@ Status decode_indexless_dev(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_
     HUFF_TRY(ctx->upload_dec_tables(t, &dt));
     if (dt->all8 && !fixed8_disabled()) {  // every code 8 bits: one symbol per whole byte
         const uint64_t nsym = valid_bits / 8;
-        HUFF_TRY(out.ensure(nsym + 16));
+        *nsym_out_alias = nsym;
+        HUFF_TRY(out_ptr(nsym));
         dev::BytemapArgs m{};
         m.src = d_comp;
-        m.dst = static_cast<uint8_t*>(out.p);
+        m.dst = out_at();
         m.n = nsym;
         for (int b = 0; b < 256; ++b) m.map[b] = static_cast<uint8_t>(dt->lut[b]);
         HIP_TRY(dev::launch_bytemap(m, ctx->stream));
@@ -701,7 +712,10 @@ Status decode_indexless_dev(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_
     uint32_t g = 0;
     for (const LeafCode& lc : t->t.leaves()) g = std::gcd(g, lc.len);
     if (g == 0) g = 1;
-    const uint64_t S = static_cast<uint64_t>(g) * ((2048 + g - 1) / g);
+    // codes <= 32 bits take the LDS-staged kernels: 1024-bit segments keep a
+    // workgroup's staging at 32 KiB (3 workgroups per CU); longer codes 2048
+    const uint64_t seg_target = dt->maxdepth <= 32 ? 1024 : 2048;
+    const uint64_t S = static_cast<uint64_t>(g) * ((seg_target + g - 1) / g);
     const uint64_t nseg = (valid_bits + S - 1) / S;
     DevBuf s, x0, x1, c, off, flag;
     HUFF_TRY(s.ensure(nseg * 8));
@@ -721,6 +735,9 @@ Status decode_indexless_dev(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_
     a.s = static_cast<uint64_t*>(s.p);
     a.x = static_cast<uint64_t*>(x0.p);
     a.c = static_cast<uint64_t*>(c.p);
+    a.mlut = static_cast<const uint32_t*>(ctx->d_lut.p) + dt->moff;
+    a.mlut_bits = dt->mbits;
+    a.max_len = dt->maxdepth;
     hipStream_t st = ctx->stream;
     HIP_TRY(dev::launch_indexless_spec(a, st));
     uint64_t* xa = static_cast<uint64_t*>(x0.p);
@@ -744,8 +761,35 @@ Status decode_indexless_dev(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_
     uint64_t total = 0;
     HIP_TRY(hipMemcpyAsync(&total, static_cast<uint64_t*>(off.p) + nseg, 8, hipMemcpyDeviceToHost, st));
     HUFF_TRY(ctx->sync());
-    HUFF_TRY(out.ensure(total + 16));
-    HIP_TRY(dev::launch_indexless_emit(a, static_cast<const uint64_t*>(off.p), static_cast<uint8_t*>(out.p), st));
+    *nsym = total;
+    HUFF_TRY(out_ptr(total));
+    const bool aligned16 = !(reinterpret_cast<uintptr_t>(d_comp) & 15) && !(reinterpret_cast<uintptr_t>(out_at()) & 15);
+    if (dev::indexless_staged(a) && total && aligned16) {
+        // a restart index for the ring decoder, then the ordinary restart-index decode
+        DevBuf sub_abs;
+        HUFF_TRY(sub_abs.ensure(((total + dev::kSub - 1) / dev::kSub) * 8));
+        HIP_TRY(dev::launch_indexless_mark(a, static_cast<const uint64_t*>(off.p),
+                                           static_cast<uint64_t*>(sub_abs.p), st));
+        dev::DecodeArgs d{};
+        d.comp = d_comp;
+        d.comp_bytes = comp_bytes;
+        d.lut = static_cast<const uint32_t*>(ctx->d_lut.p);
+        d.lut_bits = dt->bits;
+        d.lut_words = static_cast<uint32_t>(dt->lut.size());
+        d.sub_abs = static_cast<const uint64_t*>(sub_abs.p);
+        d.nchunks = static_cast<uint32_t>((total + dev::kChunk - 1) / dev::kChunk);
+        d.max_len = dt->maxdepth;
+        d.mlut = a.mlut;
+        d.mlut_bits = a.mlut_bits;
+        d.variant = dev::kDecodeRing;
+        d.n = total;
+        d.out = out_at();
+        HIP_TRY(dev::launch_decode_ring(d, st));
+        HIP_TRY(hipEventRecord(ctx->lut_free, st));
+        HUFF_TRY(ctx->sync());  // sub_abs is freed on return
+        return Status::ok();
+    }
+    HIP_TRY(dev::launch_indexless_emit(a, static_cast<const uint64_t*>(off.p), out_at(), st));
     HIP_TRY(hipEventRecord(ctx->lut_free, st));
     *nsym = total;
     return Status::ok();

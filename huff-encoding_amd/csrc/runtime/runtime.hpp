@@ -168,7 +168,8 @@ Status parse_block_size(const char* s, size_t* out);
 // decode without a restart index: valid_bits of the stream at d_comp; the
 // symbols land in `out` (grown as needed), their count in *nsym
 Status decode_indexless_dev(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_bytes, uint64_t valid_bits,
-                            const huff_tree* t, DevBuf& out, uint64_t* nsym);
+                            const huff_tree* t, DevBuf& out, uint64_t* nsym, uint8_t* d_user = nullptr,
+                            size_t user_cap = 0);
 Status decode_indexless_host(huff_ctx* ctx, const uint8_t* comp, size_t len, uint64_t valid_bits,
                              const huff_tree* t, std::vector<uint8_t>& out);
 }  // namespace huff

@@ -97,6 +97,18 @@ class EncodeJob:
         _check(load().huff_enc_decode(self.h, tree.h, C.c_void_p(d_comp), C.c_void_p(d_out)))
 
 
+def decompress_dev(ctx, tree, d_comp: int, comp_bytes: int, padding: int, d_out: int, out_cap: int) -> int:
+    """comp.rs:487-519 on a device-resident stream with no restart index
+    (self-synchronising decode); returns the number of letters written"""
+    n = C.c_size_t()
+    rc = load().huff_dev_decompress(ctx.h, tree.h, C.c_void_p(d_comp), comp_bytes, padding,
+                                    C.c_void_p(d_out) if d_out else None, out_cap, C.byref(n))
+    if not d_out and rc == _lib.E_BUFFER_TOO_SMALL:  # count-only query
+        return n.value
+    _check(rc)
+    return n.value
+
+
 def generate(ctx, kind: str, seed: int, d_out: int, n: int, offset: int = 0, cdf: Optional[np.ndarray] = None):
     """synthetic input in HBM: kind 'uniform' | 'zipf' | 'text' (cdf for zipf)"""
     k = {"uniform": 0, "zipf": 1, "text": 2}[kind]

@@ -199,6 +199,15 @@ int huff_enc_pack_shards(huff_enc* e, const uint64_t* hists, uint32_t world, uin
  * using its restart index: d_comp is the pack's d_out, d_out gets n bytes. */
 int huff_enc_decode(huff_enc* e, const huff_tree* t, const uint8_t* d_comp, uint8_t* d_out);
 
+/* decompress (comp.rs:487-519) of a device-resident stream that has no
+ * restart index (e.g. written by the reference CPU path): comp_bytes bytes at
+ * d_comp (4-B aligned), the last holding `padding` pad bits (the walk reads
+ * 8 - padding bits of it; an incomplete final code is dropped). Self-
+ * synchronising parallel decode; writes the letters to d_out and their count
+ * to *n_out (set also on HUFF_E_BUFFER_TOO_SMALL; d_out NULL: count only). */
+int huff_dev_decompress(huff_ctx* ctx, const huff_tree* t, const uint8_t* d_comp, size_t comp_bytes,
+                        uint8_t padding, uint8_t* d_out, size_t out_cap, size_t* n_out);
+
 /* synthetic inputs generated on the device (not reference functions):
  * kind 0 = uniform bytes, 1 = Zipf(alpha) with cdf[256] (host), 2 = text.
  * Byte i of the stream depends only on (kind, seed, offset + i). */

@@ -151,6 +151,44 @@ def test_decompress_foreign_streams(H, O, ctx):
             assert H.decompress(H.CompressData.try_from_bytes(raw), ctx) == O.decompress(payload, pad, t)
 
 
+def test_dev_decompress_foreign_streams(H, O, ctx):
+    """huff_dev_decompress: device-resident streams written by the CPU
+    restatement (no restart index), incl. paddings, single-letter trees,
+    garbage payloads and the count-only query"""
+    import torch
+    from huff_coding import device as D
+
+    rng = np.random.default_rng(13)
+    cases = []
+    for n in (1, 5, 1000, 65536 * 3 + 17, 700_001):
+        for hi in (1, 3, 40, 256):
+            cases.append(rng.integers(0, hi, n, dtype=np.uint8).tobytes())
+    cases.append(np.minimum(rng.geometric(0.2, 300_000), 255).astype(np.uint8).tobytes())
+    for data in cases:
+        t = O.Tree.from_weights(O.weights_from_bytes(data))
+        comp, pad = O.compress_with_tree(data, t)
+        want = O.decompress(comp, pad, t)
+        tree = H.HuffTree.try_from_bin(t.as_bin())
+        dc = torch.zeros(len(comp) + 64, dtype=torch.uint8, device="cuda")
+        dc[: len(comp)] = torch.frombuffer(bytearray(comp), dtype=torch.uint8).cuda()
+        assert D.decompress_dev(ctx, tree, dc.data_ptr(), len(comp), pad, 0, 0) == len(want)
+        out = torch.empty(len(want) + 64, dtype=torch.uint8, device="cuda")
+        got = D.decompress_dev(ctx, tree, dc.data_ptr(), len(comp), pad, out.data_ptr(), len(want))
+        torch.cuda.synchronize()
+        assert got == len(want) and out[:got].cpu().numpy().tobytes() == want
+    t = O.Tree.from_weights(O.weights_from_bytes(b"abracadabra alakazam"))
+    tree = H.HuffTree.try_from_bin(t.as_bin())
+    for n in (3, 999):
+        payload = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        for pad in (0, 5):
+            want = O.decompress(payload, pad, t)
+            dc = torch.frombuffer(bytearray(payload + bytes(64)), dtype=torch.uint8).cuda()
+            out = torch.empty(len(want) + 64, dtype=torch.uint8, device="cuda")
+            got = D.decompress_dev(ctx, tree, dc.data_ptr(), n, pad, out.data_ptr(), len(want) + 64)
+            torch.cuda.synchronize()
+            assert out[:got].cpu().numpy().tobytes() == want
+
+
 def _device_gen(H, ctx, kind, seed, n):
     import torch
     from huff_coding import device as D

@@ -27,7 +27,7 @@ SEEDS = {"uniform": 0x5EED0001, "zipf": 0x5EED0002, "text": 0x5EED0005}
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--phase", default="all", choices=["hist", "pack", "decode", "all"])
+    ap.add_argument("--phase", default="all", choices=["hist", "pack", "decode", "indexless", "all"])
     ap.add_argument("--workload", default="uniform", choices=sorted(SEEDS))
     ap.add_argument("--bytes", type=int, default=1 << 30)
     ap.add_argument("--iters", type=int, default=20)
@@ -60,6 +60,20 @@ def main():
     torch.cuda.synchronize()
     if not args.no_verify:
         assert torch.equal(dec[:n], x[:n])
+    if args.phase == "indexless":  # decode without the restart index (reference-written streams)
+        comp_bytes = (bits + 7) // 8
+        pad = (8 - bits % 8) % 8
+        got = D.decompress_dev(ctx, tree, out.data_ptr(), comp_bytes, pad, dec.data_ptr(), n + 64)
+        torch.cuda.synchronize()
+        assert got == n and (args.no_verify or torch.equal(dec[:n], x[:n]))
+        t0 = time.perf_counter()
+        for _ in range(args.iters):
+            D.decompress_dev(ctx, tree, out.data_ptr(), comp_bytes, pad, dec.data_ptr(), n + 64)
+        torch.cuda.synchronize()
+        el = (time.perf_counter() - t0) * 1e3 / args.iters
+        print(json.dumps({"phase": "indexless", "workload": args.workload, "n": n, "comp_bytes": comp_bytes,
+                          "wall_ms_per_iter": el, "GBps_out": n / el / 1e6}))
+        return
     ctx.set_timing(True)
     ctx.reset_timing()
     t0 = time.perf_counter()
