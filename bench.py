@@ -71,10 +71,23 @@ def cpu_baseline(workload: str, target_s: float):
     scale = max(1.0, target_s / max(e + d, 1e-6))
     n = int(min(256 << 20, (1 << 20) * scale)) & ~0xFFFF
     e, d = run(n)
+    # "cpu-fast" (SURVEY §8d): table-driven encode/decode on all the host
+    # threads this process may use (16 on the GPU box), a larger sample of
+    # the same stream; second of two runs (the first faults the pages in)
+    fast_threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    nf = max(n, 256 << 20)
+    data = gen(SEEDS[workload], nf)
+    for _ in range(2):
+        _, back, fe, fd = O.fast_roundtrip(data, fast_threads)
+    assert np.array_equal(back, data)
     return {"value": round(n / (e + d) / 1e9, 6), "unit": "GB/s", "cores": 12, "kind": "port",
             "sample": f"{n} B of the same {workload} stream; encode {n / e / 1e9:.4f} GB/s (12-thread "
                       f"histogram + 1-thread bit-serial encode), decode {n / d / 1e9:.4f} GB/s (1-thread "
-                      f"tree walk); oracle/huff_oracle.c restatement of huff_coding (Rust not buildable here)"}
+                      f"tree walk); oracle/huff_oracle.c restatement of huff_coding (Rust not buildable here)",
+            "fast": {"value": round(nf / (fe + fd) / 1e9, 4), "unit": "GB/s", "cores": fast_threads,
+                     "encode_GBps": round(nf / fe / 1e9, 4), "decode_GBps": round(nf / fd / 1e9, 4),
+                     "sample": f"{nf} B; table-driven histogram+tree+encode and 12-bit-table decode "
+                               f"(oracle fast_roundtrip), {fast_threads} threads"}}
 
 
 PHASE_KERNELS = {  # bench phase -> device kernels (names as in tools/summarize_prof.py)
@@ -187,6 +200,18 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
 
+    # measured streaming-copy ceiling of this GPU, same run:
+    # device-to-device copy of the n input bytes, best of 5, 2n bytes moved
+    copy_ms = []
+    for _ in range(5):
+        a_ev, b_ev = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a_ev.record()
+        dec[:n].copy_(x[:n])
+        b_ev.record()
+        b_ev.synchronize()
+        copy_ms.append(a_ev.elapsed_time(b_ev))
+    copy_gbps = 2 * n / (min(copy_ms) * 1e-3) / 1e9
+
     _, ln = tree.code_table()
     total = state["hists"].sum(axis=0, dtype=np.uint64)
     state["fixed8"] = bool((ln[total > 0] == 8).all()) and os.environ.get("HUFF_DISABLE_FIXED8", "0") in ("", "0")
@@ -232,7 +257,8 @@ def main():
                    "kernel_path": "fixed8 byte map (all codes 8 bits)" if state.get("fixed8") else "general bit pack/decode",
                    "parallelism": f"shard{world}", "collective": (f"all_gather int64[258] (weights + tail bytes) over {'RCCL' if args.dist_backend == 'nccl' else 'gloo (rehearsal)'}" if world > 1 else None)},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": ach, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                     "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": traffic, "traffic_source": traffic_src},
+                     "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": traffic, "traffic_source": traffic_src,
+                     "copy_ceiling_measured": round(copy_gbps, 1), "frac_of_copy_ceiling": round(ach / copy_gbps, 4)},
         "kernels": kernels,
         "kernel_enc_GBps": round(n / (enc_ms * 1e-3) / 1e9, 1),
         "host_gap_ms": round(ms_per_step - sum(k["avg_ms"] for k in kernels.values()), 4),

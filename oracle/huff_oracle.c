@@ -776,12 +776,24 @@ static void* fast_worker(void* p)
         uint8_t l = j->len[j->in[i]];
         acc = (acc << l) | j->code[j->in[i]];
         nacc += l;
-        while (nacc >= 8) {
-            uint8_t v = (uint8_t)(acc >> (nacc - 8));
-            if (wbyte == first_byte) *j->head = v; else j->out[wbyte] = v;
-            wbyte++;
-            nacc -= 8;
+        if (nacc >= 64) { /* 8 whole bytes, big-endian */
+            uint64_t v = (uint64_t)(acc >> (nacc - 64));
+            nacc -= 64;
+            if (wbyte == first_byte) {
+                *j->head = (uint8_t)(v >> 56);
+                for (int k = 1; k < 8; ++k) j->out[wbyte + k] = (uint8_t)(v >> (56 - 8 * k));
+            } else {
+                v = __builtin_bswap64(v);
+                memcpy(j->out + wbyte, &v, 8);
+            }
+            wbyte += 8;
         }
+    }
+    while (nacc >= 8) {
+        uint8_t v = (uint8_t)(acc >> (nacc - 8));
+        if (wbyte == first_byte) *j->head = v; else j->out[wbyte] = v;
+        wbyte++;
+        nacc -= 8;
     }
     if (nacc > 0) {
         uint8_t v = (uint8_t)(acc << (8 - nacc));
@@ -793,6 +805,13 @@ static void* fast_worker(void* p)
 int orc_fast_encode(const uint8_t* in, size_t n, const uint64_t code[256],
                     const uint8_t len[256], int threads, uint64_t bit_base,
                     uint8_t* out, size_t cap, uint64_t* total_bits)
+{
+    return orc_fast_encode_idx(in, n, code, len, threads, bit_base, out, cap, total_bits, NULL);
+}
+
+int orc_fast_encode_idx(const uint8_t* in, size_t n, const uint64_t code[256],
+                        const uint8_t len[256], int threads, uint64_t bit_base,
+                        uint8_t* out, size_t cap, uint64_t* total_bits, uint64_t* job_start)
 {
     if (threads < 1) threads = 1;
     if ((size_t)threads > n / 4096 + 1) threads = (int)(n / 4096 + 1);
@@ -811,6 +830,8 @@ int orc_fast_encode(const uint8_t* in, size_t n, const uint64_t code[256],
     uint64_t pos = bit_base;
     for (int i = 0; i < threads; ++i) { jobs[i].start_bit = pos; pos += jobs[i].bits; }
     *total_bits = pos - bit_base;
+    if (job_start)
+        for (int i = 0; i < threads; ++i) job_start[i] = jobs[i].start_bit;
     size_t need = (size_t)((pos + 7) / 8);
     if (need > cap) { free(jobs); free(th); free(heads); return ORC_E_BUFFER; }
     /* every byte from bit_base/8 .. need is written by exactly one job or merged */
@@ -839,6 +860,99 @@ static void* hist_worker(void* p)
     memset(j->w, 0, sizeof(j->w));
     for (size_t i = j->lo; i < j->hi; ++i) j->w[j->in[i]]++;
     return NULL;
+}
+
+/* table-driven decode over the encoder's job partition: job i decodes the
+ * letters [lo_i, hi_i) (split as in orc_fast_encode_idx) from bit start[i].
+ * A 2^12-entry table resolves codes of <= 12 bits in one step; longer codes
+ * continue bit by bit from the node the table reached. */
+#define FAST_K 12
+#define FAST_LEAF 0x80000000u
+
+typedef struct {
+    const uint8_t* comp;
+    size_t comp_bytes;
+    const orc_tree* t;
+    const uint32_t* lut;
+    size_t lo, hi;
+    uint64_t start;
+    uint8_t* out;
+} fdec_job;
+
+static inline uint64_t peek64(const uint8_t* comp, size_t nbytes, uint64_t bit)
+{
+    uint64_t byte = bit >> 3, v = 0;
+    unsigned sh0 = (unsigned)(bit & 7);
+    if (byte + 9 <= nbytes) {
+        memcpy(&v, comp + byte, 8);
+        v = __builtin_bswap64(v);
+        return sh0 ? (v << sh0) | (comp[byte + 8] >> (8 - sh0)) : v;
+    }
+    for (int k = 0; k < 8; ++k) v = (v << 8) | (byte + k < nbytes ? comp[byte + k] : 0);
+    unsigned sh = (unsigned)(bit & 7);
+    uint64_t nx = byte + 8 < nbytes ? comp[byte + 8] : 0;
+    return sh ? (v << sh) | (nx >> (8 - sh)) : v;
+}
+
+static void* fdec_worker(void* p)
+{
+    fdec_job* j = (fdec_job*)p;
+    const orc_node* nd = j->t->nodes;
+    uint64_t pos = j->start;
+    for (size_t i = j->lo; i < j->hi; ++i) {
+        uint64_t w = peek64(j->comp, j->comp_bytes, pos);
+        uint32_t e = j->lut[w >> (64 - FAST_K)];
+        if (e & FAST_LEAF) {
+            j->out[i] = (uint8_t)e;
+            pos += (e >> 8) & 0xFF;
+            continue;
+        }
+        int32_t cur = (int32_t)e;
+        pos += FAST_K;
+        while (!nd[cur].leaf) {
+            uint64_t bit = (j->comp[pos >> 3] >> (7 - (pos & 7))) & 1;
+            cur = bit ? nd[cur].right : nd[cur].left;
+            pos++;
+        }
+        j->out[i] = (uint8_t)nd[cur].letter;
+    }
+    return NULL;
+}
+
+int orc_fast_decode(const uint8_t* comp, size_t comp_bytes, const orc_tree* t, size_t n,
+                    int threads, const uint64_t* job_start, uint8_t* out)
+{
+    if (threads < 1) threads = 1;
+    if ((size_t)threads > n / 4096 + 1) threads = (int)(n / 4096 + 1);
+    uint32_t* lut = (uint32_t*)malloc(sizeof(uint32_t) << FAST_K);
+    const orc_node* nd = t->nodes;
+    for (uint32_t p = 0; p < (1u << FAST_K); ++p) {
+        int32_t cur = t->root;
+        uint32_t d = 0;
+        if (nd[cur].leaf) { /* single-leaf tree: one letter per bit */
+            lut[p] = FAST_LEAF | (1u << 8) | (uint32_t)(uint8_t)nd[cur].letter;
+            continue;
+        }
+        while (!nd[cur].leaf && d < FAST_K) {
+            cur = ((p >> (FAST_K - 1 - d)) & 1) ? nd[cur].right : nd[cur].left;
+            d++;
+        }
+        lut[p] = nd[cur].leaf ? FAST_LEAF | (d << 8) | (uint32_t)(uint8_t)nd[cur].letter : (uint32_t)cur;
+    }
+    fdec_job* jobs = (fdec_job*)calloc((size_t)threads, sizeof(fdec_job));
+    pthread_t* th = (pthread_t*)calloc((size_t)threads, sizeof(pthread_t));
+    size_t per = n / (size_t)threads;
+    for (int i = 0; i < threads; ++i) {
+        fdec_job* j = &jobs[i];
+        j->comp = comp; j->comp_bytes = comp_bytes; j->t = t; j->lut = lut; j->out = out;
+        j->lo = per * (size_t)i;
+        j->hi = (i == threads - 1) ? n : per * (size_t)(i + 1);
+        j->start = job_start[i];
+        pthread_create(&th[i], NULL, fdec_worker, j);
+    }
+    for (int i = 0; i < threads; ++i) pthread_join(th[i], NULL);
+    free(jobs); free(th); free(lut);
+    return ORC_OK;
 }
 
 void orc_fast_hist(const uint8_t* in, size_t n, int threads, uint64_t w[256])

@@ -108,6 +108,15 @@ size_t orc_offset_bytes(const uint8_t* bytes, size_t n, size_t shift, uint8_t* o
 int orc_fast_encode(const uint8_t* in, size_t n, const uint64_t code[256],
                     const uint8_t len[256], int threads, uint64_t bit_base,
                     uint8_t* out, size_t cap, uint64_t* total_bits);
+/* as orc_fast_encode, also writing each job's absolute start bit (the job
+ * split: threads clamped to n/4096+1, job i = [i*(n/T), (i+1)*(n/T)), the last
+ * takes the remainder) into job_start[T] when non-NULL */
+int orc_fast_encode_idx(const uint8_t* in, size_t n, const uint64_t code[256],
+                        const uint8_t len[256], int threads, uint64_t bit_base,
+                        uint8_t* out, size_t cap, uint64_t* total_bits, uint64_t* job_start);
+/* table-driven multithreaded decode of n letters over that job split */
+int orc_fast_decode(const uint8_t* comp, size_t comp_bytes, const orc_tree* t, size_t n,
+                    int threads, const uint64_t* job_start, uint8_t* out);
 void orc_fast_hist(const uint8_t* in, size_t n, int threads, uint64_t w[256]);
 
 /* ---------------- synthetic inputs (not reference code) ---------------- */

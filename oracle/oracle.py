@@ -88,6 +88,9 @@ def lib():
         L.orc_offset_bytes.restype = sz
         L.orc_fast_encode.argtypes = [u8p, sz, u64p, u8p, C.c_int, C.c_uint64, u8p, sz, C.POINTER(C.c_uint64)]
         L.orc_fast_hist.argtypes = [u8p, sz, C.c_int, u64p]
+        L.orc_fast_encode_idx.argtypes = [u8p, sz, u64p, u8p, C.c_int, C.c_uint64, u8p, sz,
+                                          C.POINTER(C.c_uint64), u64p]
+        L.orc_fast_decode.argtypes = [u8p, sz, C.c_void_p, sz, C.c_int, u64p, u8p]
         L.orc_splitmix64.argtypes = [C.c_uint64, C.c_uint64]
         L.orc_splitmix64.restype = C.c_uint64
         L.orc_gen_uniform.argtypes = [C.c_uint64, C.c_uint64, sz, u8p]
@@ -341,6 +344,34 @@ def fast_encode(data: np.ndarray, code: np.ndarray, ln: np.ndarray, threads: int
         raise OracleError(e)
     nbytes = (bit_base + tb.value + 7) // 8
     return out[:nbytes], tb.value
+
+
+def fast_roundtrip(data: np.ndarray, threads: int = 8):
+    """table-driven CPU path on all `threads`: histogram, tree, encode,
+    decode (over the encoder's job split). Returns (comp, decoded, t_enc,
+    t_dec) in seconds. The "cpu-fast" reference of SURVEY §8d."""
+    a, p = _u8(data)
+    t0 = now()
+    w = fast_hist(a, threads)
+    tree = Tree.from_weights(weights_from_array(w))
+    code, ln = tree.code_table()
+    total = int(np.dot(w.astype(np.uint64), ln.astype(np.uint64)))
+    out = np.empty((total + 7) // 8 + 1, np.uint8)
+    tb = C.c_uint64()
+    starts = np.zeros(max(threads, 1), np.uint64)
+    e = lib().orc_fast_encode_idx(p, a.size, code.ctypes.data_as(C.POINTER(C.c_uint64)),
+                                  ln.ctypes.data_as(C.POINTER(C.c_uint8)), threads, 0,
+                                  out.ctypes.data_as(C.POINTER(C.c_uint8)), out.size, C.byref(tb),
+                                  starts.ctypes.data_as(C.POINTER(C.c_uint64)))
+    if e:
+        raise OracleError(e)
+    t1 = now()
+    nbytes = (tb.value + 7) // 8
+    back = np.empty(a.size, np.uint8)
+    lib().orc_fast_decode(out.ctypes.data_as(C.POINTER(C.c_uint8)), nbytes, tree.h, a.size, threads,
+                          starts.ctypes.data_as(C.POINTER(C.c_uint64)), back.ctypes.data_as(C.POINTER(C.c_uint8)))
+    t2 = now()
+    return out[:nbytes], back, t1 - t0, t2 - t1
 
 
 def fast_hist(data: np.ndarray, threads: int = 8) -> np.ndarray:

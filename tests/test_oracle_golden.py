@@ -157,3 +157,20 @@ def test_fast_checker_matches_faithful(O):
             fast, bits = O.fast_encode(data, code, ln, threads=th)
             assert fast.tobytes() == comp
         assert (O.fast_hist(data, 4) == O.weights_from_bytes(data).as_array()).all()
+
+
+def test_fast_roundtrip_matches_faithful(O):
+    """the cpu-fast leg of bench.py (table-driven encode + decode over the
+    encoder's job split) == the bit-serial restatement, incl. codes > 12 bits
+    and a single-letter input"""
+    rng = np.random.default_rng(4)
+    skew = np.minimum(rng.geometric(0.35, 200_000) - 1, 255).astype(np.uint8)  # long codes
+    cases = [np.frombuffer(b"z" * 9000, np.uint8), rng.integers(0, 256, 100_000, dtype=np.uint8), skew,
+             O.gen_text(5, 250_001)]
+    for data in cases:
+        t = O.Tree.from_weights(O.weights_from_bytes(data))
+        comp, pad = O.compress_with_tree(data, t)
+        for th in (1, 5):
+            fast, back, _, _ = O.fast_roundtrip(data, th)
+            assert fast.tobytes() == comp
+            assert np.array_equal(back, data)
