@@ -9,10 +9,14 @@
 
 #include "runtime/runtime.hpp"
 
-namespace {
+#include "capi_util.hpp"
 
+namespace huff::capi {
+
+namespace {
 thread_local std::string t_last_error;
 thread_local uint8_t t_missing = 0;
+}  // namespace
 
 int report(const huff::Status& s) {
     if (s.code != HUFF_OK) {
@@ -27,23 +31,19 @@ int fail(int code, const char* msg) {
     return code;
 }
 
-template <class F>
-int guarded(F&& f) {
-    try {
-        return report(f());
-    } catch (const std::bad_alloc&) {
-        return fail(HUFF_E_INVALID_ARG, "host allocation failed");
-    } catch (const std::exception& e) {
-        return fail(HUFF_E_INVALID_ARG, e.what());
-    }
-}
+const char* last_error() { return t_last_error.c_str(); }
+uint8_t last_missing() { return t_missing; }
 
-}  // namespace
+}  // namespace huff::capi
+
+using huff::capi::fail;
+using huff::capi::guarded;
+using huff::capi::report;
 
 extern "C" {
 
-const char* huff_last_error(void) { return t_last_error.c_str(); }
-uint8_t huff_last_missing_letter(void) { return t_missing; }
+const char* huff_last_error(void) { return huff::capi::last_error(); }
+uint8_t huff_last_missing_letter(void) { return huff::capi::last_missing(); }
 const char* huff_version(void) { return "huffgpu 0.1 (gfx950)"; }
 
 // --------------------------------------------------------------------------

@@ -104,6 +104,45 @@ struct BytemapArgs {
     uint32_t* sub_bit;            // may be null
 };
 
+// wider letters (wide.hip): W-byte keys, hash-table code lookup
+struct WideArgs {
+    const uint8_t* in;            // n letters of `width` bytes, native layout, 16-B aligned
+    uint64_t n;
+    uint32_t width;               // 1, 2, 4, 8, 16
+    uint32_t log2_slots;          // hash table: 2^log2_slots slots
+    const uint8_t* keys;          // [slots * width]
+    const uint64_t* vals;         // [slots] (code << 8) | len, 0 = empty
+    uint32_t table_in_lds;        // stage the table in LDS (wide_table_lds_bytes)
+    uint32_t nchunks;             // ceil(n / kChunk)
+    uint64_t* chunk_bits;         // [nchunks]            (bits pass)
+    const uint64_t* chunk_start;  // [nchunks + 1]        (pack pass)
+    uint32_t* sub_bit;            // [ceil(n / kSub)]
+    unsigned long long* first_missing;  // min index of a letter without a code
+    uint32_t* out;                // 4-B aligned, ceil(bits / 32) words
+};
+struct WideDecArgs {
+    const uint8_t* comp;          // 4-B aligned
+    uint64_t comp_bytes;
+    const uint32_t* lut;          // leaf = (len << 24) | leaf, ptr = kLutPtr | offset
+    uint32_t lut_bits;
+    const uint8_t* letters;       // [leaves * width]
+    uint32_t width;
+    const uint64_t* chunk_start;
+    const uint32_t* sub_bit;
+    const uint64_t* sub_abs;      // non-null: index-free restart points
+    uint32_t nchunks;
+    uint64_t n;
+    uint8_t* out;                 // n * width bytes
+};
+size_t wide_table_lds_bytes(uint32_t width, uint32_t log2_slots);
+hipError_t launch_wide_bits(const WideArgs& a, hipStream_t s);
+hipError_t launch_wide_pack(const WideArgs& a, hipStream_t s);
+hipError_t launch_wide_decode(const WideDecArgs& a, hipStream_t s);
+// build_weights_map on the device (wweights.hip): sorted distinct letters and
+// their counts. d_tmp == nullptr: *tmp_bytes = scratch needed.
+hipError_t wide_weights(uint32_t width, const void* d_in, uint64_t n, void* d_sorted, void* d_uniq,
+                        uint64_t* d_counts, uint64_t* d_nruns, void* d_tmp, size_t* tmp_bytes, hipStream_t s);
+
 size_t pack_lds_bytes(bool long_codes, uint32_t stage_words);
 size_t decode_lds_bytes(uint32_t lut_bits, uint32_t rep_log2);
 constexpr uint32_t kDecodeSingle = 1;  // decode.hip k_decode_short

@@ -1,5 +1,6 @@
 // container.cpp — CompressData byte container (huff_coding/src/comp.rs).
 #include <cstring>
+#include <functional>
 
 #include "huff_coding.hpp"
 
@@ -20,10 +21,9 @@ std::vector<uint8_t> unpack_msb0(const uint8_t* bytes, size_t nbits) {
     return bits;
 }
 
-Status container_to_bytes(const HuffTree& t, const uint8_t* comp, size_t len, uint8_t padding,
-                          std::vector<uint8_t>& out) {
+Status container_bits_to_bytes(const std::vector<uint8_t>& tree_bits, const uint8_t* comp, size_t len,
+                               uint8_t padding, std::vector<uint8_t>& out) {
     // comp.rs:279-300
-    std::vector<uint8_t> tree_bits = t.as_bin();
     uint8_t tree_pad = calc_padding_bits(tree_bits.size());
     uint32_t tree_len = static_cast<uint32_t>((tree_bits.size() + tree_pad) / 8);
     std::vector<uint8_t> tree_bytes = pack_msb0(tree_bits);
@@ -39,8 +39,13 @@ Status container_to_bytes(const HuffTree& t, const uint8_t* comp, size_t len, ui
     return Status::ok();
 }
 
-Status container_from_bytes(const uint8_t* bytes, size_t n, HuffTree& tree, uint8_t& padding,
-                            size_t& comp_off, size_t& comp_len) {
+Status container_to_bytes(const HuffTree& t, const uint8_t* comp, size_t len, uint8_t padding,
+                          std::vector<uint8_t>& out) {
+    return container_bits_to_bytes(t.as_bin(), comp, len, padding, out);
+}
+
+Status container_parse(const uint8_t* bytes, size_t n, const std::function<Status(const std::vector<uint8_t>&)>& tree,
+                       uint8_t& padding, size_t& comp_off, size_t& comp_len) {
     // comp.rs:128-184, errors in the reference's order; its panics are
     // returned as their own status codes.
     if (n < 1) return Status::err(HUFF_E_FROM_BYTES, "slice is empty");
@@ -54,7 +59,7 @@ Status container_from_bytes(const uint8_t* bytes, size_t n, HuffTree& tree, uint
     size_t nbits = tree_len * 8;
     nbits = tree_pad > nbits ? 0 : nbits - tree_pad;  // `for _ in 0..tree_padding_bits { b.pop(); }`
     std::vector<uint8_t> bits = unpack_msb0(bytes + 5, nbits);
-    if (HuffTree::try_from_bin(bits, tree)) return Status::err(HUFF_E_FROM_BYTES, "invalid tree in slice");
+    if (tree(bits)) return Status::err(HUFF_E_FROM_BYTES, "invalid tree in slice");
     comp_off = 5 + tree_len;
     comp_len = n - comp_off;
     // CompressData::new (comp.rs:55-68)
@@ -62,6 +67,13 @@ Status container_from_bytes(const uint8_t* bytes, size_t n, HuffTree& tree, uint
     if (data_pad > 7) return Status::err(HUFF_E_PADDING, "padding bits cannot be larger than 7");
     padding = data_pad;
     return Status::ok();
+}
+
+Status container_from_bytes(const uint8_t* bytes, size_t n, HuffTree& tree, uint8_t& padding,
+                            size_t& comp_off, size_t& comp_len) {
+    return container_parse(
+        bytes, n, [&](const std::vector<uint8_t>& bits) { return HuffTree::try_from_bin(bits, tree); }, padding,
+        comp_off, comp_len);
 }
 
 }  // namespace huff

@@ -7,6 +7,7 @@
 
 #include <array>
 #include <cstdint>
+#include <functional>
 #include <memory>
 #include <vector>
 
@@ -62,6 +63,13 @@ public:
     static Status from_weights(const ByteWeights& w, HuffTree& out);
     // Generic leaf list in push order (used for the tree_init known answer).
     static Status from_leaves(const uint8_t* letters, const uint64_t* weights, size_t n, HuffTree& out);
+    // A tree of the given nodes (the generic-letter tree's shape, wide.hpp).
+    static HuffTree from_nodes(std::vector<HuffNode> nodes, int32_t root) {
+        HuffTree t;
+        t.nodes_ = std::move(nodes);
+        t.root_ = root;
+        return t;
+    }
     // tree_inner.rs:522-604 try_from_bin (bits one per element).
     static Status try_from_bin(const std::vector<uint8_t>& bits, HuffTree& out);
 
@@ -110,6 +118,11 @@ std::vector<uint8_t> unpack_msb0(const uint8_t* bytes, size_t nbits);
 
 Status container_to_bytes(const HuffTree& t, const uint8_t* comp, size_t len, uint8_t padding,
                           std::vector<uint8_t>& out);
+Status container_bits_to_bytes(const std::vector<uint8_t>& tree_bits, const uint8_t* comp, size_t len,
+                               uint8_t padding, std::vector<uint8_t>& out);
+// comp.rs:128-184 with the tree parsed by `tree` (try_from_bin of the bits)
+Status container_parse(const uint8_t* bytes, size_t n, const std::function<Status(const std::vector<uint8_t>&)>& tree,
+                       uint8_t& padding, size_t& comp_off, size_t& comp_len);
 // On success comp_off/comp_len locate the data inside `bytes`.
 Status container_from_bytes(const uint8_t* bytes, size_t n, HuffTree& tree, uint8_t& padding,
                             size_t& comp_off, size_t& comp_len);

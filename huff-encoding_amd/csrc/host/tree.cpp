@@ -1,87 +1,17 @@
 // tree.cpp — HuffTree on the host (huff_coding/src/tree/).
 //
 // The tree decides every output bit, so it is built with the reference's
-// exact tie order: the reference pushes leaves into a Rust std BinaryHeap whose
-// Ord is reversed on weight only (branch_heap.rs:67-71, leaf.rs:31-35) and
-// repeatedly pops the two minima (tree_inner.rs:289-303). RustMaxHeap below is
-// that std heap's algorithm (sift_up on push; on pop the last element is
-// swapped into the root, sifted down to the bottom always taking the right
-// child on ties, then sifted up), keyed so that "a <= b" means a.w >= b.w.
+// exact tie order: leaves go into RustMaxHeap (rust_heap.hpp) in the weights'
+// iteration order and the two minima are popped repeatedly
+// (tree_inner.rs:289-303).
 #include <algorithm>
 #include <utility>
 
 #include "huff_coding.hpp"
+#include "rust_heap.hpp"
 
 namespace huff {
 
-namespace {
-
-struct HeapEntry {
-    uint64_t w;
-    int32_t node;
-};
-
-class RustMaxHeap {
-public:
-    explicit RustMaxHeap(size_t reserve) : v_(reserve) {}
-    size_t size() const { return n_; }
-
-    void push(HeapEntry e) {
-        v_[n_++] = e;
-        sift_up(0, n_ - 1);
-    }
-
-    HeapEntry pop() {
-        HeapEntry top = v_[--n_];
-        if (n_) {
-            std::swap(top, v_[0]);
-            sift_down_to_bottom(0);
-        }
-        return top;
-    }
-
-private:
-    // "a <= b" under the reversed Ord of HuffBranchHeapItem
-    static bool le(const HeapEntry& a, const HeapEntry& b) { return a.w >= b.w; }
-
-    size_t sift_up(size_t start, size_t pos) {
-        HeapEntry* v = v_.data();
-        const HeapEntry hole = v[pos];
-        while (pos > start) {
-            const size_t parent = (pos - 1) >> 1;
-            if (le(hole, v[parent])) break;
-            v[pos] = v[parent];
-            pos = parent;
-        }
-        v[pos] = hole;
-        return pos;
-    }
-
-    void sift_down_to_bottom(size_t pos) {
-        HeapEntry* v = v_.data();
-        const size_t end = n_;
-        const size_t start = pos;
-        const HeapEntry hole = v[pos];
-        size_t child = 2 * pos + 1;
-        while (end >= 2 && child <= end - 2) {
-            child += le(v[child], v[child + 1]) ? 1 : 0;
-            v[pos] = v[child];
-            pos = child;
-            child = 2 * pos + 1;
-        }
-        if (child == end - 1) {
-            v[pos] = v[child];
-            pos = child;
-        }
-        v[pos] = hole;
-        sift_up(start, pos);
-    }
-
-    std::vector<HeapEntry> v_;
-    size_t n_ = 0;
-};
-
-}  // namespace
 
 Status HuffTree::from_leaves(const uint8_t* letters, const uint64_t* weights, size_t n, HuffTree& out) {
     if (n == 0) return Status::err(HUFF_E_EMPTY_WEIGHTS, "provided empty weights");

@@ -675,6 +675,70 @@ Status parse_block_size(const char* s, size_t* out) {
 // ---------------------------------------------------------------------------
 namespace huff {
 
+Status indexless_sync(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_bytes, uint64_t valid_bits,
+                      const huff_tree* t, IndexlessSync& st) {
+    const DecTables* dt = st.dt;
+    // segment length: a multiple of the gcd of all code lengths
+    uint32_t g = 0;
+    for (const LeafCode& lc : t->t.leaves()) g = std::gcd(g, lc.len);
+    if (g == 0) g = 1;
+    // codes <= 32 bits take the LDS-staged kernels: 1024-bit segments keep a
+    // workgroup's staging at 32 KiB (3 workgroups per CU); longer codes 2048
+    const uint64_t seg_target = dt->maxdepth <= 32 ? 1024 : 2048;
+    const uint64_t S = static_cast<uint64_t>(g) * ((seg_target + g - 1) / g);
+    const uint64_t nseg = (valid_bits + S - 1) / S;
+    if (nseg > 0xFFFFFFFFull) return Status::err(HUFF_E_INVALID_ARG, "stream too long for one decode");
+    HUFF_TRY(st.s.ensure(nseg * 8));
+    HUFF_TRY(st.x0.ensure(nseg * 8));
+    HUFF_TRY(st.x1.ensure(nseg * 8));
+    HUFF_TRY(st.c.ensure(nseg * 8));
+    HUFF_TRY(st.off.ensure((nseg + 1) * 8));
+    HUFF_TRY(st.flag.ensure(4));
+    dev::IndexlessArgs& a = st.a;
+    a = dev::IndexlessArgs{};
+    a.comp = d_comp;
+    a.comp_bytes = comp_bytes;
+    a.valid_bits = valid_bits;
+    a.seg_bits = S;
+    a.nseg = nseg;
+    a.lut = static_cast<const uint32_t*>(ctx->d_lut.p);
+    a.lut_bits = dt->bits;
+    a.s = static_cast<uint64_t*>(st.s.p);
+    a.x = static_cast<uint64_t*>(st.x0.p);
+    a.c = static_cast<uint64_t*>(st.c.p);
+    a.mlut = static_cast<const uint32_t*>(ctx->d_lut.p) + dt->moff;
+    a.mlut_bits = dt->mbits;
+    a.max_len = dt->maxdepth;
+    hipStream_t strm = ctx->stream;
+    HIP_TRY(dev::launch_indexless_spec(a, strm));
+    uint64_t* xa = static_cast<uint64_t*>(st.x0.p);
+    uint64_t* xb = static_cast<uint64_t*>(st.x1.p);
+    bool settled = false;
+    for (int it = 0; it < 32 && !settled; ++it) {
+        HIP_TRY(hipMemsetAsync(st.flag.p, 0, 4, strm));
+        HIP_TRY(dev::launch_indexless_fix(a, xa, xb, static_cast<unsigned int*>(st.flag.p), strm));
+        unsigned int changed = 0;
+        HIP_TRY(hipMemcpyAsync(&changed, st.flag.p, 4, hipMemcpyDeviceToHost, strm));
+        HUFF_TRY(ctx->sync());
+        std::swap(xa, xb);
+        settled = changed == 0;
+    }
+    if (!settled) HIP_TRY(dev::launch_indexless_settle(a, xa, strm));
+    HUFF_TRY(st.tsum.ensure((nseg / 1024 + 2) * 8));
+    HIP_TRY(dev::launch_scan(static_cast<const uint64_t*>(st.c.p), static_cast<uint32_t>(nseg), 0,
+                             static_cast<uint64_t*>(st.off.p), static_cast<uint64_t*>(st.tsum.p), strm));
+    st.total = 0;
+    HIP_TRY(hipMemcpyAsync(&st.total, static_cast<uint64_t*>(st.off.p) + nseg, 8, hipMemcpyDeviceToHost, strm));
+    return ctx->sync();
+}
+
+Status indexless_mark(huff_ctx* ctx, IndexlessSync& st, DevBuf& sub_abs) {
+    HUFF_TRY(sub_abs.ensure(((st.total + dev::kSub - 1) / dev::kSub) * 8 + 8));
+    HIP_TRY(dev::launch_indexless_mark(st.a, static_cast<const uint64_t*>(st.off.p),
+                                       static_cast<uint64_t*>(sub_abs.p), ctx->stream));
+    return Status::ok();
+}
+
 Status decode_indexless_dev(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_bytes, uint64_t valid_bits,
                             const huff_tree* t, DevBuf& out, uint64_t* nsym, uint8_t* d_user, size_t user_cap) {
     *nsym = 0;
@@ -688,7 +752,6 @@ Status decode_indexless_dev(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_
         return out.ensure(need + 16);
     };
     auto out_at = [&]() { return d_user ? d_user : static_cast<uint8_t*>(out.p); };
-    uint64_t* nsym_out_alias = nsym;
     if (valid_bits == 0) return Status::ok();
     if (reinterpret_cast<uintptr_t>(d_comp) & 3)
         return Status::err(HUFF_E_INVALID_ARG, "compressed stream must be 4-byte aligned");
@@ -696,80 +759,29 @@ Status decode_indexless_dev(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_
     const DecTables* dt = nullptr;
     HUFF_TRY(ctx->upload_dec_tables(t, &dt));
     if (dt->all8 && !fixed8_disabled()) {  // every code 8 bits: one symbol per whole byte
-        const uint64_t nsym = valid_bits / 8;
-        *nsym_out_alias = nsym;
-        HUFF_TRY(out_ptr(nsym));
+        const uint64_t n = valid_bits / 8;
+        *nsym = n;
+        HUFF_TRY(out_ptr(n));
         dev::BytemapArgs m{};
         m.src = d_comp;
         m.dst = out_at();
-        m.n = nsym;
+        m.n = n;
         for (int b = 0; b < 256; ++b) m.map[b] = static_cast<uint8_t>(dt->lut[b]);
         HIP_TRY(dev::launch_bytemap(m, ctx->stream));
-        *nsym_out_alias = nsym;
         return Status::ok();
     }
-    // segment length: a multiple of the gcd of all code lengths
-    uint32_t g = 0;
-    for (const LeafCode& lc : t->t.leaves()) g = std::gcd(g, lc.len);
-    if (g == 0) g = 1;
-    // codes <= 32 bits take the LDS-staged kernels: 1024-bit segments keep a
-    // workgroup's staging at 32 KiB (3 workgroups per CU); longer codes 2048
-    const uint64_t seg_target = dt->maxdepth <= 32 ? 1024 : 2048;
-    const uint64_t S = static_cast<uint64_t>(g) * ((seg_target + g - 1) / g);
-    const uint64_t nseg = (valid_bits + S - 1) / S;
-    DevBuf s, x0, x1, c, off, flag;
-    HUFF_TRY(s.ensure(nseg * 8));
-    HUFF_TRY(x0.ensure(nseg * 8));
-    HUFF_TRY(x1.ensure(nseg * 8));
-    HUFF_TRY(c.ensure(nseg * 8));
-    HUFF_TRY(off.ensure((nseg + 1) * 8));
-    HUFF_TRY(flag.ensure(4));
-    dev::IndexlessArgs a{};
-    a.comp = d_comp;
-    a.comp_bytes = comp_bytes;
-    a.valid_bits = valid_bits;
-    a.seg_bits = S;
-    a.nseg = nseg;
-    a.lut = static_cast<const uint32_t*>(ctx->d_lut.p);
-    a.lut_bits = dt->bits;
-    a.s = static_cast<uint64_t*>(s.p);
-    a.x = static_cast<uint64_t*>(x0.p);
-    a.c = static_cast<uint64_t*>(c.p);
-    a.mlut = static_cast<const uint32_t*>(ctx->d_lut.p) + dt->moff;
-    a.mlut_bits = dt->mbits;
-    a.max_len = dt->maxdepth;
-    hipStream_t st = ctx->stream;
-    HIP_TRY(dev::launch_indexless_spec(a, st));
-    uint64_t* xa = static_cast<uint64_t*>(x0.p);
-    uint64_t* xb = static_cast<uint64_t*>(x1.p);
-    bool settled = false;
-    for (int it = 0; it < 32 && !settled; ++it) {
-        HIP_TRY(hipMemsetAsync(flag.p, 0, 4, st));
-        HIP_TRY(dev::launch_indexless_fix(a, xa, xb, static_cast<unsigned int*>(flag.p), st));
-        unsigned int changed = 0;
-        HIP_TRY(hipMemcpyAsync(&changed, flag.p, 4, hipMemcpyDeviceToHost, st));
-        HUFF_TRY(ctx->sync());
-        std::swap(xa, xb);
-        settled = changed == 0;
-    }
-    if (!settled) HIP_TRY(dev::launch_indexless_settle(a, xa, st));
-    if (nseg > 0xFFFFFFFFull) return Status::err(HUFF_E_INVALID_ARG, "stream too long for one decode");
-    DevBuf tsum;
-    HUFF_TRY(tsum.ensure((nseg / 1024 + 2) * 8));
-    HIP_TRY(dev::launch_scan(static_cast<const uint64_t*>(c.p), static_cast<uint32_t>(nseg), 0,
-                             static_cast<uint64_t*>(off.p), static_cast<uint64_t*>(tsum.p), st));
-    uint64_t total = 0;
-    HIP_TRY(hipMemcpyAsync(&total, static_cast<uint64_t*>(off.p) + nseg, 8, hipMemcpyDeviceToHost, st));
-    HUFF_TRY(ctx->sync());
+    IndexlessSync st;
+    st.dt = dt;
+    HUFF_TRY(indexless_sync(ctx, d_comp, comp_bytes, valid_bits, t, st));
+    const uint64_t total = st.total;
     *nsym = total;
     HUFF_TRY(out_ptr(total));
+    hipStream_t strm = ctx->stream;
     const bool aligned16 = !(reinterpret_cast<uintptr_t>(d_comp) & 15) && !(reinterpret_cast<uintptr_t>(out_at()) & 15);
-    if (dev::indexless_staged(a) && total && aligned16) {
+    if (dev::indexless_staged(st.a) && total && aligned16) {
         // a restart index for the ring decoder, then the ordinary restart-index decode
         DevBuf sub_abs;
-        HUFF_TRY(sub_abs.ensure(((total + dev::kSub - 1) / dev::kSub) * 8));
-        HIP_TRY(dev::launch_indexless_mark(a, static_cast<const uint64_t*>(off.p),
-                                           static_cast<uint64_t*>(sub_abs.p), st));
+        HUFF_TRY(indexless_mark(ctx, st, sub_abs));
         dev::DecodeArgs d{};
         d.comp = d_comp;
         d.comp_bytes = comp_bytes;
@@ -779,19 +791,17 @@ Status decode_indexless_dev(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_
         d.sub_abs = static_cast<const uint64_t*>(sub_abs.p);
         d.nchunks = static_cast<uint32_t>((total + dev::kChunk - 1) / dev::kChunk);
         d.max_len = dt->maxdepth;
-        d.mlut = a.mlut;
-        d.mlut_bits = a.mlut_bits;
+        d.mlut = st.a.mlut;
+        d.mlut_bits = st.a.mlut_bits;
         d.variant = dev::kDecodeRing;
         d.n = total;
         d.out = out_at();
-        HIP_TRY(dev::launch_decode_ring(d, st));
-        HIP_TRY(hipEventRecord(ctx->lut_free, st));
-        HUFF_TRY(ctx->sync());  // sub_abs is freed on return
-        return Status::ok();
+        HIP_TRY(dev::launch_decode_ring(d, strm));
+        HIP_TRY(hipEventRecord(ctx->lut_free, strm));
+        return ctx->sync();  // sub_abs is freed on return
     }
-    HIP_TRY(dev::launch_indexless_emit(a, static_cast<const uint64_t*>(off.p), out_at(), st));
-    HIP_TRY(hipEventRecord(ctx->lut_free, st));
-    *nsym = total;
+    HIP_TRY(dev::launch_indexless_emit(st.a, static_cast<const uint64_t*>(st.off.p), out_at(), strm));
+    HIP_TRY(hipEventRecord(ctx->lut_free, strm));
     return Status::ok();
 }
 

@@ -170,6 +170,18 @@ Status parse_block_size(const char* s, size_t* out);
 Status decode_indexless_dev(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_bytes, uint64_t valid_bits,
                             const huff_tree* t, DevBuf& out, uint64_t* nsym, uint8_t* d_user = nullptr,
                             size_t user_cap = 0);
+// the self-synchronising part of the index-free decode (spec, fix, scan):
+// symbol offsets per segment in `off`, the symbol count in `total`
+struct IndexlessSync {
+    const DecTables* dt = nullptr;  // tables of the tree, uploaded to ctx->d_lut
+    DevBuf s, x0, x1, c, off, flag, tsum;
+    dev::IndexlessArgs a{};
+    uint64_t total = 0;
+};
+Status indexless_sync(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_bytes, uint64_t valid_bits,
+                      const huff_tree* t, IndexlessSync& st);
+// sub_abs[g] = first bit of symbol 256 g (needs dev::indexless_staged(st.a))
+Status indexless_mark(huff_ctx* ctx, IndexlessSync& st, DevBuf& sub_abs);
 Status decode_indexless_host(huff_ctx* ctx, const uint8_t* comp, size_t len, uint64_t valid_bits,
                              const huff_tree* t, std::vector<uint8_t>& out);
 }  // namespace huff

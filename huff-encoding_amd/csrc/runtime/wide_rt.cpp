@@ -1,0 +1,337 @@
+// wide_rt.cpp — the wider-letter job and host-pointer pipelines
+// (wide_rt.hpp; kernels in device/wide.hip, device/wweights.hip).
+#include "wide_rt.hpp"
+
+#include <atomic>
+#include <cstring>
+
+namespace {
+std::atomic<uint64_t> g_wtree_ids{1};
+constexpr size_t kTableLdsMax = 64 * 1024;  // stage the code hash table in LDS up to this
+}  // namespace
+
+#define HIP_TRY(expr) HIP_TRY_RT(expr)
+
+using huff::Status;
+
+huff_wtree::huff_wtree() : id(g_wtree_ids.fetch_add(1)) {}
+
+Status huff_wtree::enc_tables(const huff::WideEncTables** out) const {
+    std::lock_guard<std::mutex> g(m);
+    if (!enc) {
+        auto e = std::make_unique<huff::WideEncTables>();
+        HUFF_TRY(huff::build_wide_enc_tables(t, *e));
+        enc = std::move(e);
+    }
+    *out = enc.get();
+    return Status::ok();
+}
+
+Status huff_wtree::dec_tables(const huff::WideDecTables** out) const {
+    std::lock_guard<std::mutex> g(m);
+    if (!dec) {
+        auto d = std::make_unique<huff::WideDecTables>();
+        HUFF_TRY(huff::build_wide_dec_tables(t, *d));
+        dec = std::move(d);
+    }
+    *out = dec.get();
+    return Status::ok();
+}
+
+const huff_tree* huff_wtree::shape_tree() const {
+    std::lock_guard<std::mutex> g(m);
+    if (!shape) {
+        shape = std::make_unique<huff_tree>();
+        shape->t = t.shape();
+    }
+    return shape.get();
+}
+
+// ---------------------------------------------------------------------------
+Status huff_wenc::init(huff_ctx* c, uint32_t w, const uint8_t* d, uint64_t nletters) {
+    if (!huff::valid_width(w)) return Status::err(HUFF_E_INVALID_ARG, "letter width must be 1, 2, 4, 8 or 16 bytes");
+    if (reinterpret_cast<uintptr_t>(d) & 15) return Status::err(HUFF_E_INVALID_ARG, "letters must be 16-byte aligned");
+    if (nletters >= (uint64_t(1) << 44)) return Status::err(HUFF_E_INVALID_ARG, "too many letters for one job");
+    ctx = c;
+    width = w;
+    d_in = d;
+    n = nletters;
+    nchunks = static_cast<uint32_t>((n + huff::dev::kChunk - 1) / huff::dev::kChunk);
+    HUFF_TRY(chunk_bits.ensure((nchunks + 1) * 8));
+    HUFF_TRY(chunk_start.ensure((nchunks + 2) * 8));
+    HUFF_TRY(tsum.ensure((nchunks / 1024 + 2) * 8));
+    HUFF_TRY(sub_bit.ensure(((n + huff::dev::kSub - 1) / huff::dev::kSub + 1) * 4));
+    HUFF_TRY(missing.ensure(8));
+    return Status::ok();
+}
+
+Status huff_wenc::bits(const huff_wtree* t, uint64_t* total, huff::u128* missing_letter) {
+    HUFF_TRY(ctx->activate());
+    HUFF_TRY(t->enc_tables(&et));
+    if (et->width != width) return Status::err(HUFF_E_INVALID_ARG, "the tree's letter width differs from the job's");
+    hipStream_t s = ctx->stream;
+    if (enc_tree != t->id) {
+        HUFF_TRY(keys.ensure(et->keys.size()));
+        HUFF_TRY(vals.ensure(et->vals.size() * 8));
+        HIP_TRY(hipMemcpyAsync(keys.p, et->keys.data(), et->keys.size(), hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemcpyAsync(vals.p, et->vals.data(), et->vals.size() * 8, hipMemcpyHostToDevice, s));
+        enc_tree = t->id;
+    }
+    HIP_TRY(hipMemsetAsync(missing.p, 0xFF, 8, s));
+    huff::dev::WideArgs a{};
+    a.in = d_in;
+    a.n = n;
+    a.width = width;
+    a.log2_slots = et->log2_slots;
+    a.keys = static_cast<const uint8_t*>(keys.p);
+    a.vals = static_cast<const uint64_t*>(vals.p);
+    a.table_in_lds = huff::dev::wide_table_lds_bytes(width, et->log2_slots) <= kTableLdsMax;
+    a.nchunks = nchunks;
+    a.chunk_bits = static_cast<uint64_t*>(chunk_bits.p);
+    a.sub_bit = static_cast<uint32_t*>(sub_bit.p);
+    a.first_missing = static_cast<unsigned long long*>(missing.p);
+    HUFF_TRY(ctx->timed("wbits", [&] { return huff::dev::launch_wide_bits(a, s); }));
+    HUFF_TRY(ctx->timed("wscan", [&] {
+        return huff::dev::launch_scan(static_cast<const uint64_t*>(chunk_bits.p), nchunks, 0,
+                                      static_cast<uint64_t*>(chunk_start.p), static_cast<uint64_t*>(tsum.p), s);
+    }));
+    uint64_t hv[2] = {0, 0};
+    HIP_TRY(hipMemcpyAsync(&hv[0], static_cast<uint64_t*>(chunk_start.p) + nchunks, 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(&hv[1], missing.p, 8, hipMemcpyDeviceToHost, s));
+    HUFF_TRY(ctx->sync());
+    bits_tree = 0;
+    if (hv[1] != ~0ull) {  // comp.rs:426-432: the first letter (input order) with no code
+        uint8_t lb[16] = {};
+        HIP_TRY(hipMemcpy(lb, d_in + hv[1] * width, width, hipMemcpyDeviceToHost));
+        if (missing_letter) *missing_letter = huff::load_letter(lb, width);
+        return Status::err(HUFF_E_MISSING_LETTER, "letter not found in codes");
+    }
+    total_bits = hv[0];
+    bits_tree = t->id;
+    if (total) *total = total_bits;
+    return Status::ok();
+}
+
+Status huff_wenc::pack(const huff_wtree* t, uint8_t* d_out, size_t out_cap, uint64_t* total) {
+    if (bits_tree != t->id) HUFF_TRY(bits(t, nullptr, nullptr));
+    if (total) *total = total_bits;
+    const uint64_t need = (total_bits + 31) / 32 * 4;
+    if (out_cap < need) return Status::err(HUFF_E_BUFFER_TOO_SMALL, "output buffer too small");
+    if (reinterpret_cast<uintptr_t>(d_out) & 3) return Status::err(HUFF_E_INVALID_ARG, "output must be 4-byte aligned");
+    huff::dev::WideArgs a{};
+    a.in = d_in;
+    a.n = n;
+    a.width = width;
+    a.log2_slots = et->log2_slots;
+    a.keys = static_cast<const uint8_t*>(keys.p);
+    a.vals = static_cast<const uint64_t*>(vals.p);
+    a.table_in_lds = huff::dev::wide_table_lds_bytes(width, et->log2_slots) <= kTableLdsMax;
+    a.nchunks = nchunks;
+    a.chunk_start = static_cast<const uint64_t*>(chunk_start.p);
+    a.sub_bit = static_cast<uint32_t*>(sub_bit.p);
+    a.out = reinterpret_cast<uint32_t*>(d_out);
+    hipStream_t s = ctx->stream;
+    return ctx->timed("wpack", [&] { return huff::dev::launch_wide_pack(a, s); });
+}
+
+Status huff_wenc::upload_dec(const huff_wtree* t) {
+    HUFF_TRY(t->dec_tables(&dt));
+    if (t->t.width() != width) return Status::err(HUFF_E_INVALID_ARG, "the tree's letter width differs from the job's");
+    if (dec_tree == t->id) return Status::ok();
+    HUFF_TRY(lut.ensure(dt->lut.size() * 4));
+    HUFF_TRY(letters.ensure(dt->letters.size() + 16));
+    HIP_TRY(hipMemcpyAsync(lut.p, dt->lut.data(), dt->lut.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(letters.p, dt->letters.data(), dt->letters.size(), hipMemcpyHostToDevice, ctx->stream));
+    dec_tree = t->id;
+    return Status::ok();
+}
+
+Status huff_wenc::decode(const huff_wtree* t, const uint8_t* d_comp, uint64_t comp_bytes, uint8_t* d_out,
+                         const uint64_t* sub_abs) {
+    HUFF_TRY(ctx->activate());
+    if (reinterpret_cast<uintptr_t>(d_comp) & 3) return Status::err(HUFF_E_INVALID_ARG, "stream must be 4-byte aligned");
+    HUFF_TRY(upload_dec(t));
+    huff::dev::WideDecArgs a{};
+    a.comp = d_comp;
+    a.comp_bytes = comp_bytes;
+    a.lut = static_cast<const uint32_t*>(lut.p);
+    a.lut_bits = dt->bits;
+    a.letters = static_cast<const uint8_t*>(letters.p);
+    a.width = width;
+    a.chunk_start = static_cast<const uint64_t*>(chunk_start.p);
+    a.sub_bit = static_cast<const uint32_t*>(sub_bit.p);
+    a.sub_abs = sub_abs;
+    a.nchunks = nchunks;
+    a.n = n;
+    a.out = d_out;
+    hipStream_t s = ctx->stream;
+    return ctx->timed("wdecode", [&] { return huff::dev::launch_wide_decode(a, s); });
+}
+
+Status huff_wenc::download_index(huff_index_host& idx) {
+    idx.n = n;
+    idx.chunk_start.resize(nchunks + 1);
+    idx.sub_bit.resize((n + huff::dev::kSub - 1) / huff::dev::kSub);
+    HIP_TRY(hipMemcpyAsync(idx.chunk_start.data(), chunk_start.p, idx.chunk_start.size() * 8, hipMemcpyDeviceToHost,
+                           ctx->stream));
+    if (!idx.sub_bit.empty())
+        HIP_TRY(hipMemcpyAsync(idx.sub_bit.data(), sub_bit.p, idx.sub_bit.size() * 4, hipMemcpyDeviceToHost,
+                               ctx->stream));
+    return ctx->sync();
+}
+
+Status huff_wenc::upload_index(const huff_index_host& idx) {
+    if (idx.n != n || idx.chunk_start.size() != nchunks + 1u)
+        return Status::err(HUFF_E_INVALID_ARG, "restart index does not match the job");
+    HIP_TRY(hipMemcpyAsync(chunk_start.p, idx.chunk_start.data(), idx.chunk_start.size() * 8, hipMemcpyHostToDevice,
+                           ctx->stream));
+    if (!idx.sub_bit.empty())
+        HIP_TRY(hipMemcpyAsync(sub_bit.p, idx.sub_bit.data(), idx.sub_bit.size() * 4, hipMemcpyHostToDevice,
+                               ctx->stream));
+    return Status::ok();
+}
+
+// ---------------------------------------------------------------------------
+namespace huff {
+
+Status wweights_map_host(huff_ctx* ctx, uint32_t width, const uint8_t* letters, size_t n,
+                         std::vector<uint8_t>& uniq, std::vector<uint64_t>& counts) {
+    uniq.clear();
+    counts.clear();
+    if (!valid_width(width)) return Status::err(HUFF_E_INVALID_ARG, "letter width must be 1, 2, 4, 8 or 16 bytes");
+    if (n == 0) return Status::ok();
+    HUFF_TRY(ctx->activate());
+    hipStream_t s = ctx->stream;
+    const size_t nb = n * width;
+    HUFF_TRY(ctx->d_in.ensure(nb + 16));
+    HIP_TRY(hipMemcpyAsync(ctx->d_in.p, letters, nb, hipMemcpyHostToDevice, s));
+    DevBuf sorted, du, dc, dn, tmp;
+    size_t tmp_bytes = 0;
+    HIP_TRY(dev::wide_weights(width, ctx->d_in.p, n, nullptr, nullptr, nullptr, nullptr, nullptr, &tmp_bytes, s));
+    HUFF_TRY(sorted.ensure(nb + 16));
+    HUFF_TRY(du.ensure(nb + 16));
+    HUFF_TRY(dc.ensure(n * 8 + 8));
+    HUFF_TRY(dn.ensure(8));
+    HUFF_TRY(tmp.ensure(tmp_bytes + 16));
+    HUFF_TRY(ctx->timed("wweights", [&] {
+        return dev::wide_weights(width, ctx->d_in.p, n, sorted.p, du.p, static_cast<uint64_t*>(dc.p),
+                                 static_cast<uint64_t*>(dn.p), tmp.p, &tmp_bytes, s);
+    }));
+    uint64_t runs = 0;
+    HIP_TRY(hipMemcpyAsync(&runs, dn.p, 8, hipMemcpyDeviceToHost, s));
+    HUFF_TRY(ctx->sync());
+    uniq.resize(runs * width);
+    counts.resize(runs);
+    HIP_TRY(hipMemcpyAsync(uniq.data(), du.p, uniq.size(), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(counts.data(), dc.p, runs * 8, hipMemcpyDeviceToHost, s));
+    return ctx->sync();
+}
+
+Status wcompress_host(huff_ctx* ctx, uint32_t width, const uint8_t* letters, size_t n, const huff_wtree* t,
+                      huff_wcompress_data** out, u128* missing) {
+    *out = nullptr;
+    std::unique_ptr<huff_wtree> own;
+    if (!t) {  // compress (comp.rs:353-359): the tree of build_weights_map
+        std::vector<uint8_t> uniq;
+        std::vector<uint64_t> counts;
+        HUFF_TRY(wweights_map_host(ctx, width, letters, n, uniq, counts));
+        own = std::make_unique<huff_wtree>();
+        HUFF_TRY(WideTree::from_weights(width, uniq.data(), counts.data(), counts.size(), own->t));
+        t = own.get();
+    }
+    if (t->t.width() != width) return Status::err(HUFF_E_INVALID_ARG, "the tree's letter width differs from the letters'");
+    // comp.rs:443-449: no letters -> no bytes -> CompressData::new panics
+    if (n == 0) return Status::err(HUFF_E_EMPTY_COMP, "provided comp_bytes are empty");
+    HUFF_TRY(ctx->activate());
+    hipStream_t s = ctx->stream;
+    HUFF_TRY(ctx->d_in.ensure(n * width + 16));
+    HIP_TRY(hipMemcpyAsync(ctx->d_in.p, letters, n * width, hipMemcpyHostToDevice, s));
+    huff_wenc e;
+    HUFF_TRY(e.init(ctx, width, static_cast<const uint8_t*>(ctx->d_in.p), n));
+    uint64_t tb = 0;
+    HUFF_TRY(e.bits(t, &tb, missing));
+    const size_t words = static_cast<size_t>((tb + 31) / 32);
+    HUFF_TRY(ctx->d_out.ensure(words * 4 + 16));
+    HUFF_TRY(e.pack(t, static_cast<uint8_t*>(ctx->d_out.p), words * 4, &tb));
+    auto cd = std::make_unique<huff_wcompress_data>();
+    cd->comp.resize(static_cast<size_t>((tb + 7) / 8));
+    HIP_TRY(hipMemcpyAsync(cd->comp.data(), ctx->d_out.p, cd->comp.size(), hipMemcpyDeviceToHost, s));
+    cd->padding = calc_padding_bits(tb);  // comp.rs:446
+    cd->index = std::make_unique<huff_index_host>();
+    HUFF_TRY(e.download_index(*cd->index));
+    if (own) {
+        cd->tree = own.release();
+    } else {
+        cd->tree = new huff_wtree();
+        cd->tree->t = t->t;
+    }
+    *out = cd.release();
+    return Status::ok();
+}
+
+Status wdecode_indexless_dev(huff_ctx* ctx, const huff_wtree* t, const uint8_t* d_comp, uint64_t comp_bytes,
+                             uint64_t valid_bits, uint8_t* d_out, size_t cap_letters, uint64_t* n_out) {
+    *n_out = 0;
+    if (valid_bits == 0) return Status::ok();
+    if (reinterpret_cast<uintptr_t>(d_comp) & 15)
+        return Status::err(HUFF_E_INVALID_ARG, "compressed stream must be 16-byte aligned");
+    HUFF_TRY(ctx->activate());
+    // synchronise on the tree's shape (the sync kernels only use code lengths)
+    const huff_tree* shape = t->shape_tree();
+    const DecTables* dt = nullptr;
+    HUFF_TRY(ctx->upload_dec_tables(shape, &dt));
+    IndexlessSync st;
+    st.dt = dt;
+    HUFF_TRY(indexless_sync(ctx, d_comp, comp_bytes, valid_bits, shape, st));
+    *n_out = st.total;
+    if (!d_out) return Status::err(HUFF_E_BUFFER_TOO_SMALL, "output buffer too small");
+    if (st.total > cap_letters) return Status::err(HUFF_E_BUFFER_TOO_SMALL, "output buffer too small");
+    if (!dev::indexless_staged(st.a))
+        return Status::err(HUFF_E_CODE_TOO_LONG, "index-free decode of letters wider than a byte needs codes <= 32 bits");
+    DevBuf sub_abs;
+    HUFF_TRY(indexless_mark(ctx, st, sub_abs));
+    HIP_TRY(hipEventRecord(ctx->lut_free, ctx->stream));
+    huff_wenc e;
+    HUFF_TRY(e.init(ctx, t->t.width(), nullptr, st.total));
+    HUFF_TRY(e.decode(t, d_comp, comp_bytes, d_out, static_cast<const uint64_t*>(sub_abs.p)));
+    return ctx->sync();  // sub_abs is freed on return
+}
+
+Status wdecompress_host(huff_ctx* ctx, const huff_wcompress_data* cd, uint8_t* out, size_t cap_letters,
+                        size_t* n_out) {
+    const uint32_t W = cd->tree->t.width();
+    HUFF_TRY(ctx->activate());
+    hipStream_t s = ctx->stream;
+    HUFF_TRY(ctx->d_in.ensure(cd->comp.size() + 16));
+    HIP_TRY(hipMemcpyAsync(ctx->d_in.p, cd->comp.data(), cd->comp.size(), hipMemcpyHostToDevice, s));
+    if (!cd->index) {
+        // comp.rs:513-516: all bytes but the last give 8 bits, the last 8 - padding
+        const uint64_t valid = static_cast<uint64_t>(cd->comp.size()) * 8 - cd->padding;
+        uint64_t cnt = 0;
+        Status q = wdecode_indexless_dev(ctx, cd->tree, static_cast<const uint8_t*>(ctx->d_in.p), cd->comp.size(),
+                                         valid, nullptr, 0, &cnt);
+        if (q.code != HUFF_E_BUFFER_TOO_SMALL && q.code != HUFF_OK) return q;
+        *n_out = cnt;
+        if (cap_letters < cnt) return Status::err(HUFF_E_BUFFER_TOO_SMALL, "output buffer too small");
+        if (cnt == 0) return Status::ok();
+        HUFF_TRY(ctx->d_out.ensure(cnt * W + 16));
+        HUFF_TRY(wdecode_indexless_dev(ctx, cd->tree, static_cast<const uint8_t*>(ctx->d_in.p), cd->comp.size(),
+                                       valid, static_cast<uint8_t*>(ctx->d_out.p), cnt, &cnt));
+        HIP_TRY(hipMemcpyAsync(out, ctx->d_out.p, cnt * W, hipMemcpyDeviceToHost, s));
+        return ctx->sync();
+    }
+    const uint64_t n = cd->index->n;
+    *n_out = n;
+    if (cap_letters < n) return Status::err(HUFF_E_BUFFER_TOO_SMALL, "output buffer too small");
+    if (n == 0) return Status::ok();
+    HUFF_TRY(ctx->d_out.ensure(n * W + 16));
+    huff_wenc e;
+    HUFF_TRY(e.init(ctx, W, nullptr, n));
+    HUFF_TRY(e.upload_index(*cd->index));
+    HUFF_TRY(e.decode(cd->tree, static_cast<const uint8_t*>(ctx->d_in.p), cd->comp.size(),
+                      static_cast<uint8_t*>(ctx->d_out.p)));
+    HIP_TRY(hipMemcpyAsync(out, ctx->d_out.p, n * W, hipMemcpyDeviceToHost, s));
+    return ctx->sync();
+}
+
+}  // namespace huff

@@ -99,6 +99,34 @@ SIGNATURES = [
     ("huff_file_compress", i, [vp, C.c_char_p, C.c_char_p, sz]),
     ("huff_file_decompress", i, [vp, C.c_char_p, C.c_char_p, sz]),
     ("huff_parse_block_size", i, [C.c_char_p, szp]),
+    # include/huffgpu_wide.h
+    ("huff_wtree_from_weights", i, [C.c_uint32, vp, vp, sz, C.POINTER(vp)]),
+    ("huff_wtree_clone", i, [vp, C.POINTER(vp)]),
+    ("huff_wtree_free", None, [vp]),
+    ("huff_wtree_width", C.c_uint32, [vp]),
+    ("huff_wtree_num_leaves", sz, [vp]),
+    ("huff_wtree_read_codes", i, [vp, vp, vp, vp, sz, szp]),
+    ("huff_wtree_as_bin", i, [vp, vp, sz, szp]),
+    ("huff_wtree_try_from_bin", i, [C.c_uint32, vp, sz, C.POINTER(vp)]),
+    ("huff_wweights_map", i, [vp, C.c_uint32, vp, sz, vp, vp, sz, szp]),
+    ("huff_wcd_new", i, [vp, sz, C.c_uint8, vp, C.POINTER(vp)]),
+    ("huff_wcd_free", None, [vp]),
+    ("huff_wcd_comp_bytes", i, [vp, C.POINTER(u8p), szp]),
+    ("huff_wcd_padding", C.c_uint8, [vp]),
+    ("huff_wcd_tree", vp, [vp]),
+    ("huff_wcd_has_index", i, [vp]),
+    ("huff_wcd_to_bytes", i, [vp, vp, sz, szp]),
+    ("huff_wcd_try_from_bytes", i, [C.c_uint32, vp, sz, C.POINTER(vp)]),
+    ("huff_wcompress_with_tree", i, [vp, vp, sz, vp, C.POINTER(vp)]),
+    ("huff_wcompress", i, [vp, C.c_uint32, vp, sz, C.POINTER(vp)]),
+    ("huff_wdecompress", i, [vp, vp, vp, sz, szp]),
+    ("huff_last_missing_wletter", i, [vp, C.POINTER(C.c_uint32)]),
+    ("huff_wenc_create", i, [vp, C.c_uint32, vp, sz, C.POINTER(vp)]),
+    ("huff_wenc_free", None, [vp]),
+    ("huff_wenc_bits", i, [vp, vp, vp]),
+    ("huff_wenc_pack", i, [vp, vp, vp, sz, vp]),
+    ("huff_wenc_decode", i, [vp, vp, vp, vp]),
+    ("huff_dev_wdecompress", i, [vp, vp, vp, sz, C.c_uint8, vp, sz, szp]),
 ]
 
 _lib = None

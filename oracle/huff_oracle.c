@@ -487,6 +487,153 @@ size_t orc_decompress(const uint8_t* comp, size_t len, uint8_t padding,
     return s.count;
 }
 
+/* ---- the same two functions for letters wider than a byte (u64 values;
+ * letter.rs:41-60 integer types up to 64 bits) ---- */
+typedef struct { uint64_t letter; uint32_t len; size_t order; uint8_t* bits; } wcode;
+
+typedef struct { wcode* v; size_t n, cap; uint8_t* path; size_t path_cap; } wcodes_ctx;
+
+static void wcodes_rec(const orc_tree* t, int32_t nd, uint32_t depth, wcodes_ctx* c)
+{
+    const orc_node* n = &t->nodes[nd];
+    if (depth + 1 > c->path_cap) {
+        c->path_cap = 2 * (depth + 1);
+        c->path = (uint8_t*)realloc(c->path, c->path_cap);
+    }
+    if (n->leaf) {
+        if (c->n == c->cap) {
+            c->cap = c->cap ? 2 * c->cap : 64;
+            c->v = (wcode*)realloc(c->v, c->cap * sizeof(wcode));
+        }
+        wcode* w = &c->v[c->n];
+        w->letter = n->letter;
+        w->len = depth;
+        w->order = c->n;
+        w->bits = (uint8_t*)malloc(depth ? depth : 1);
+        memcpy(w->bits, c->path, depth);
+        c->n++;
+        return;
+    }
+    c->path[depth] = 0;
+    wcodes_rec(t, n->left, depth + 1, c);
+    c->path[depth] = 1;
+    wcodes_rec(t, n->right, depth + 1, c);
+}
+
+static int wcode_cmp(const void* a, const void* b)
+{
+    const wcode* x = (const wcode*)a;
+    const wcode* y = (const wcode*)b;
+    if (x->letter != y->letter) return x->letter < y->letter ? -1 : 1;
+    return x->order < y->order ? -1 : (x->order > y->order);
+}
+
+/* read_codes (tree_inner.rs:356-419): preorder inserts into a map, a later
+ * leaf of the same letter overwriting; here: sorted by (letter, order) and the
+ * last of each letter kept */
+static size_t wcodes(const orc_tree* t, wcode** out)
+{
+    wcodes_ctx c;
+    memset(&c, 0, sizeof(c));
+    const orc_node* r = &t->nodes[t->root];
+    if (r->leaf) {  /* tree_inner.rs:313-315: the root leaf's code is "0" */
+        c.v = (wcode*)malloc(sizeof(wcode));
+        c.v[0].letter = r->letter; c.v[0].len = 1; c.v[0].order = 0;
+        c.v[0].bits = (uint8_t*)calloc(1, 1);
+        *out = c.v;
+        return 1;
+    }
+    wcodes_rec(t, t->root, 0, &c);
+    free(c.path);
+    qsort(c.v, c.n, sizeof(wcode), wcode_cmp);
+    size_t k = 0;
+    for (size_t i = 0; i < c.n; ++i) {
+        if (i + 1 < c.n && c.v[i + 1].letter == c.v[i].letter) { free(c.v[i].bits); continue; }
+        c.v[k++] = c.v[i];
+    }
+    *out = c.v;
+    return k;
+}
+
+static const wcode* wfind(const wcode* v, size_t n, uint64_t letter)
+{
+    size_t lo = 0, hi = n;
+    while (lo < hi) {
+        size_t mid = (lo + hi) / 2;
+        if (v[mid].letter < letter) lo = mid + 1; else hi = mid;
+    }
+    return (lo < n && v[lo].letter == letter) ? &v[lo] : NULL;
+}
+
+/* comp.rs:419-451 over u64 letters; ORC_E_MISSING_LETTER with the index of
+ * the first letter (input order) that has no code */
+int orc_wcompress_with_tree(const uint64_t* in, size_t n, const orc_tree* t,
+                            uint8_t* out, size_t cap, size_t* out_len,
+                            uint8_t* padding, size_t* missing_idx)
+{
+    wcode* v;
+    size_t nv = wcodes(t, &v);
+    size_t o = 0;
+    uint8_t comp_byte = 0;
+    int bit_ptr = 7, rc = ORC_OK;
+    for (size_t i = 0; i < n; ++i) {
+        const wcode* c = wfind(v, nv, in[i]);
+        if (!c) {                                                  /* :426-432 */
+            if (missing_idx) *missing_idx = i;
+            rc = ORC_E_MISSING_LETTER;
+            goto done;
+        }
+        for (uint32_t b = 0; b < c->len; ++b) {
+            comp_byte |= (uint8_t)(c->bits[b] << bit_ptr);
+            if (bit_ptr == 0) {
+                if (o < cap) out[o] = comp_byte;
+                o++;
+                comp_byte = 0;
+                bit_ptr = 7;
+            } else {
+                bit_ptr -= 1;
+            }
+        }
+    }
+    {
+        uint8_t pad = (bit_ptr == 7) ? 0 : (uint8_t)(bit_ptr + 1);
+        if (pad != 0) {
+            if (o < cap) out[o] = comp_byte;
+            o++;
+        }
+        *out_len = o;
+        if (padding) *padding = pad;
+        if (o == 0) rc = ORC_E_EMPTY_COMP;
+        else if (o > cap) rc = ORC_E_BUFFER;
+    }
+done:
+    for (size_t i = 0; i < nv; ++i) free(v[i].bits);
+    free(v);
+    return rc;
+}
+
+/* comp.rs:487-519 over u64 letters */
+size_t orc_wdecompress(const uint8_t* comp, size_t len, uint8_t padding,
+                       const orc_tree* t, uint64_t* out, size_t cap)
+{
+    if (len == 0) return 0;
+    const orc_node* nodes = t->nodes;
+    int32_t cur = t->root;
+    size_t count = 0;
+    for (size_t i = 0; i < len; ++i) {
+        int nbits = (i + 1 < len) ? 8 : 8 - padding;
+        for (int bp = 0; bp < nbits; ++bp) {
+            if (!nodes[cur].leaf) cur = ((comp[i] >> (7 - bp)) & 1) ? nodes[cur].right : nodes[cur].left;
+            if (nodes[cur].leaf) {
+                if (count < cap) out[count] = nodes[cur].letter;
+                count++;
+                cur = t->root;
+            }
+        }
+    }
+    return count;
+}
+
 /* bitvec into_vec (Msb0): bit i -> byte i/8, mask 0x80 >> (i%8), zero tail */
 static void pack_bits(const uint8_t* bits, size_t nbits, uint8_t* out)
 {

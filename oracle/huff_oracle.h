@@ -98,6 +98,14 @@ int orc_cli_compress(const uint8_t* file, size_t n, size_t block_size,
                      uint8_t* out, size_t cap, size_t* out_len);
 int orc_cli_decompress(const uint8_t* hff, size_t n, size_t block_size,
                        uint8_t* out, size_t cap, size_t* out_len);
+/* compress_with_tree / decompress over u64 letters (the wider integer
+ * HuffLetterAsBytes types, letter.rs:41-60; trees from orc_tree_from_leaves
+ * or orc_tree_try_from_bin with letter_bits = 8 * width) */
+int orc_wcompress_with_tree(const uint64_t* in, size_t n, const orc_tree* t,
+                            uint8_t* out, size_t cap, size_t* out_len,
+                            uint8_t* padding, size_t* missing_idx);
+size_t orc_wdecompress(const uint8_t* comp, size_t len, uint8_t padding,
+                       const orc_tree* t, uint64_t* out, size_t cap);
 /* huff/src/utils.rs:2-25 */
 size_t orc_offset_bytes(const uint8_t* bytes, size_t n, size_t shift, uint8_t* out);
 

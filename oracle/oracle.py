@@ -88,6 +88,9 @@ def lib():
         L.orc_offset_bytes.restype = sz
         L.orc_fast_encode.argtypes = [u8p, sz, u64p, u8p, C.c_int, C.c_uint64, u8p, sz, C.POINTER(C.c_uint64)]
         L.orc_fast_hist.argtypes = [u8p, sz, C.c_int, u64p]
+        L.orc_wcompress_with_tree.argtypes = [u64p, sz, C.c_void_p, u8p, sz, C.POINTER(sz), u8p, C.POINTER(sz)]
+        L.orc_wdecompress.argtypes = [u8p, sz, C.c_uint8, C.c_void_p, u64p, sz]
+        L.orc_wdecompress.restype = sz
         L.orc_fast_encode_idx.argtypes = [u8p, sz, u64p, u8p, C.c_int, C.c_uint64, u8p, sz,
                                           C.POINTER(C.c_uint64), u64p]
         L.orc_fast_decode.argtypes = [u8p, sz, C.c_void_p, sz, C.c_int, u64p, u8p]
@@ -267,6 +270,34 @@ def decompress(comp: bytes, padding: int, tree: Tree) -> bytes:
     out = np.zeros(max(n, 1), np.uint8)
     lib().orc_decompress(p, a.size, padding, tree.h, out.ctypes.data_as(C.POINTER(C.c_uint8)), n)
     return out[:n].tobytes()
+
+
+def wcompress_with_tree(letters, tree: Tree):
+    """comp.rs:419-451 over integer letters (<= 64 bits, as u64 bit patterns)
+    -> (comp_bytes, padding); OracleError(E_MISSING_LETTER) carries .index"""
+    a = np.ascontiguousarray(np.asarray(letters).astype(np.uint64))
+    cap = 8 * a.size * 8 + 16  # codes of any length the tests build
+    out = np.zeros(cap, np.uint8)
+    olen = C.c_size_t()
+    pad = C.c_uint8()
+    miss = C.c_size_t()
+    e = lib().orc_wcompress_with_tree(a.ctypes.data_as(C.POINTER(C.c_uint64)), a.size, tree.h,
+                                      out.ctypes.data_as(C.POINTER(C.c_uint8)), cap, C.byref(olen), C.byref(pad),
+                                      C.byref(miss))
+    if e:
+        err = OracleError(e, "letter not found in codes" if e == E_MISSING_LETTER else "")
+        err.index = miss.value
+        raise err
+    return out[:olen.value].tobytes(), pad.value
+
+
+def wdecompress(comp: bytes, padding: int, tree: Tree) -> np.ndarray:
+    """comp.rs:487-519 over integer letters -> u64 array"""
+    a, p = _u8(_as_bytes(comp))
+    n = lib().orc_wdecompress(p, a.size, padding, tree.h, None, 0)
+    out = np.zeros(max(n, 1), np.uint64)
+    lib().orc_wdecompress(p, a.size, padding, tree.h, out.ctypes.data_as(C.POINTER(C.c_uint64)), n)
+    return out[:n]
 
 
 def to_bytes(comp: bytes, padding: int, tree: Tree) -> bytes:

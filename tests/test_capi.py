@@ -7,12 +7,13 @@ import re
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADER = os.path.join(ROOT, "include", "huffgpu.h")
+HEADERS = [os.path.join(ROOT, "include", h) for h in sorted(os.listdir(os.path.join(ROOT, "include")))
+           if h.endswith(".h")]
 LIB = os.path.join(ROOT, "huff-encoding_amd", "lib", "libhuffgpu.so")
 
 
 def declared():
-    src = open(HEADER).read()
+    src = "".join(open(h).read() for h in HEADERS)
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     return sorted(set(re.findall(r"\b(huff_[a-z0-9_]+)\s*\(", src)))
 
@@ -22,7 +23,8 @@ def test_header_declares_entry_points():
     assert len(names) >= 45
     for must in ("huff_weights_from_bytes", "huff_tree_from_weights", "huff_compress_with_tree",
                  "huff_decompress", "huff_cd_to_bytes", "huff_cd_try_from_bytes", "huff_enc_pack",
-                 "huff_file_compress", "huff_file_decompress"):
+                 "huff_file_compress", "huff_file_decompress", "huff_wtree_from_weights",
+                 "huff_wcompress_with_tree", "huff_wdecompress", "huff_wweights_map"):
         assert must in names
 
 

@@ -1,0 +1,188 @@
+"""GPU parity of the wider-letter path: compress_with_tree /
+decompress for u8 ... u128 letters through the C ABI, bit-exact against the
+oracle's restatement (orc_wcompress_with_tree / orc_wdecompress, which follow
+comp.rs:419-451 and 487-519 over u64 letters).
+
+128-bit letters are checked through rank relabelling: the tree built from
+(rank_i, w_i) in the same order has the same shape and leaf positions, so
+the compressed stream must be identical.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+LENGTHS = [1, 2, 7, 255, 256, 257, 4095, 65535, 65536, 65537, 65536 * 3 + 1001, 400_003]
+
+
+@pytest.fixture(scope="module")
+def W():
+    import huff_coding.wide as W
+
+    return W
+
+
+def zipf_letters(rng, n, dtype, k=3000):
+    info = np.iinfo(dtype)
+    alphabet = np.unique(rng.integers(info.min, info.max, k, dtype=dtype, endpoint=True))
+    p = 1.0 / np.arange(1, alphabet.size + 1) ** 1.1
+    p /= p.sum()
+    return alphabet[rng.choice(alphabet.size, n, p=p)]
+
+
+def oracle_stream(O, letters, weights_items, lbits):
+    mask = (1 << lbits) - 1
+    ot = O.Tree.from_leaves([int(k) & mask for k, _ in weights_items], [int(v) for _, v in weights_items])
+    u = np.asarray(letters).astype(np.int64).view(np.uint64) & np.uint64(mask) if lbits < 64 else \
+        np.asarray(letters).view(np.uint64)
+    return O.wcompress_with_tree(u, ot), ot
+
+
+@pytest.mark.parametrize("dtype", [np.uint8, np.int16, np.uint16, np.int32, np.uint64])
+def test_compress_with_tree_matches_oracle(W, O, ctx, dtype):
+    rng = np.random.default_rng(np.dtype(dtype).itemsize * 7 + 1)
+    lbits = 8 * np.dtype(dtype).itemsize
+    for n in LENGTHS:
+        letters = zipf_letters(rng, n, dtype, k=50 if dtype == np.uint8 else 3000)
+        wmap = W.build_weights_map(letters, ctx)
+        u, c = np.unique(letters, return_counts=True)
+        assert sorted(wmap.items()) == sorted(zip(u.tolist(), c.tolist()))
+        items = list(wmap.items())
+        rng.shuffle(items)  # any HashMap iteration order
+        t = W.WideTree.from_weights(items, dtype)
+        cd = W.compress_with_tree(letters, t, ctx)
+        (ocomp, opad), _ = oracle_stream(O, letters, items, lbits)
+        assert cd.comp_bytes() == ocomp, (dtype, n)
+        assert cd.padding_bits() == opad
+        assert cd.has_index()
+        back = W.decompress(cd, ctx)
+        assert back.dtype == np.dtype(dtype) and np.array_equal(back, letters), (dtype, n)
+
+
+@pytest.mark.parametrize("dtype", [np.int16, np.uint32, np.int64])
+def test_index_free_decode(W, O, ctx, dtype):
+    """a container from to_bytes has no restart index: the self-synchronising
+    decoder (run on the tree's shape) + the wide decoder from its restart points"""
+    rng = np.random.default_rng(11)
+    for n in (1, 300, 65536 + 77, 250_001):
+        letters = zipf_letters(rng, n, dtype)
+        cd = W.compress(letters, ctx)
+        raw = cd.to_bytes()
+        back_cd = W.WideCompressData.try_from_bytes(raw, dtype)
+        assert not back_cd.has_index()
+        got = W.decompress(back_cd, ctx)
+        # the oracle's bit walk over the same bytes (comp.rs:487-519)
+        ot_items = list(W.build_weights_map(letters, ctx).items())
+        (ocomp, opad), ot = oracle_stream(O, letters, ot_items, 8 * np.dtype(dtype).itemsize)
+        assert back_cd.comp_bytes() == ocomp
+        assert np.array_equal(got, letters), (dtype, n)
+
+
+def test_u128_letters(W, O, ctx):
+    rng = np.random.default_rng(5)
+    base = [(1 << 127) | (int(x) << 40) | 17 for x in rng.integers(0, 1 << 60, 500)] + [0, 1, (1 << 128) - 1]
+    vals = list(dict.fromkeys(base))
+    for n in (1, 1000, 70_001):
+        idx = np.minimum(rng.geometric(0.02, n) - 1, len(vals) - 1)
+        letters = W.letters_u128([vals[i] for i in idx])
+        wmap = W.build_weights_map(letters, ctx)
+        u, c = np.unique(idx, return_counts=True)
+        assert wmap == {vals[i]: int(k) for i, k in zip(u, c)}
+        items = list(wmap.items())
+        rng.shuffle(items)
+        t = W.WideTree.from_weights(items, W.U128)
+        cd = W.compress_with_tree(letters, t, ctx)
+        rank = {v: r for r, v in enumerate(vals)}
+        ot = O.Tree.from_leaves([rank[k] for k, _ in items], [w for _, w in items])
+        ocomp, opad = O.wcompress_with_tree(np.asarray([rank[vals[i]] for i in idx], np.uint64), ot)
+        assert cd.comp_bytes() == ocomp and cd.padding_bits() == opad
+        back = W.decompress(cd, ctx)
+        assert back.tobytes() == letters.tobytes()
+        # index-free
+        back2 = W.decompress(W.WideCompressData.try_from_bytes(cd.to_bytes(), W.U128), ctx)
+        assert back2.tobytes() == letters.tobytes()
+
+
+def test_missing_letter_first_in_input_order(W, ctx):
+    """comp.rs:426-432: CompressError for the first letter without a code"""
+    import huff_coding as H
+
+    t = W.WideTree.from_weights({10: 3, 20: 2, 30: 1}, np.int32)
+    letters = np.array([10, 20] * 40000 + [-5, 30, 99], np.int32)
+    with pytest.raises(H.CompressError) as e:
+        W.compress_with_tree(letters, t, ctx)
+    assert e.value.missing_letter == (-5) & 0xFFFFFFFF or e.value.missing_letter == -5
+    assert "letter not found in codes" in str(e.value)
+
+
+def test_single_letter_and_empty(W, ctx):
+    import huff_coding as H
+
+    letters = np.full(100_000, -12, np.int32)
+    cd = W.compress(letters, ctx)
+    assert cd.huff_tree().read_codes() == {-12: "0"}
+    assert cd.comp_bytes() == bytes(12500) and cd.padding_bits() == 0
+    assert np.array_equal(W.decompress(cd, ctx), letters)
+    back = W.decompress(W.WideCompressData.try_from_bytes(cd.to_bytes(), np.int32), ctx)
+    assert np.array_equal(back, letters)
+    with pytest.raises(H.HuffPanic):  # from_weights of no letters panics first
+        W.compress(np.zeros(0, np.int32), ctx)
+    t = W.WideTree.from_weights({1: 1}, np.int32)
+    with pytest.raises(H.HuffPanic):  # no bytes: CompressData::new panics
+        W.compress_with_tree(np.zeros(0, np.int32), t, ctx)
+
+
+def test_long_codes(W, O, ctx):
+    """Fibonacci weights give codes up to 39 bits: the > 32-bit split in the
+    packer and the secondary tables in the decoder; the index-free decoder
+    refuses them (> 32 bits) with CODE_TOO_LONG"""
+    import huff_coding as H
+
+    fib = [1, 1]
+    while len(fib) < 40:
+        fib.append(fib[-1] + fib[-2])
+    items = [(1000 + i, f) for i, f in enumerate(fib)]
+    t = W.WideTree.from_weights(items, np.uint16)
+    assert max(len(c) for c in t.read_codes().values()) == 39
+    rng = np.random.default_rng(9)
+    letters = (1000 + rng.integers(0, 40, 300_000)).astype(np.uint16)
+    cd = W.compress_with_tree(letters, t, ctx)
+    (ocomp, opad), _ = oracle_stream(O, letters, items, 16)
+    assert cd.comp_bytes() == ocomp and cd.padding_bits() == opad
+    assert np.array_equal(W.decompress(cd, ctx), letters)
+    with pytest.raises(H.HuffError) as e:
+        W.decompress(W.WideCompressData.try_from_bytes(cd.to_bytes(), np.uint16), ctx)
+    assert e.value.code == 7
+
+
+def test_device_job_large(W, ctx):
+    """HBM-resident job: 64 Mi u16 letters, bits = sum of code lengths, pack,
+    restart-index decode and index-free decode round trips"""
+    import torch
+
+    n = 64 << 20
+    g = torch.Generator(device="cuda").manual_seed(3)
+    # a skewed u16 alphabet: low byte uniform, high byte geometric-ish
+    hi = torch.clamp(torch.empty(n, device="cuda").exponential_(0.7, generator=g).long(), max=255)
+    lo = torch.randint(0, 256, (n,), device="cuda", generator=g)
+    x = ((hi << 8) | lo).to(torch.int32).to(torch.int16)
+    xs = x.cpu().numpy().view(np.uint16)
+    u, c = np.unique(xs, return_counts=True)
+    t = W.WideTree.from_weights(list(zip(u.tolist(), c.tolist())), np.uint16)
+    letters, code, ln = t.code_table()
+    lens = np.zeros(65536, np.uint64)
+    lens[letters.astype(np.int64)] = ln
+    want_bits = int((c.astype(np.uint64) * lens[u.astype(np.int64)]).sum())
+    job = W.WideEncodeJob(ctx, 2, x.data_ptr(), n)
+    assert job.bits(t) == want_bits
+    out = torch.empty((want_bits + 31) // 32 * 4 + 16, dtype=torch.uint8, device="cuda")
+    assert job.pack(t, out.data_ptr(), out.numel()) == want_bits
+    dec = torch.empty(n, dtype=torch.int16, device="cuda")
+    job.decode(t, out.data_ptr(), dec.data_ptr())
+    torch.cuda.synchronize()
+    assert torch.equal(dec, x)
+    dec.zero_()
+    nb = (want_bits + 7) // 8
+    cnt = W.decompress_dev(ctx, t, out.data_ptr(), nb, (8 - want_bits % 8) % 8, dec.data_ptr(), n)
+    torch.cuda.synchronize()
+    assert cnt == n and torch.equal(dec, x)
