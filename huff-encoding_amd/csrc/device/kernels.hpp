@@ -109,11 +109,13 @@ struct WideArgs {
     const uint8_t* in;            // n letters of `width` bytes, native layout, 16-B aligned
     uint64_t n;
     uint32_t width;               // 1, 2, 4, 8, 16
-    uint32_t log2_slots;          // hash table: 2^log2_slots slots
-    const uint8_t* keys;          // [slots * width]
-    const uint64_t* vals;         // [slots] (code << 8) | len, 0 = empty
+    uint32_t log2_slots;          // cuckoo table: 2^log2_slots slots in buckets of 2
+    const uint8_t* keys;          // [slots * max(4, width)]
+    const void* vals;             // [slots] (code << 8) | len, 0 = empty; u32 if val32 else u64
+    uint32_t val32;               // every code <= 24 bits
     uint32_t table_in_lds;        // stage the table in LDS (wide_table_lds_bytes)
     uint32_t nchunks;             // ceil(n / kChunk)
+    uint32_t cu_count;            // persistent grid size
     uint64_t* chunk_bits;         // [nchunks]            (bits pass)
     const uint64_t* chunk_start;  // [nchunks + 1]        (pack pass)
     uint32_t* sub_bit;            // [ceil(n / kSub)]
@@ -126,15 +128,20 @@ struct WideDecArgs {
     const uint32_t* lut;          // leaf = (len << 24) | leaf, ptr = kLutPtr | offset
     uint32_t lut_bits;
     const uint8_t* letters;       // [leaves * width]
+    uint32_t nleaves;
     uint32_t width;
     const uint64_t* chunk_start;
     const uint32_t* sub_bit;
     const uint64_t* sub_abs;      // non-null: index-free restart points
     uint32_t nchunks;
+    uint32_t cu_count;
+    uint32_t max_len;             // longest code (<= 32: the 64-byte-unit decoder)
     uint64_t n;
     uint8_t* out;                 // n * width bytes
 };
-size_t wide_table_lds_bytes(uint32_t width, uint32_t log2_slots);
+inline size_t wide_table_lds_bytes(uint32_t width, uint32_t log2_slots, bool val32) {
+    return (size_t(1) << log2_slots) * ((val32 ? 4 : 8) + (width < 4 ? 4 : width));
+}
 hipError_t launch_wide_bits(const WideArgs& a, hipStream_t s);
 hipError_t launch_wide_pack(const WideArgs& a, hipStream_t s);
 hipError_t launch_wide_decode(const WideDecArgs& a, hipStream_t s);

@@ -82,9 +82,9 @@ private:
 };
 
 // Device tables of a wide tree.
-//  encode: open-addressing hash table of 2^k >= 2 * distinct slots, key W
-//          bytes (native layout), value (code << 8) | len (len 0 = empty);
-//          codes must fit 56 bits.
+//  encode: two-choice cuckoo table (wide_buckets) of 2^k >= 2 * distinct
+//          slots, keys of wide_key_bytes (native layout), value
+//          (code << 8) | len (len 0 = empty); codes must fit 56 bits.
 //  decode: primary table of 2^bits entries then 8-bit secondaries; leaf =
 //          (len << 24) | leaf index, pointer = kLutPtr | secondary offset;
 //          letters[leaf index] (W bytes each) in `letters`.
@@ -95,9 +95,10 @@ constexpr uint32_t kWideMaxEncodeLen = 56;      // (code << 8) | len in a u64
 
 struct WideEncTables {
     uint32_t width = 1;
-    uint32_t log2_slots = 0;
-    std::vector<uint8_t> keys;   // slots * W
+    uint32_t log2_slots = 0;     // slots = 2 * buckets
+    std::vector<uint8_t> keys;   // slots * wide_key_bytes(width)
     std::vector<uint64_t> vals;  // slots
+    std::vector<uint32_t> vals32;  // the same when every code has <= 24 bits (else empty)
     uint32_t maxlen = 0;
     size_t distinct = 0;
 };
@@ -107,10 +108,21 @@ struct WideDecTables {
     std::vector<uint8_t> letters;  // leaves * W
 };
 
-// same hash on host and device: slot of a key (value v, W bytes)
-inline uint32_t wide_slot(uint64_t lo, uint64_t hi, uint32_t log2_slots) {
+// Two-choice cuckoo table for encode: buckets of 2 slots (slot = 2 b + j);
+// a key lives in one of the slots of bucket b1 or b2, so a lookup is four
+// fixed loads and no loop. Keys of <= 4 bytes are stored as u32. Same hashes
+// on host and device (device/wide.hip buckets_of).
+inline uint32_t wide_key_bytes(uint32_t width) { return width < 4 ? 4 : width; }
+inline void wide_buckets(uint64_t lo, uint64_t hi, uint32_t lgb, uint32_t width, uint32_t* b1, uint32_t* b2) {
+    if (width <= 4) {
+        const uint32_t x = static_cast<uint32_t>(lo);
+        *b1 = static_cast<uint32_t>((static_cast<uint64_t>(x * 0x9E3779B1u)) >> (32 - lgb));
+        *b2 = static_cast<uint32_t>((static_cast<uint64_t>(x * 0x85EBCA77u + 0x165667B1u)) >> (32 - lgb));
+        return;
+    }
     const uint64_t k = lo ^ (hi * 0xC2B2AE3D27D4EB4Full);
-    return static_cast<uint32_t>((k * 0x9E3779B97F4A7C15ull) >> (64 - log2_slots));
+    *b1 = static_cast<uint32_t>((k * 0x9E3779B97F4A7C15ull) >> (64 - lgb));
+    *b2 = static_cast<uint32_t>((k * 0xD6E8FEB86659FD93ull + 0x165667B19E3779F9ull) >> (64 - lgb));
 }
 
 Status build_wide_enc_tables(const WideTree& t, WideEncTables& out);

@@ -199,21 +199,59 @@ Status build_wide_enc_tables(const WideTree& t, WideEncTables& out) {
     if (maxlen > kWideMaxEncodeLen)
         return Status::err(HUFF_E_CODE_TOO_LONG, "code longer than 56 bits: outside the GPU encoder's range");
     const uint32_t W = t.width();
-    uint32_t lg = 6;
-    while ((1ull << lg) < 2 * codes.size()) ++lg;
-    const size_t slots = size_t(1) << lg;
+    const uint32_t KB = wide_key_bytes(W);
     out.width = W;
-    out.log2_slots = lg;
     out.maxlen = maxlen;
     out.distinct = codes.size();
-    out.keys.assign(slots * W, 0);
-    out.vals.assign(slots, 0);
-    for (const WideLeaf& c : codes) {
-        uint32_t h = wide_slot(static_cast<uint64_t>(c.letter), static_cast<uint64_t>(c.letter >> 64), lg);
-        while (out.vals[h]) h = (h + 1) & static_cast<uint32_t>(slots - 1);
-        store_letter(&out.keys[h * W], W, c.letter);
-        out.vals[h] = (c.code << 8) | c.len;
+    // buckets of 2 slots, load <= 1/2; grow until every key is placed
+    uint32_t lgb = 5;
+    while ((2ull << lgb) < 2 * codes.size()) ++lgb;
+    struct Ent {
+        u128 key;
+        uint64_t val;
+        bool used;
+    };
+    std::vector<Ent> slot;
+    uint64_t rng = 0x9E3779B97F4A7C15ull;
+    for (;; ++lgb) {
+        slot.assign(size_t(2) << lgb, Ent{0, 0, false});
+        bool ok = true;
+        for (const WideLeaf& c : codes) {
+            Ent cur{c.letter, (c.code << 8) | c.len, true};
+            bool placed = false;
+            for (int kick = 0; kick < 1000 && !placed; ++kick) {
+                uint32_t b[2];
+                wide_buckets(static_cast<uint64_t>(cur.key), static_cast<uint64_t>(cur.key >> 64), lgb, W, &b[0], &b[1]);
+                for (int q = 0; q < 4 && !placed; ++q) {
+                    Ent& e = slot[2 * b[q >> 1] + (q & 1)];
+                    if (!e.used) {
+                        e = cur;
+                        placed = true;
+                    }
+                }
+                if (placed) break;
+                rng ^= rng << 13;
+                rng ^= rng >> 7;
+                rng ^= rng << 17;
+                std::swap(cur, slot[2 * b[rng & 1] + ((rng >> 1) & 1)]);  // evict, re-place the evicted
+            }
+            if (!placed) {
+                ok = false;
+                break;
+            }
+        }
+        if (ok) break;
     }
+    out.log2_slots = lgb + 1;
+    out.keys.assign(slot.size() * KB, 0);
+    out.vals.assign(slot.size(), 0);
+    for (size_t i = 0; i < slot.size(); ++i) {
+        if (!slot[i].used) continue;
+        store_letter(&out.keys[i * KB], W, slot[i].key);
+        out.vals[i] = slot[i].val;
+    }
+    out.vals32.clear();
+    if (maxlen <= 24) out.vals32.assign(out.vals.begin(), out.vals.end());
     return Status::ok();
 }
 

@@ -74,7 +74,10 @@ Status huff_wenc::bits(const huff_wtree* t, uint64_t* total, huff::u128* missing
         HUFF_TRY(keys.ensure(et->keys.size()));
         HUFF_TRY(vals.ensure(et->vals.size() * 8));
         HIP_TRY(hipMemcpyAsync(keys.p, et->keys.data(), et->keys.size(), hipMemcpyHostToDevice, s));
-        HIP_TRY(hipMemcpyAsync(vals.p, et->vals.data(), et->vals.size() * 8, hipMemcpyHostToDevice, s));
+        if (!et->vals32.empty())
+            HIP_TRY(hipMemcpyAsync(vals.p, et->vals32.data(), et->vals32.size() * 4, hipMemcpyHostToDevice, s));
+        else
+            HIP_TRY(hipMemcpyAsync(vals.p, et->vals.data(), et->vals.size() * 8, hipMemcpyHostToDevice, s));
         enc_tree = t->id;
     }
     HIP_TRY(hipMemsetAsync(missing.p, 0xFF, 8, s));
@@ -84,9 +87,11 @@ Status huff_wenc::bits(const huff_wtree* t, uint64_t* total, huff::u128* missing
     a.width = width;
     a.log2_slots = et->log2_slots;
     a.keys = static_cast<const uint8_t*>(keys.p);
-    a.vals = static_cast<const uint64_t*>(vals.p);
-    a.table_in_lds = huff::dev::wide_table_lds_bytes(width, et->log2_slots) <= kTableLdsMax;
+    a.vals = vals.p;
+    a.val32 = !et->vals32.empty();
+    a.table_in_lds = huff::dev::wide_table_lds_bytes(width, et->log2_slots, a.val32) <= kTableLdsMax;
     a.nchunks = nchunks;
+    a.cu_count = static_cast<uint32_t>(ctx->cu_count);
     a.chunk_bits = static_cast<uint64_t*>(chunk_bits.p);
     a.sub_bit = static_cast<uint32_t*>(sub_bit.p);
     a.first_missing = static_cast<unsigned long long*>(missing.p);
@@ -124,9 +129,11 @@ Status huff_wenc::pack(const huff_wtree* t, uint8_t* d_out, size_t out_cap, uint
     a.width = width;
     a.log2_slots = et->log2_slots;
     a.keys = static_cast<const uint8_t*>(keys.p);
-    a.vals = static_cast<const uint64_t*>(vals.p);
-    a.table_in_lds = huff::dev::wide_table_lds_bytes(width, et->log2_slots) <= kTableLdsMax;
+    a.vals = vals.p;
+    a.val32 = !et->vals32.empty();
+    a.table_in_lds = huff::dev::wide_table_lds_bytes(width, et->log2_slots, a.val32) <= kTableLdsMax;
     a.nchunks = nchunks;
+    a.cu_count = static_cast<uint32_t>(ctx->cu_count);
     a.chunk_start = static_cast<const uint64_t*>(chunk_start.p);
     a.sub_bit = static_cast<uint32_t*>(sub_bit.p);
     a.out = reinterpret_cast<uint32_t*>(d_out);
@@ -157,11 +164,14 @@ Status huff_wenc::decode(const huff_wtree* t, const uint8_t* d_comp, uint64_t co
     a.lut = static_cast<const uint32_t*>(lut.p);
     a.lut_bits = dt->bits;
     a.letters = static_cast<const uint8_t*>(letters.p);
+    a.nleaves = static_cast<uint32_t>(dt->letters.size() / width);
+    a.max_len = dt->maxdepth;
     a.width = width;
     a.chunk_start = static_cast<const uint64_t*>(chunk_start.p);
     a.sub_bit = static_cast<const uint32_t*>(sub_bit.p);
     a.sub_abs = sub_abs;
     a.nchunks = nchunks;
+    a.cu_count = static_cast<uint32_t>(ctx->cu_count);
     a.n = n;
     a.out = d_out;
     hipStream_t s = ctx->stream;
