@@ -26,5 +26,12 @@ HUFF_DISABLE_FIXED8=1 timeout -k 10 300 python bench.py --no-cpu-baseline > "$ou
 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
   --master-port 29533 bench.py --gpus 2 --steps 5 --warmup 2 --workload text --bytes-per-gpu $((1<<28)) \
   --dist-backend gloo > "$out/bench_2rank_gloo.json" 2> "$out/bench_2rank_gloo.err"
+# wider letters: timings at 1 GiB and a kernel-trace profile
+for w in 2 4 8; do
+  timeout -k 10 300 python tools/wbench.py --width $w --indexless > "$out/wide_w$w.json" 2> "$out/wide_w$w.err"
+done
+bash tools/prof_wide.sh 2 "${tag}_wide_w2" > /dev/null
+python tools/summarize_prof.py "gpurun_out/prof/${tag}_wide_w2" > "$out/prof_wide_w2.json"
+cp "gpurun_out/prof/${tag}_wide_w2/trace/run_kernel_stats.csv" "$out/kernel_stats_wide_w2.csv"
 mkdir -p "$out/profiles_copy" && cp profiles/traffic_*.json "$out/profiles_copy/"
 echo "gpu_round $tag done"
