@@ -18,8 +18,8 @@
  *    legacy default stream (PyTorch's default). Calls on
  *    different contexts are thread-safe; the host-only functions (weights,
  *    tree) are reentrant and need no context.
- *  - Only the u8 alphabet is supported (the reference's ByteWeights path);
- *    generic HuffLetter alphabets are out of scope.
+ *  - This header is the u8 alphabet (the reference's ByteWeights path); the
+ *    other integer letter types are in huffgpu_wide.h.
  */
 #ifndef HUFFGPU_H
 #define HUFFGPU_H
