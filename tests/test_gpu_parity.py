@@ -234,6 +234,38 @@ def test_device_job_medium(H, O, ctx, kind, seed, dec, monkeypatch):
     assert torch.equal(dec[:n], x[:n])
 
 
+@pytest.mark.parametrize("dec", ["auto", "1", "7"], ids=["dec-auto", "dec-single", "dec-ring"])
+def test_device_job_long_tail_codes(H, O, ctx, dec, monkeypatch):
+    """geometric bytes: codes from 1 to > 12 bits (the multi-symbol table's
+    slow path); each decode kernel forced"""
+    import torch
+
+    if dec != "auto":
+        monkeypatch.setenv("HUFF_DEC_VARIANT", dec)
+    rng = np.random.default_rng(77)
+    n = (1 << 22) + 999
+    host = np.minimum(rng.geometric(0.45, n) - 1, 255).astype(np.uint8)
+    host[rng.integers(0, n, 3000)] = rng.integers(0, 256, 3000, dtype=np.uint8)  # rare letters: long codes
+    x = torch.from_numpy(np.concatenate([host, np.zeros(64, np.uint8)])).cuda()
+    job = H.EncodeJob(ctx, x.data_ptr(), n)
+    w = job.hist()
+    tree = H.HuffTree.from_weights(H.ByteWeights.from_array(w))
+    _, ln = tree.code_table()
+    assert ln.max() > 12
+    bits = job.bits(tree)
+    out = torch.zeros((bits + 7) // 8 + 64, dtype=torch.uint8, device="cuda")
+    assert job.pack(tree, out.data_ptr(), out.numel()) == bits
+    ot = O.Tree.from_weights(O.weights_from_array(w))
+    code, oln = ot.code_table()
+    want, wbits = O.fast_encode(host, code, oln, threads=8)
+    torch.cuda.synchronize()
+    assert wbits == bits and (out[: (bits + 7) // 8].cpu().numpy() == want).all()
+    dec_t = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
+    job.decode(tree, out.data_ptr(), dec_t.data_ptr())
+    torch.cuda.synchronize()
+    assert torch.equal(dec_t[:n], x[:n])
+
+
 @pytest.mark.parametrize("general", [False, True], ids=["fixed8", "general"])
 def test_device_job_full_size_uniform(H, O, ctx, general, monkeypatch):
     """BASELINE config 2: 1 GiB uniform, bit-exact vs the checker + round trip.
