@@ -74,8 +74,8 @@ __global__ __launch_bounds__(kThreads) void k_bytemap(BytemapArgs a) {
     if (a.chunk_start)
         for (uint64_t c = gid; c <= a.nchunks; c += stride) a.chunk_start[c] = a.base_bits + c * kChunk * 8;
     if (a.sub_bit) {
-        const uint64_t nsub = (a.n + kSub - 1) / kSub;
-        for (uint64_t g = gid; g < nsub; g += stride) a.sub_bit[g] = static_cast<uint32_t>(((g * kSub) % kChunk) * 8);
+        const uint64_t nsub = (a.n + kIdx - 1) / kIdx;
+        for (uint64_t g = gid; g < nsub; g += stride) a.sub_bit[g] = static_cast<uint32_t>(((g * kIdx) % kChunk) * 8);
     }
 }
 

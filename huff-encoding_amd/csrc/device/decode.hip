@@ -107,7 +107,7 @@ __global__ __launch_bounds__(kThreads) void k_decode(DecodeArgs a) {
         }                                                                 \
     } while (0)
     if (cnt) {
-        pos = a.chunk_start[c] + a.sub_bit[(sym0 + lsym0) / kSub];
+        pos = a.chunk_start[c] + a.sub_bit[(sym0 + lsym0) / kIdx];
         START_AT(pos);
     }
     const BitSrc src{reinterpret_cast<const uint32_t*>(a.comp), a.comp, a.comp_bytes};
@@ -212,7 +212,7 @@ __global__ __launch_bounds__(kThreads) void k_decode_short(DecodeArgs a) {
     const uint32_t cnt = lsym0 >= nsym ? 0u : static_cast<uint32_t>(nsym - lsym0 < kSub ? nsym - lsym0 : kSub);
     if (cnt == 0) return;
 
-    const uint64_t pos = a.chunk_start[c] + a.sub_bit[(sym0 + lsym0) / kSub];
+    const uint64_t pos = a.chunk_start[c] + a.sub_bit[(sym0 + lsym0) / kIdx];
     uint8_t* dst = a.out + sym0 + lsym0;
     uint32_t* row = rows + t * kStageStride;
     uint64_t unit = pos >> 9;                          // 64-byte units
@@ -304,6 +304,8 @@ hipError_t launch_decode(const DecodeArgs& a, hipStream_t s) {
     if (a.nchunks == 0) return hipSuccess;
     if (a.max_len > 32) {
         hipLaunchKernelGGL(k_decode<true>, dim3(a.nchunks), dim3(kThreads), decode_lds_bytes(a.lut_bits, 0), s, a);
+    } else if (a.variant == kDecodeWave && a.mlut) {
+        return launch_decode_wave(a, s);
     } else if (a.variant == kDecodeRing && a.mlut) {
         return launch_decode_ring(a, s);
     } else {

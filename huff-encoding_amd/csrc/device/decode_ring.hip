@@ -85,7 +85,7 @@ __global__ __launch_bounds__(kThreads) void k_decode_ring(DecodeArgs a) {
     uint64_t h0 = 0;
     uint4 Bp, Bq;
     if (cnt) {
-        pos = a.sub_abs ? a.sub_abs[(sym0 + lsym0) / kSub] : a.chunk_start[c] + a.sub_bit[(sym0 + lsym0) / kSub];
+        pos = a.sub_abs ? a.sub_abs[(sym0 + lsym0) / kSub] : a.chunk_start[c] + a.sub_bit[(sym0 + lsym0) / kIdx];
         h0 = pos >> 8;  // first 32-byte half
         uint4 p, q;
         load_half(a.comp, a.comp_bytes, h0, p, q);

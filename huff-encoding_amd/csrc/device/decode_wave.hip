@@ -1,0 +1,284 @@
+// decode_wave.hip — restart-index decode with wave-contiguous memory traffic
+// (comp.rs:487-519 semantics; restart index = chunk_start + sub_bit, one
+// entry per kIdx = 64 symbols, written by pack).
+//
+// Work unit: a TASK of 4,096 consecutive symbols per wave (lane l decodes
+// symbols [64 l, 64 l + 64) of the task). A task's compressed bits are one
+// contiguous range, and so is its output, so both move as whole lines:
+//  1. the wave loads the task's compressed byte range (16-B aligned, with a
+//     small lookahead) into its LDS input stage with coalesced 16-B loads;
+//  2. every lane decodes its 64 symbols from the stage: a 64-bit window
+//     refilled 32 bits at a time (the next dword is read one refill ahead),
+//     one lookup of the top K (= 12) window bits in the multi-symbol table
+//     (LDS) per step giving up to 3 letters, ORed into the lane's current
+//     output dword, which is stored (aligned) after every step;
+//  3. the wave stores its 4 KiB of letters as 16-B coalesced stores.
+// The loads of task t+1 are issued before task t is decoded (register
+// staging), so the HBM latency of a wave's input overlaps its own decode.
+// A task whose range exceeds the stage (long local codes; never for byte
+// data whose mean code length is <= 8 bits in any 4,096-symbol window of
+// up to 9 bits/symbol) decodes straight from global memory instead.
+//
+// Roofline: HBM-bound; algorithmic traffic ceil(bits/8) (read) + n (write)
+// + 4 B per 64 symbols of index.
+#include <algorithm>
+
+#include "bitreader.hpp"
+
+namespace huff::dev {
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kWaves = kThreads / 64;
+constexpr uint32_t kLaneSym = kIdx;              // symbols per lane per task
+constexpr uint32_t kTaskSym = 64 * kLaneSym;     // 4,096 symbols per wave task
+constexpr uint32_t kOutWords = kLaneSym / 4 + 2; // output dwords per lane (64 letters + overshoot)
+constexpr uint32_t kInCap = 4608;                // input stage bytes per wave (9 bits per symbol)
+constexpr uint32_t kInPieces = kInCap / 16;      // 288 16-B pieces
+constexpr uint32_t kLoadRounds = (kInPieces + 63) / 64;  // 5
+constexpr uint32_t kWaveLds = kInCap + 64 * 4 * kOutWords;
+static_assert(kChunk % kTaskSym == 0, "a task never straddles a chunk");
+
+__device__ __forceinline__ uint4 load16_guarded(const uint8_t* __restrict__ comp, uint64_t nbytes, uint64_t b) {
+    if (b + 16 <= nbytes) return *reinterpret_cast<const uint4*>(comp + b);
+    uint32_t w[4] = {0, 0, 0, 0};
+    for (uint32_t i = 0; i < 16 && b + i < nbytes; ++i) w[i >> 2] |= static_cast<uint32_t>(comp[b + i]) << (8 * (i & 3));
+    return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+struct Task {
+    uint64_t sym0;      // first symbol
+    uint32_t nsym;      // symbols in the task (<= kTaskSym)
+    uint64_t lane_bit;  // this lane's first bit (valid when cnt > 0)
+    uint32_t cnt;       // this lane's symbols
+    uint64_t b0;        // first staged byte (16-B aligned)
+    uint32_t len;       // staged bytes
+};
+
+__device__ __forceinline__ Task task_info(const DecodeArgs& a, uint64_t t, uint32_t lane) {
+    Task k;
+    k.sym0 = t * kTaskSym;
+    k.nsym = static_cast<uint32_t>(a.n - k.sym0 < kTaskSym ? a.n - k.sym0 : kTaskSym);
+    const uint32_t ls = lane * kLaneSym;
+    k.cnt = ls >= k.nsym ? 0u : (k.nsym - ls < kLaneSym ? k.nsym - ls : kLaneSym);
+    const uint32_t c = static_cast<uint32_t>(k.sym0 / kChunk);
+    const uint64_t cs = a.chunk_start[c];
+    k.lane_bit = k.cnt ? cs + a.sub_bit[k.sym0 / kIdx + lane] : 0;
+    // readfirstlane returns int: widen through uint32_t (no sign extension)
+    const uint32_t f_lo = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(k.lane_bit)));
+    const uint32_t f_hi = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(k.lane_bit >> 32)));
+    const uint64_t first = (static_cast<uint64_t>(f_hi) << 32) | f_lo;
+    const uint64_t next = k.sym0 + kTaskSym;
+    uint64_t end;
+    if (next < a.n) {
+        end = a.chunk_start[next / kChunk] + a.sub_bit[next / kIdx];
+    } else {
+        end = a.chunk_start[a.nchunks];
+    }
+    k.b0 = (first >> 3) & ~15ull;
+    uint64_t b1 = ((end + 7) >> 3) + 32;  // lookahead: window + the dword read ahead
+    b1 = (b1 + 15) & ~15ull;
+    k.len = static_cast<uint32_t>(b1 - k.b0 < 0xFFFFFFFFull ? b1 - k.b0 : 0xFFFFFFFFull);
+    return k;
+}
+
+// dword sources for the lane decoder (stream order: the first byte is the
+// most significant): the LDS stage (byte-swapped when staged), or global memory
+struct LdsWords {
+    const uint32_t* w;
+    __device__ __forceinline__ uint32_t operator()(uint32_t i) const { return w[i]; }
+};
+struct GlobalWords {
+    const uint8_t* comp;
+    uint64_t nbytes;
+    uint64_t dw0;  // absolute dword index of word 0
+    __device__ __forceinline__ uint32_t operator()(uint32_t i) const {
+        const uint64_t b = (dw0 + i) * 4;
+        if (b + 4 <= nbytes) return __builtin_bswap32(*reinterpret_cast<const uint32_t*>(comp + b));
+        uint32_t v = 0;
+        for (uint32_t k = 0; k < 4 && b + k < nbytes; ++k) v |= static_cast<uint32_t>(comp[b + k]) << (24 - 8 * k);
+        return v;
+    }
+};
+
+// Decode `cnt` symbols starting at bit `rel` of the word source into the
+// lane's output column (dword d of the lane at ocol[64 d]: the 64 lanes of
+// a wave write 64 consecutive dwords whatever their progress, conflict-free). The window holds >= 32 valid
+// bits before every pair of lookups; a multi-symbol entry uses <= K (= 12)
+// bits. SLOW: some code is longer than K (<= 32 bits): a window whose first
+// code is that long (entry kMsSlow, rare) is refilled, decoded with the
+// single-symbol tables (global, L2-resident) and refilled again, so the
+// invariant holds for the next lookup.
+template <bool SLOW, class Words>
+__device__ __forceinline__ void decode_lane(const Words& src, uint32_t rel, uint32_t cnt, uint32_t* ocol,
+                                            const uint32_t* __restrict__ mlut, uint32_t K,
+                                            const uint32_t* __restrict__ glut, uint32_t Ks) {
+    if (cnt == 0) return;
+    uint32_t rp = rel >> 5;
+    const uint32_t sh = rel & 31;
+    uint64_t buf = ((static_cast<uint64_t>(src(rp)) << 32) | src(rp + 1)) << sh;
+    uint32_t nb = 64 - sh;
+    rp += 2;
+    uint32_t nextw = src(rp);
+    uint32_t j = 0;    // letters decoded
+    uint32_t cur = 0;  // the output dword j / 4, partially filled (aligned LDS stores only:
+                       // an unaligned ds_write_b32 is replayed by the LDS)
+
+#define WV_REFILL()                                                                                 \
+    do {                                                                                            \
+        const bool need_ = nb < 32;                                                                 \
+        const uint64_t add_ = static_cast<uint64_t>(nextw) << ((32 - nb) & 63);                     \
+        buf |= need_ ? add_ : 0ull;                                                                 \
+        nb += need_ ? 32u : 0u;                                                                     \
+        rp += need_ ? 1u : 0u;                                                                      \
+        nextw = src(rp);                                                                            \
+    } while (0)
+
+#define WV_LOOKUP()                                                                                 \
+    do {                                                                                            \
+        uint32_t e = mlut[static_cast<uint32_t>(buf >> 32) >> (32 - K)];                            \
+        if (SLOW && (e & kMsSlow)) {                                                                \
+            WV_REFILL();                                                                            \
+            uint32_t e1 = glut[static_cast<uint32_t>(buf >> (64 - Ks))];                            \
+            uint32_t d = Ks;                                                                        \
+            while (e1 & kLutPtr) {                                                                  \
+                const uint32_t idx = static_cast<uint32_t>((buf >> (56 - d)) & 0xFFu);              \
+                e1 = glut[(e1 & ~kLutPtr) + idx];                                                   \
+                d += 8;                                                                             \
+            }                                                                                       \
+            const uint32_t l1 = (e1 >> 8) & 0xFFu;                                                  \
+            buf <<= l1;                                                                             \
+            nb -= l1;                                                                               \
+            WV_REFILL();                                                                            \
+            e = (e1 & 0xFFu) | (1u << 29);                                                          \
+        }                                                                                           \
+        const uint32_t used = (e >> 24) & 31u;                                                      \
+        buf <<= used;                                                                               \
+        nb -= used;                                                                                 \
+        const uint64_t v_ = static_cast<uint64_t>(e & 0xFFFFFFu) << ((j & 3u) * 8);                 \
+        cur |= static_cast<uint32_t>(v_);                                                           \
+        ocol[(j & ~3u) * 16] = cur;                                                                 \
+        const uint32_t j2_ = j + ((e >> 29) & 3u);                                                  \
+        cur = ((j2_ ^ j) & ~3u) ? static_cast<uint32_t>(v_ >> 32) : cur;                            \
+        j = j2_;                                                                                    \
+    } while (0)
+
+    while (j < cnt) {
+        WV_REFILL();
+        WV_LOOKUP();
+        WV_LOOKUP();
+    }
+    // letters carried into the next dword by the last step
+    ocol[(j & ~3u) * 16] = cur;
+#undef WV_LOOKUP
+#undef WV_REFILL
+}
+
+template <bool SLOW>
+__global__ __launch_bounds__(kThreads) void k_decode_wave(DecodeArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    const uint32_t K = a.mlut_bits;
+    const uint32_t nent = 1u << K;
+    const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    uint32_t* mlut = lds;
+    uint8_t* wbase = reinterpret_cast<uint8_t*>(lds + nent) + wave * kWaveLds;
+    uint4* in_stage = reinterpret_cast<uint4*>(wbase);
+    uint32_t* out_stage = reinterpret_cast<uint32_t*>(wbase + kInCap);
+    for (uint32_t i = t; i < nent; i += kThreads) mlut[i] = a.mlut[i];
+    __syncthreads();
+
+    const uint64_t ntasks = (a.n + kTaskSym - 1) / kTaskSym;
+    const uint64_t step = static_cast<uint64_t>(gridDim.x) * kWaves;
+    uint64_t task = static_cast<uint64_t>(blockIdx.x) * kWaves + wave;
+    if (task >= ntasks) return;
+
+    // register staging of the next task's input
+    uint4 pre[kLoadRounds];
+    Task cur = task_info(a, task, lane);
+    auto issue = [&](const Task& k) {
+        const uint32_t np = k.len <= kInCap ? k.len / 16 : 0u;
+#pragma unroll
+        for (uint32_t r = 0; r < kLoadRounds; ++r) {
+            const uint32_t p = lane + 64 * r;
+            pre[r] = p < np ? load16_guarded(a.comp, a.comp_bytes, k.b0 + 16ull * p) : make_uint4(0, 0, 0, 0);
+        }
+    };
+    issue(cur);
+
+    while (true) {
+        // the staged input of `cur` goes to LDS, then the next task's loads are issued
+        const uint32_t np = cur.len <= kInCap ? cur.len / 16 : 0u;
+#pragma unroll
+        for (uint32_t r = 0; r < kLoadRounds; ++r) {
+            const uint32_t p = lane + 64 * r;
+            if (p < np) {
+                const uint4 v = pre[r];
+                in_stage[p] = make_uint4(__builtin_bswap32(v.x), __builtin_bswap32(v.y), __builtin_bswap32(v.z),
+                                         __builtin_bswap32(v.w));
+            }
+        }
+        const uint64_t nxt_task = task + step;
+        Task nxt;
+        const bool more = nxt_task < ntasks;
+        if (more) {
+            nxt = task_info(a, nxt_task, lane);
+            issue(nxt);
+        }
+        wave_sync();
+
+        const uint32_t rel = static_cast<uint32_t>(cur.lane_bit - cur.b0 * 8);
+        uint32_t* ocol = out_stage + lane;
+        if (cur.len <= kInCap) {
+            decode_lane<SLOW>(LdsWords{reinterpret_cast<const uint32_t*>(in_stage)}, rel, cur.cnt, ocol, mlut, K,
+                              a.lut, a.lut_bits);
+        } else {
+            decode_lane<SLOW>(GlobalWords{a.comp, a.comp_bytes, cur.b0 / 4}, rel, cur.cnt, ocol, mlut, K, a.lut,
+                              a.lut_bits);
+        }
+        wave_sync();
+
+        // 4 KiB of letters: piece p (16 B) = dwords 4 (p%4) .. +3 of lane p/4
+        uint8_t* dst = a.out + cur.sym0;
+#pragma unroll
+        for (uint32_t r = 0; r < 4; ++r) {
+            const uint32_t p = lane + 64 * r;
+            const uint32_t o = p * 16;
+            if (o >= cur.nsym) continue;
+            const uint32_t* s = out_stage + (p & 3) * 4 * 64 + (p >> 2);
+            const uint4 x = make_uint4(s[0], s[64], s[128], s[192]);
+            if (o + 16 <= cur.nsym) {
+                *reinterpret_cast<uint4*>(dst + o) = x;
+            } else {
+                const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+                for (uint32_t i = 0; o + i < cur.nsym; ++i) dst[o + i] = static_cast<uint8_t>(w[i >> 2] >> (8 * (i & 3)));
+            }
+        }
+        if (!more) break;
+        wave_sync();  // the stages are reused by the next task
+        task = nxt_task;
+        cur = nxt;
+    }
+}
+
+}  // namespace
+
+size_t decode_wave_lds_bytes(uint32_t mlut_bits) {
+    return static_cast<size_t>(1u << mlut_bits) * 4 + static_cast<size_t>(kWaves) * kWaveLds;
+}
+
+hipError_t launch_decode_wave(const DecodeArgs& a, hipStream_t s) {
+    if (a.n == 0) return hipSuccess;
+    const size_t lds = decode_wave_lds_bytes(a.mlut_bits);
+    const uint64_t ntasks = (a.n + kTaskSym - 1) / kTaskSym;
+    const uint32_t per_cu = static_cast<uint32_t>(std::max<size_t>(1, std::min<size_t>(8, (160 * 1024) / lds)));
+    const uint64_t want = (ntasks + kWaves - 1) / kWaves;
+    const uint32_t grid = static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>(want, uint64_t(a.cu_count ? a.cu_count : 256) * per_cu)));
+    if (a.max_len > a.mlut_bits)
+        hipLaunchKernelGGL(k_decode_wave<true>, dim3(grid), dim3(kThreads), lds, s, a);
+    else
+        hipLaunchKernelGGL(k_decode_wave<false>, dim3(grid), dim3(kThreads), lds, s, a);
+    return hipGetLastError();
+}
+
+}  // namespace huff::dev

@@ -6,8 +6,8 @@
 //   gw            u64[8][256]           global weights, one copy per XCD group
 //   chunk_bits    u64[nchunks]          bits per chunk (after the tree is known)
 //   chunk_start   u64[nchunks + 1]      exclusive scan of chunk_bits (+ bit base)
-//   sub_bit       u32[ceil(n/256)]      restart index: bit offset of every
-//                                       256th symbol, relative to its chunk
+//   sub_bit       u32[ceil(n/64)]       restart index: bit offset of every
+//                                       64th symbol (kIdx), relative to its chunk
 //   out           u8[ceil(bits/8)]      the compress_with_tree byte stream
 #pragma once
 
@@ -19,7 +19,8 @@ namespace huff::dev {
 
 constexpr uint32_t kChunk = 65536;      // input bytes (= symbols) per chunk / workgroup
 constexpr uint32_t kRound = 4096;       // bytes per workgroup round (256 lanes x 16 B)
-constexpr uint32_t kSub = 256;          // symbols per decode lane (restart index stride)
+constexpr uint32_t kSub = 256;          // symbols per lane of the chunk decoders (decode.hip, decode_ring.hip)
+constexpr uint32_t kIdx = 64;           // restart index stride of the byte path (sub_bit): symbols
 constexpr uint32_t kShortMaxLen = 27;   // u32 table entries: code << 5 | len
 constexpr uint32_t kLongMaxLen = 57;    // u64 table entries: code << 6 | len
 constexpr uint32_t kHistCopies = 8;     // XCD-group copies of the global weights
@@ -63,7 +64,7 @@ struct DecodeArgs {
     uint32_t lut_bits;            // K
     uint32_t lut_words;           // total words (primary + secondary)
     const uint64_t* chunk_start;  // [nchunks + 1]
-    const uint32_t* sub_bit;      // [ceil(n / kSub)]
+    const uint32_t* sub_bit;      // [ceil(n / kIdx)]
     uint32_t nchunks;
     uint32_t max_len;             // longest code (> 32: window slow path)
     uint32_t lut_rep_log2;        // primary table copies in LDS (bank spread)
@@ -71,7 +72,8 @@ struct DecodeArgs {
                                   // (index-free decode), instead of chunk_start + sub_bit
     const uint32_t* mlut;         // multi-symbol table [1 << mlut_bits] (null: none)
     uint32_t mlut_bits;
-    uint32_t variant;             // kDecodeRing or kDecodeSingle (codes <= 32 bits)
+    uint32_t variant;             // kDecodeWave, kDecodeRing or kDecodeSingle (codes <= 32 bits)
+    uint32_t cu_count;            // persistent grid of k_decode_wave
     uint64_t n;
     uint8_t* out;
 };
@@ -154,6 +156,7 @@ size_t pack_lds_bytes(bool long_codes, uint32_t stage_words);
 size_t decode_lds_bytes(uint32_t lut_bits, uint32_t rep_log2);
 constexpr uint32_t kDecodeSingle = 1;  // decode.hip k_decode_short
 constexpr uint32_t kDecodeRing = 7;    // decode_ring.hip k_decode_ring
+constexpr uint32_t kDecodeWave = 9;    // decode_wave.hip k_decode_wave (codes <= 32 bits)
 
 // Pass 1's totals straight to pinned host memory (device-visible pointer):
 // host[b] = (tag << 48) | total_b. host == nullptr: the totals stay in gw.
@@ -175,6 +178,8 @@ hipError_t launch_pack(bool long_codes, const PackArgs& a, hipStream_t s);
 hipError_t launch_decode(const DecodeArgs& a, hipStream_t s);
 hipError_t launch_decode_ring(const DecodeArgs& a, hipStream_t s);
 size_t decode_ring_lds_bytes(uint32_t mlut_bits);
+hipError_t launch_decode_wave(const DecodeArgs& a, hipStream_t s);
+size_t decode_wave_lds_bytes(uint32_t mlut_bits);
 hipError_t launch_indexless_spec(const IndexlessArgs& a, hipStream_t s);
 hipError_t launch_indexless_fix(const IndexlessArgs& a, const uint64_t* xin, uint64_t* xout, unsigned int* changed,
                                 hipStream_t s);

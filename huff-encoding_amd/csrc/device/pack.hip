@@ -263,8 +263,8 @@ __global__ __launch_bounds__(kThreads) void k_pack(PackArgs a) {
             const uint32_t tot = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(incl), 63));
             const uint32_t excl = incl - bits;
 
-            if (a.sub_bit && nvalid > 0 && (s_in_chunk & (kSub - 1)) == 0)
-                a.sub_bit[(sym0 + s_in_chunk) / kSub] = static_cast<uint32_t>(round_bit - cs + excl);
+            if (a.sub_bit && nvalid > 0 && (s_in_chunk & (kIdx - 1)) == 0)
+                a.sub_bit[(sym0 + s_in_chunk) / kIdx] = static_cast<uint32_t>(round_bit - cs + excl);
 
             if constexpr (LONG) {
                 if (bits) emit_codes<LONG>(stage, round_bit - stage_bit0 + excl, ent);

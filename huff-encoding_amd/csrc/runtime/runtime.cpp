@@ -286,7 +286,7 @@ huff::Status huff_enc::init(huff_ctx* c, const uint8_t* d, uint64_t nbytes) {
     HUFF_TRY(chunk_bits.ensure(nc * 8));
     HUFF_TRY(chunk_start.ensure((nc + 1) * 8));
     HUFF_TRY(tsum.ensure((nc / 1024 + 2) * 8));
-    HUFF_TRY(sub_bit.ensure(((n + huff::dev::kSub - 1) / huff::dev::kSub + 1) * 4));
+    HUFF_TRY(sub_bit.ensure(((n + huff::dev::kIdx - 1) / huff::dev::kIdx + 1) * 4));
     HUFF_TRY(mask.ensure(256));
     HUFF_TRY(pos.ensure(8));
     return huff::Status::ok();
@@ -467,16 +467,23 @@ huff::Status huff_enc::decode(const huff_tree* t, const uint8_t* d_comp, uint64_
     // single-symbol kernel: primary table replicated up to 4 KiB of LDS
     // (fewer bank conflicts, occupancy kept)
     a.lut_rep_log2 = static_cast<uint32_t>(std::max(0, std::min(5, 10 - static_cast<int>(dt->bits))));
-    // kernel choice: the multi-symbol ring decoder pays off when lookups
+    // kernel choice: the multi-symbol wave decoder pays off when lookups
     // return more than one letter (mean code length well under the 12-bit
-    // table index); near-8-bit codes run the single-symbol kernel.
-    // HUFF_DEC_VARIANT=1|7 forces one (tests, measurements).
-    a.variant = (total_bits < 7 * n) ? huff::dev::kDecodeRing : huff::dev::kDecodeSingle;
+    // table index: 1 GiB Zipf 1.10 -> 0.73 ms, text 0.96 -> 0.61 ms against
+    // the ring decoder); near-8-bit codes run the single-symbol kernel
+    // (0.91 ms vs 1.07 ms for the wave decoder on 8-bit codes).
+    // HUFF_DEC_VARIANT=1|7|9 forces one (tests, measurements).
+    a.variant = (total_bits < 7 * n) ? huff::dev::kDecodeWave : huff::dev::kDecodeSingle;
     if (const char* env = std::getenv("HUFF_DEC_VARIANT")) {
         const int v = std::atoi(env);
-        if (v == static_cast<int>(huff::dev::kDecodeRing) || v == static_cast<int>(huff::dev::kDecodeSingle))
+        if (v == static_cast<int>(huff::dev::kDecodeRing) || v == static_cast<int>(huff::dev::kDecodeSingle) ||
+            v == static_cast<int>(huff::dev::kDecodeWave))
             a.variant = static_cast<uint32_t>(v);
     }
+    // the wave decoder stores 16-B pieces: the output must be 16-B aligned
+    if (a.variant == huff::dev::kDecodeWave && (reinterpret_cast<uintptr_t>(d_out) & 15))
+        a.variant = (total_bits < 7 * n) ? huff::dev::kDecodeRing : huff::dev::kDecodeSingle;
+    a.cu_count = static_cast<uint32_t>(ctx->cu_count);
     a.mlut = static_cast<const uint32_t*>(ctx->d_lut.p) + dt->moff;
     a.mlut_bits = dt->mbits;
     a.n = n;
@@ -489,7 +496,7 @@ huff::Status huff_enc::decode(const huff_tree* t, const uint8_t* d_comp, uint64_
 huff::Status huff_enc::download_index(huff_index_host& idx) {
     idx.n = n;
     idx.chunk_start.resize(nchunks + 1);
-    idx.sub_bit.resize((n + huff::dev::kSub - 1) / huff::dev::kSub);
+    idx.sub_bit.resize((n + huff::dev::kIdx - 1) / huff::dev::kIdx);
     HUFF_TRY(ctx->activate());
     HIP_TRY(hipMemcpyAsync(idx.chunk_start.data(), chunk_start.p, idx.chunk_start.size() * 8, hipMemcpyDeviceToHost,
                            ctx->stream));

@@ -72,7 +72,7 @@ struct huff_tree {
 struct huff_index_host {
     uint64_t n = 0;
     std::vector<uint64_t> chunk_start;  // nchunks + 1
-    std::vector<uint32_t> sub_bit;      // ceil(n / kSub)
+    std::vector<uint32_t> sub_bit;      // ceil(n / kIdx) (byte path), ceil(n / kSub) (wide path)
 };
 
 struct huff_compress_data {
