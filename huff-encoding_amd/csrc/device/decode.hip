@@ -304,6 +304,8 @@ hipError_t launch_decode(const DecodeArgs& a, hipStream_t s) {
     if (a.nchunks == 0) return hipSuccess;
     if (a.max_len > 32) {
         hipLaunchKernelGGL(k_decode<true>, dim3(a.nchunks), dim3(kThreads), decode_lds_bytes(a.lut_bits, 0), s, a);
+    } else if (a.variant == kDecodeFixed && a.stab) {
+        return launch_decode_fixed(a, s);
     } else if (a.variant == kDecodeWave && a.mlut) {
         return launch_decode_wave(a, s);
     } else if (a.variant == kDecodeRing && a.mlut) {

@@ -261,6 +261,189 @@ __global__ __launch_bounds__(kThreads) void k_decode_wave(DecodeArgs a) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// k_decode_fixed: the same tasks, one letter per lookup. Every lane makes
+// exactly 64 lookups, so every letter has a static place: four letters are
+// joined in a register (v_perm) and a lane's 64 letters (16 registers) leave
+// as four 16-B stores that together cover whole lines. There is no output
+// stage in LDS (6 workgroups per CU instead of 3) and no lane waits for
+// another (the multi-symbol decoder's lanes need different lookup counts).
+// Per lookup: index, u16 table read, 64-bit shift by the entry (its low 6 bits
+// are the code length), one subtraction for the valid-bit count and one
+// v_perm; per two lookups a refill that ORs the next dword in unconditionally
+// (the bits it lands on are the same stream bits) and advances when fewer
+// than 32 bits were valid.
+// ---------------------------------------------------------------------------
+
+// nb (valid window bits) lives in the low 6 bits of X; the bits above are
+// don't-care (X -= entry borrows only from them)
+template <bool SLOW, class Words>
+__device__ __forceinline__ void decode_fixed64(const Words& src, uint32_t rel, uint32_t (&o)[16],
+                                               const uint16_t* __restrict__ stab, uint32_t K,
+                                               const uint32_t* __restrict__ glut, uint32_t Ks) {
+    uint32_t rp = rel >> 5;
+    const uint32_t sh = rel & 31;
+    uint64_t buf = static_cast<uint64_t>(src(rp) << sh) << 32;
+    uint32_t X = 32 - sh;
+    rp += 1;
+    uint32_t nextw = src(rp);
+
+#define FX_REFILL()                                                              \
+    do {                                                                         \
+        buf |= (static_cast<uint64_t>(nextw) << 32) >> (X & 63);                 \
+        rp += (X & 32) ? 0u : 1u;                                                \
+        X |= 32;                                                                 \
+        nextw = src(rp);                                                         \
+    } while (0)
+
+#define FX_LOOKUP(i)                                                                          \
+    do {                                                                                      \
+        uint32_t e = stab[static_cast<uint32_t>(buf >> 32) >> (32 - K)];                      \
+        if (SLOW && (e & kSsSlow)) {                                                          \
+            FX_REFILL();                                                                      \
+            uint32_t e1 = glut[static_cast<uint32_t>(buf >> (64 - Ks))];                      \
+            uint32_t d = Ks;                                                                  \
+            while (e1 & kLutPtr) {                                                            \
+                const uint32_t idx = static_cast<uint32_t>((buf >> (56 - d)) & 0xFFu);        \
+                e1 = glut[(e1 & ~kLutPtr) + idx];                                             \
+                d += 8;                                                                       \
+            }                                                                                 \
+            const uint32_t l1 = (e1 >> 8) & 0xFFu;                                            \
+            buf <<= l1;                                                                       \
+            X -= l1;                                                                          \
+            FX_REFILL();                                                                      \
+            e = (e1 & 0xFFu) << 8;                                                            \
+        }                                                                                     \
+        buf <<= (e & 63u);                                                                    \
+        X -= e;                                                                               \
+        if (((i) & 3) == 0) o[(i) >> 2] = e >> 8;                                             \
+        else o[(i) >> 2] = __builtin_amdgcn_perm(e, o[(i) >> 2],                              \
+                                                 ((i) & 3) == 1 ? 0x0C0C0500u                 \
+                                                 : ((i) & 3) == 2 ? 0x0C050100u : 0x05020100u); \
+    } while (0)
+
+#pragma unroll
+    for (int i = 0; i < 64; i += 2) {
+        FX_REFILL();
+        FX_LOOKUP(i);
+        FX_LOOKUP(i + 1);
+    }
+#undef FX_LOOKUP
+#undef FX_REFILL
+}
+
+// fallback for a task whose compressed range exceeds the stage: a compact
+// loop straight from global memory, one letter per lookup stored as a byte
+template <class Words>
+__device__ __forceinline__ void decode_fixed_global(const Words& src, uint32_t rel, uint32_t cnt, uint8_t* dst,
+                                                 const uint32_t* __restrict__ glut, uint32_t Ks) {
+    uint32_t rp = rel >> 5;
+    const uint32_t sh = rel & 31;
+    uint64_t buf = ((static_cast<uint64_t>(src(rp)) << 32) | src(rp + 1)) << sh;
+    uint32_t nb = 64 - sh;
+    rp += 2;
+    for (uint32_t j = 0; j < cnt; ++j) {
+        if (nb < 32) {
+            buf |= static_cast<uint64_t>(src(rp)) << (32 - nb);
+            nb += 32;
+            ++rp;
+        }
+        uint32_t e1 = glut[static_cast<uint32_t>(buf >> (64 - Ks))];
+        uint32_t d = Ks;
+        while (e1 & kLutPtr) {
+            const uint32_t idx = static_cast<uint32_t>((buf >> (56 - d)) & 0xFFu);
+            e1 = glut[(e1 & ~kLutPtr) + idx];
+            d += 8;
+        }
+        const uint32_t l1 = (e1 >> 8) & 0xFFu;
+        buf <<= l1;
+        nb -= l1;
+        dst[j] = static_cast<uint8_t>(e1);
+    }
+}
+
+template <bool SLOW>
+__device__ __forceinline__ void decode_fixed_body(const DecodeArgs& a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    const uint32_t K = a.stab_bits;
+    const uint32_t nent = 1u << K;
+    const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    uint16_t* stab = reinterpret_cast<uint16_t*>(lds);
+    const uint32_t tab_words = (nent + 1) / 2;
+    uint4* in_stage = reinterpret_cast<uint4*>(lds + ((tab_words + 3) & ~3u)) + wave * (kInCap / 16);
+    for (uint32_t i = t; i < tab_words; i += kThreads) lds[i] = reinterpret_cast<const uint32_t*>(a.stab)[i];
+    __syncthreads();
+
+    const uint64_t ntasks = (a.n + kTaskSym - 1) / kTaskSym;
+    const uint64_t step = static_cast<uint64_t>(gridDim.x) * kWaves;
+    uint64_t task = static_cast<uint64_t>(blockIdx.x) * kWaves + wave;
+    if (task >= ntasks) return;
+
+    uint4 pre[kLoadRounds];
+    Task cur = task_info(a, task, lane);
+    auto issue = [&](const Task& k) {
+        const uint32_t np = k.len <= kInCap ? k.len / 16 : 0u;
+#pragma unroll
+        for (uint32_t r = 0; r < kLoadRounds; ++r) {
+            const uint32_t p = lane + 64 * r;
+            pre[r] = p < np ? load16_guarded(a.comp, a.comp_bytes, k.b0 + 16ull * p) : make_uint4(0, 0, 0, 0);
+        }
+    };
+    issue(cur);
+
+    while (true) {
+        const uint32_t np = cur.len <= kInCap ? cur.len / 16 : 0u;
+#pragma unroll
+        for (uint32_t r = 0; r < kLoadRounds; ++r) {
+            const uint32_t p = lane + 64 * r;
+            if (p < np) {
+                const uint4 v = pre[r];
+                in_stage[p] = make_uint4(__builtin_bswap32(v.x), __builtin_bswap32(v.y), __builtin_bswap32(v.z),
+                                         __builtin_bswap32(v.w));
+            }
+        }
+        const uint64_t nxt_task = task + step;
+        Task nxt;
+        const bool more = nxt_task < ntasks;
+        if (more) {
+            nxt = task_info(a, nxt_task, lane);
+            issue(nxt);
+        }
+        wave_sync();
+
+        const uint32_t rel = static_cast<uint32_t>(cur.lane_bit - cur.b0 * 8);
+        uint8_t* dst = a.out + cur.sym0 + lane * kLaneSym;
+        if (cur.len > kInCap) {
+            if (cur.cnt) decode_fixed_global(GlobalWords{a.comp, a.comp_bytes, cur.b0 / 4}, rel, cur.cnt, dst, a.lut,
+                                             a.lut_bits);
+        } else if (cur.cnt) {
+            uint32_t o[16];
+            decode_fixed64<SLOW>(LdsWords{reinterpret_cast<const uint32_t*>(in_stage)}, rel, o, stab, K, a.lut,
+                                 a.lut_bits);
+            if (cur.cnt == kLaneSym) {
+                uint4* d4 = reinterpret_cast<uint4*>(dst);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) d4[q] = make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
+            } else {
+#pragma unroll
+                for (uint32_t i = 0; i < kLaneSym; ++i)
+                    if (i < cur.cnt) dst[i] = static_cast<uint8_t>(o[i >> 2] >> (8 * (i & 3)));
+            }
+        }
+        if (!more) break;
+        wave_sync();  // the input stage is reused by the next task
+        task = nxt_task;
+        cur = nxt;
+    }
+}
+
+// 5 waves per SIMD fit the fast path's registers without spilling (90 VGPRs);
+// the long-code variant keeps the compiler's allocation
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(5, 8))) void k_decode_fixed(DecodeArgs a) {
+    decode_fixed_body<false>(a);
+}
+__global__ __launch_bounds__(kThreads) void k_decode_fixed_slow(DecodeArgs a) { decode_fixed_body<true>(a); }
+
 }  // namespace
 
 size_t decode_wave_lds_bytes(uint32_t mlut_bits) {
@@ -278,6 +461,35 @@ hipError_t launch_decode_wave(const DecodeArgs& a, hipStream_t s) {
         hipLaunchKernelGGL(k_decode_wave<true>, dim3(grid), dim3(kThreads), lds, s, a);
     else
         hipLaunchKernelGGL(k_decode_wave<false>, dim3(grid), dim3(kThreads), lds, s, a);
+    return hipGetLastError();
+}
+
+}  // namespace huff::dev
+
+namespace huff::dev {
+
+size_t decode_fixed_lds_bytes(uint32_t stab_bits) {
+    const size_t tab_words = ((1u << stab_bits) + 1) / 2;
+    return ((tab_words + 3) & ~size_t(3)) * 4 + static_cast<size_t>(kWaves) * kInCap;
+}
+
+hipError_t launch_decode_fixed(const DecodeArgs& a, hipStream_t s) {
+    if (a.n == 0) return hipSuccess;
+    const size_t lds = decode_fixed_lds_bytes(a.stab_bits);
+    const uint64_t ntasks = (a.n + kTaskSym - 1) / kTaskSym;
+    const bool slow = a.max_len > a.stab_bits;
+    // persistent grid = resident workgroups (registers and LDS both limit)
+    int per_cu = 0;
+    hipError_t err = slow ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_decode_fixed_slow, kThreads, lds)
+                          : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_decode_fixed, kThreads, lds);
+    if (err != hipSuccess || per_cu < 1) per_cu = 1;
+    const uint64_t want = (ntasks + kWaves - 1) / kWaves;
+    const uint32_t grid = static_cast<uint32_t>(
+        std::max<uint64_t>(1, std::min<uint64_t>(want, uint64_t(a.cu_count ? a.cu_count : 256) * per_cu)));
+    if (slow)
+        hipLaunchKernelGGL(k_decode_fixed_slow, dim3(grid), dim3(kThreads), lds, s, a);
+    else
+        hipLaunchKernelGGL(k_decode_fixed, dim3(grid), dim3(kThreads), lds, s, a);
     return hipGetLastError();
 }
 

@@ -32,6 +32,11 @@ constexpr uint32_t kPackWaveRound = 2048;  // bytes per wave round in pack (64 l
 // the table's index bits (decode it with the single-symbol tables)
 constexpr uint32_t kMsMaxBits = 12;
 constexpr uint32_t kMsSlow = 0x80000000u;
+// single-symbol u16 decode entry (k_decode_fixed): code length in bits
+// [0, 6), letter in [8, 16); kSsSlow: the first code is longer than the
+// table's index bits (<= kSsMaxBits)
+constexpr uint32_t kSsMaxBits = 12;
+constexpr uint32_t kSsSlow = 0x80u;
 
 
 // The code table travels in the kernel arguments (no upload copy on the
@@ -72,7 +77,9 @@ struct DecodeArgs {
                                   // (index-free decode), instead of chunk_start + sub_bit
     const uint32_t* mlut;         // multi-symbol table [1 << mlut_bits] (null: none)
     uint32_t mlut_bits;
-    uint32_t variant;             // kDecodeWave, kDecodeRing or kDecodeSingle (codes <= 32 bits)
+    const uint16_t* stab;         // single-symbol table [1 << stab_bits] (k_decode_fixed)
+    uint32_t stab_bits;
+    uint32_t variant;             // kDecodeFixed, kDecodeWave, kDecodeRing or kDecodeSingle (codes <= 32 bits)
     uint32_t cu_count;            // persistent grid of k_decode_wave
     uint64_t n;
     uint8_t* out;
@@ -157,6 +164,7 @@ size_t decode_lds_bytes(uint32_t lut_bits, uint32_t rep_log2);
 constexpr uint32_t kDecodeSingle = 1;  // decode.hip k_decode_short
 constexpr uint32_t kDecodeRing = 7;    // decode_ring.hip k_decode_ring
 constexpr uint32_t kDecodeWave = 9;    // decode_wave.hip k_decode_wave (codes <= 32 bits)
+constexpr uint32_t kDecodeFixed = 10;  // decode_wave.hip k_decode_fixed (codes <= 32 bits)
 
 // Pass 1's totals straight to pinned host memory (device-visible pointer):
 // host[b] = (tag << 48) | total_b. host == nullptr: the totals stay in gw.
@@ -179,6 +187,7 @@ hipError_t launch_decode(const DecodeArgs& a, hipStream_t s);
 hipError_t launch_decode_ring(const DecodeArgs& a, hipStream_t s);
 size_t decode_ring_lds_bytes(uint32_t mlut_bits);
 hipError_t launch_decode_wave(const DecodeArgs& a, hipStream_t s);
+hipError_t launch_decode_fixed(const DecodeArgs& a, hipStream_t s);
 size_t decode_wave_lds_bytes(uint32_t mlut_bits);
 hipError_t launch_indexless_spec(const IndexlessArgs& a, hipStream_t s);
 hipError_t launch_indexless_fix(const IndexlessArgs& a, const uint64_t* xin, uint64_t* xout, unsigned int* changed,

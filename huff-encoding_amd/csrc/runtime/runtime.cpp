@@ -82,6 +82,33 @@ void build_multi_table(const HuffTree& t, uint32_t mbits, DecTables& out) {
     }
 }
 
+// entry i of the single-symbol table: the first code of the sbits-bit window
+// i (MSB first), walked from the root as decompress does (comp.rs:487-519)
+static void build_single_table(const HuffTree& t, uint32_t sbits, DecTables& out) {
+    const auto& nodes = t.nodes();
+    const uint32_t n = 1u << sbits;
+    out.sbits = sbits;
+    out.soff = static_cast<uint32_t>(out.lut.size());
+    out.lut.resize(out.lut.size() + (n + 1) / 2, 0);
+    uint16_t* s = reinterpret_cast<uint16_t*>(out.lut.data() + out.soff);
+    for (uint32_t i = 0; i < n; ++i) {
+        uint16_t e = static_cast<uint16_t>(dev::kSsSlow);
+        if (t.root_is_leaf()) {  // every bit decodes the root letter (comp.rs:506-509)
+            e = static_cast<uint16_t>(1u | (static_cast<uint32_t>(nodes[t.root()].letter) << 8));
+        } else {
+            int32_t x = t.root();
+            for (uint32_t p = 0; p < sbits; ++p) {
+                x = ((i >> (sbits - 1 - p)) & 1u) ? nodes[x].right : nodes[x].left;
+                if (nodes[x].is_leaf) {
+                    e = static_cast<uint16_t>((p + 1) | (static_cast<uint32_t>(nodes[x].letter) << 8));
+                    break;
+                }
+            }
+        }
+        s[i] = e;
+    }
+}
+
 Status build_dec_tables(const HuffTree& t, DecTables& out) {
     const auto& nodes = t.nodes();
     out.lut.clear();
@@ -91,6 +118,7 @@ Status build_dec_tables(const HuffTree& t, DecTables& out) {
         const uint32_t e = (1u << 8) | nodes[t.root()].letter;
         out.lut = {e, e};
         build_multi_table(t, ms_bits(), out);
+        build_single_table(t, 1, out);
         return Status::ok();
     }
     const uint32_t maxd = t.max_depth();
@@ -141,6 +169,7 @@ Status build_dec_tables(const HuffTree& t, DecTables& out) {
         }
     }
     build_multi_table(t, ms_bits(), out);
+    build_single_table(t, std::min<uint32_t>(maxd, dev::kSsMaxBits), out);
     return Status::ok();
 }
 
@@ -467,25 +496,29 @@ huff::Status huff_enc::decode(const huff_tree* t, const uint8_t* d_comp, uint64_
     // single-symbol kernel: primary table replicated up to 4 KiB of LDS
     // (fewer bank conflicts, occupancy kept)
     a.lut_rep_log2 = static_cast<uint32_t>(std::max(0, std::min(5, 10 - static_cast<int>(dt->bits))));
-    // kernel choice: the multi-symbol wave decoder pays off when lookups
-    // return more than one letter (mean code length well under the 12-bit
-    // table index: 1 GiB Zipf 1.10 -> 0.73 ms, text 0.96 -> 0.61 ms against
-    // the ring decoder); near-8-bit codes run the single-symbol kernel
-    // (0.91 ms vs 1.07 ms for the wave decoder on 8-bit codes).
-    // HUFF_DEC_VARIANT=1|7|9 forces one (tests, measurements).
-    a.variant = (total_bits < 7 * n) ? huff::dev::kDecodeWave : huff::dev::kDecodeSingle;
+    // kernel choice: the fixed-count single-symbol decoder (decode_wave.hip,
+    // k_decode_fixed) for every tree with codes <= 32 bits. 1 GiB, ms:
+    //                 fixed  wave(multi-symbol)  ring  single
+    //   Zipf(1.2)     0.59   0.73                1.10  -
+    //   text          0.56   0.61                0.90  -
+    //   8-bit codes   0.74   1.06                -     0.94
+    // HUFF_DEC_VARIANT=1|7|9|10 forces one (tests, measurements).
+    a.variant = huff::dev::kDecodeFixed;
     if (const char* env = std::getenv("HUFF_DEC_VARIANT")) {
         const int v = std::atoi(env);
         if (v == static_cast<int>(huff::dev::kDecodeRing) || v == static_cast<int>(huff::dev::kDecodeSingle) ||
-            v == static_cast<int>(huff::dev::kDecodeWave))
+            v == static_cast<int>(huff::dev::kDecodeWave) || v == static_cast<int>(huff::dev::kDecodeFixed))
             a.variant = static_cast<uint32_t>(v);
     }
     // the wave decoder stores 16-B pieces: the output must be 16-B aligned
-    if (a.variant == huff::dev::kDecodeWave && (reinterpret_cast<uintptr_t>(d_out) & 15))
+    if ((a.variant == huff::dev::kDecodeWave || a.variant == huff::dev::kDecodeFixed) &&
+        (reinterpret_cast<uintptr_t>(d_out) & 15))
         a.variant = (total_bits < 7 * n) ? huff::dev::kDecodeRing : huff::dev::kDecodeSingle;
     a.cu_count = static_cast<uint32_t>(ctx->cu_count);
     a.mlut = static_cast<const uint32_t*>(ctx->d_lut.p) + dt->moff;
     a.mlut_bits = dt->mbits;
+    a.stab = reinterpret_cast<const uint16_t*>(static_cast<const uint32_t*>(ctx->d_lut.p) + dt->soff);
+    a.stab_bits = dt->sbits;
     a.n = n;
     a.out = d_out;
     HUFF_TRY(ctx->timed("decode", [&] { return huff::dev::launch_decode(a, ctx->stream); }));

@@ -44,6 +44,10 @@ struct DecTables {
     // multi-symbol table, appended to `lut` at word `moff`: [1 << mbits]
     // entries for the top mbits bits of the window (dev::kMs* layout)
     uint32_t mbits = 0, moff = 0;
+    // single-symbol u16 table (decode_wave.hip k_decode_fixed), packed two
+    // entries per word at word `soff`: [1 << sbits] entries, used | letter << 8,
+    // kSsSlow for windows whose first code is longer than sbits
+    uint32_t sbits = 0, soff = 0;
 };
 
 // append the multi-symbol table (decode.hip k_decode_ms) to out.lut

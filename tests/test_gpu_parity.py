@@ -198,7 +198,7 @@ def _device_gen(H, ctx, kind, seed, n):
     return x
 
 
-@pytest.mark.parametrize("dec", ["auto", "1", "7", "9"], ids=["dec-auto", "dec-single", "dec-ring", "dec-wave"])
+@pytest.mark.parametrize("dec", ["auto", "1", "7", "9", "10"], ids=["dec-auto", "dec-single", "dec-ring", "dec-wave", "dec-fixed"])
 @pytest.mark.parametrize("kind,seed", [("uniform", 0x5EED0001), ("zipf", 0x5EED0002), ("text", 0x5EED0005)])
 def test_device_job_medium(H, O, ctx, kind, seed, dec, monkeypatch):
     """16 MiB + ragged tail of each workload; decode through the kernel the
@@ -234,7 +234,7 @@ def test_device_job_medium(H, O, ctx, kind, seed, dec, monkeypatch):
     assert torch.equal(dec[:n], x[:n])
 
 
-@pytest.mark.parametrize("dec", ["auto", "1", "7", "9"], ids=["dec-auto", "dec-single", "dec-ring", "dec-wave"])
+@pytest.mark.parametrize("dec", ["auto", "1", "7", "9", "10"], ids=["dec-auto", "dec-single", "dec-ring", "dec-wave", "dec-fixed"])
 def test_device_job_long_tail_codes(H, O, ctx, dec, monkeypatch):
     """geometric bytes: codes from 1 to > 12 bits (the multi-symbol table's
     slow path); each decode kernel forced"""
