@@ -109,7 +109,7 @@ def dominant_traffic(kind, phase, fixed8, dec_kernel):
     if phase == "pack":
         names = ["k_bytemap"] if fixed8 else ["k_pack"]
     elif phase == "decode":
-        names = ["k_bytemap"] if fixed8 else [dec_kernel or "k_decode_ring"]
+        names = ["k_bytemap"] if fixed8 else [dec_kernel or "k_decode_fixed"]
     if not names or not all(n in t for n in names):
         return None, None
     return int(sum(t[n]["hbm_bytes"] for n in names)), os.path.relpath(path, ROOT)
@@ -216,7 +216,7 @@ def main():
     total = state["hists"].sum(axis=0, dtype=np.uint64)
     state["fixed8"] = bool((ln[total > 0] == 8).all()) and os.environ.get("HUFF_DISABLE_FIXED8", "0") in ("", "0")
     maxlen = int(ln[total > 0].max())  # the decode kernel the runtime picks (runtime.cpp, huff_enc::decode)
-    state["dec_kernel"] = ("k_decode" if maxlen > 32 else "k_decode_ring" if bits < 7 * n else "k_decode_short")
+    state["dec_kernel"] = "k_decode" if maxlen > 32 else "k_decode_fixed"
     ms_per_step = elapsed * 1e3 / args.steps
     value = world * n / (elapsed / args.steps) / 1e9
     comp_bytes = (bits + 7) // 8
