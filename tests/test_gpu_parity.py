@@ -47,6 +47,32 @@ def test_weights_from_bytes(H, O, ctx):
     assert H.ByteWeights.from_bytes(b"", ctx).is_empty()
 
 
+def test_pass1_repeated_and_ragged(H, O, ctx, monkeypatch):
+    """pass 1 (k_hist1 + k_rows_sum + publish) run several times on one job
+    and on ragged lengths: every run equals the oracle's counts, and a pack
+    over the per-chunk rows is byte-exact (the rows set chunk_start)"""
+    import torch
+    from huff_coding import device as D
+
+    monkeypatch.setenv("HUFF_DISABLE_FIXED8", "1")
+    for n, kind, seed in [(3 * 65536 * 257 + 4095, "zipf", 11), (65536 * 5 + 1, "text", 12), (777, "uniform", 13),
+                          (65536, "uniform", 14)]:
+        x = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
+        D.generate(ctx, kind, seed, x.data_ptr(), n, cdf=D.zipf_cdf(1.2) if kind == "zipf" else None)
+        host = x[:n].cpu().numpy()
+        want = O.fast_hist(host, 8)
+        job = H.EncodeJob(ctx, x.data_ptr(), n)
+        for _ in range(3):
+            assert (job.hist() == want).all(), (n, kind)
+        tree = H.HuffTree.from_weights(H.ByteWeights.from_array(want))
+        bits = job.bits(tree)
+        out = torch.zeros((bits + 7) // 8 + 64, dtype=torch.uint8, device="cuda")
+        assert job.pack(tree, out.data_ptr(), out.numel()) == bits
+        code, ln = O.Tree.from_weights(O.weights_from_array(want)).code_table()
+        ref, rbits = O.fast_encode(host, code, ln, threads=8)
+        assert rbits == bits and (out[: (bits + 7) // 8].cpu().numpy() == ref).all(), (n, kind)
+
+
 def test_threaded_weights(H, O, ctx):
     rng = np.random.default_rng(2)
     cases = [bytes([0, 1] * 12), bytes([0, 1] * 5000), rng.integers(0, 200, 100_003, dtype=np.uint8).tobytes(),
