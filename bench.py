@@ -157,13 +157,18 @@ def main():
     state["out"] = torch.empty(n + 128, dtype=torch.uint8, device="cuda")
     state["cap"] = n + 128
 
+    # N>1 over RCCL: the pass-1 row is built on the GPU and all-gathered in
+    # stream order (one host wait per step); gloo rehearsal: host row exchange
+    dx = mgpu.DeviceExchange(dev) if world > 1 and args.dist_backend == "nccl" else None
+
     def step():
         """pass 1 -> (N>1: one all_gather) -> pass 2 (native: tree, bit base, pack) -> decode"""
-        w = job.hist()
-        if world > 1:
-            hists, tails = mgpu.exchange(w, x[n - 8:n], device=dev)
+        if dx is not None:
+            hists, tails = dx(job)
+        elif world > 1:
+            hists, tails = mgpu.exchange(job.hist(), x[n - 8:n], device=dev)
         else:
-            hists, tails = w[None, :], [b""]
+            hists, tails = job.hist()[None, :], [b""]
         try:
             tree, base, bits = job.pack_shards(hists, rank, tails, state["out"].data_ptr(), state["cap"])
         except H.HuffError as e:  # compressed shard larger than the buffer: grow once, redo

@@ -361,6 +361,12 @@ int huff_enc_hist(huff_enc* e, uint64_t weights[256]) {
     });
 }
 
+int huff_enc_hist_row(huff_enc* e, int64_t* d_row) {
+    if (!e || !d_row) return fail(HUFF_E_INVALID_ARG, "null argument");
+    if (reinterpret_cast<uintptr_t>(d_row) & 7) return fail(HUFF_E_INVALID_ARG, "d_row must be 8-byte aligned");
+    return guarded([&] { return e->hist_row(reinterpret_cast<long long*>(d_row)); });
+}
+
 int huff_enc_bits(huff_enc* e, const huff_tree* t, uint64_t* total_bits) {
     if (!e || !t || !total_bits) return fail(HUFF_E_INVALID_ARG, "null argument");
     return guarded([&] { return e->bits(t, total_bits); });
@@ -381,6 +387,10 @@ int huff_enc_pack_shards(huff_enc* e, const uint64_t* hists, uint32_t world, uin
     if (reinterpret_cast<uintptr_t>(d_out) & 15) return fail(HUFF_E_INVALID_ARG, "d_out must be 16-byte aligned");
     *tree_out = nullptr;
     return guarded([&]() -> huff::Status {
+        if (!e->have_hist) {  // pass 1 ran as huff_enc_hist_row: this shard's row is hists[rank]
+            std::memcpy(e->w, hists + static_cast<size_t>(rank) * 256, sizeof(e->w));
+            e->have_hist = true;
+        }
         auto t = std::make_unique<huff_tree>();
         HUFF_TRY(huff::HuffTree::from_weights(huff::shard_weights(hists, world), t->t));
         const huff::EncTables& et = t->enc_tables();

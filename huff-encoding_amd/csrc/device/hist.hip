@@ -199,6 +199,28 @@ __global__ __launch_bounds__(256) void k_hist_publish(const unsigned long long* 
     __hip_atomic_store(&host[t], (tag << 48) | tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// Pass 1's result as one device row for a collective (multi-GPU, SURVEY
+// §8e): row[b] = total of bin b (b < 256), row[256] = the job's last
+// min(8, n) input bytes packed little-endian, row[257] = their count. The
+// all-gather of these rows (RCCL, stream-ordered after this kernel) is the
+// only exchange of the sharded path; no host round trip precedes it.
+__global__ __launch_bounds__(256) void k_hist_row(const unsigned long long* __restrict__ gw,
+                                                  const uint8_t* __restrict__ in, uint64_t n,
+                                                  long long* __restrict__ row) {
+    const uint32_t t = threadIdx.x;
+    uint64_t tot = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kHistCopies; ++k) tot += gw[k * 256 + t];
+    row[t] = static_cast<long long>(tot);
+    if (t == 0) {
+        const uint32_t m = n < 8 ? static_cast<uint32_t>(n) : 8u;
+        uint64_t packed = 0;
+        for (uint32_t i = 0; i < m; ++i) packed |= static_cast<uint64_t>(in[n - m + i]) << (8 * i);
+        row[256] = static_cast<long long>(packed);
+        row[257] = m;
+    }
+}
+
 // bits[c] = sum_b chunk_hist[c][b] * len[b]; one wave per chunk.
 __global__ __launch_bounds__(256) void k_chunk_bits(const uint32_t* __restrict__ chunk_hist, uint32_t nchunks,
                                                     CodeLens lens, uint64_t* __restrict__ bits) {
@@ -291,6 +313,12 @@ hipError_t launch_hist(const uint8_t* base, uint64_t lo, uint64_t hi, uint32_t n
     const hipError_t e = hipMemsetAsync(gw, 0, kHistCopies * 256 * 8, s);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_hist, dim3(grid), dim3(kThreads), 0, s, base, lo, hi, nchunks, chunk_hist, gw);
+    return hipGetLastError();
+}
+
+hipError_t launch_hist_row(const unsigned long long* gw, const uint8_t* in, uint64_t n, long long* row,
+                           hipStream_t s) {
+    hipLaunchKernelGGL(k_hist_row, dim3(1), dim3(256), 0, s, gw, in, n, row);
     return hipGetLastError();
 }
 

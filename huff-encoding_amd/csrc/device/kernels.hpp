@@ -174,6 +174,10 @@ struct HistDone {
 };
 hipError_t launch_hist(const uint8_t* base, uint64_t lo, uint64_t hi, uint32_t nchunks, uint32_t* chunk_hist,
                        unsigned long long* gw, hipStream_t s, HistDone done = HistDone{});
+// row[0..256) = gw summed over its copies, row[256] = in's last min(8, n)
+// bytes (little-endian), row[257] = their count
+hipError_t launch_hist_row(const unsigned long long* gw, const uint8_t* in, uint64_t n, long long* row,
+                           hipStream_t s);
 struct alignas(8) CodeLens {
     uint8_t len[256];
 };

@@ -364,6 +364,23 @@ huff::Status huff_enc::hist() {
     return huff::Status::ok();
 }
 
+huff::Status huff_enc::hist_row(long long* d_row) {
+    HUFF_TRY(ctx->activate());
+    hipStream_t s = ctx->stream;
+    have_hist = packed = false;
+    if (nchunks == 0) {
+        HIP_TRY(hipMemsetAsync(d_row, 0, 258 * 8, s));
+        return huff::Status::ok();
+    }
+    HUFF_TRY(ctx->timed("hist", [&] {
+        hipError_t e = huff::dev::launch_hist(d_in, 0, n, nchunks, static_cast<uint32_t*>(chunk_hist.p),
+                                              static_cast<unsigned long long*>(gw.p), s);
+        if (e != hipSuccess) return e;
+        return huff::dev::launch_hist_row(static_cast<const unsigned long long*>(gw.p), d_in, n, d_row, s);
+    }));
+    return huff::Status::ok();
+}
+
 huff::Status huff_enc::bits(const huff_tree* t, uint64_t* total) {
     if (!have_hist) return huff::Status::err(HUFF_E_STATE, "huff_enc_hist must run before bits/pack");
     const huff::EncTables& et = t->enc_tables();

@@ -151,6 +151,9 @@ struct huff_enc {
 
     huff::Status init(huff_ctx* c, const uint8_t* d, uint64_t nbytes);
     huff::Status hist();
+    // pass 1 without a host wait: weights + tail bytes as a device row (see
+    // huff_enc_hist_row); the weights reach the host with the exchanged rows
+    huff::Status hist_row(long long* d_row);
     huff::Status bits(const huff_tree* t, uint64_t* total);
     huff::Status pack(const huff_tree* t, uint64_t bit_base, const uint8_t* prev_tail, size_t prev_tail_len,
                       uint8_t* d_out, size_t out_cap, uint64_t* total);

@@ -47,6 +47,11 @@ class EncodeJob:
         _check(load().huff_enc_hist(self.h, w.ctypes.data))
         return w
 
+    def hist_row(self, d_row: int):
+        """pass 1 enqueued without a host wait: 258 int64 at d_row (device) =
+        [weights(256) | last <= 8 input bytes, little-endian | their count]"""
+        _check(load().huff_enc_hist_row(self.h, C.c_void_p(d_row)))
+
     def bits(self, tree) -> int:
         v = C.c_uint64()
         _check(load().huff_enc_bits(self.h, tree.h, C.byref(v)))

@@ -62,10 +62,38 @@ def exchange(weights: np.ndarray, tail, device: Optional[torch.device] = None, g
         rt.view(torch.uint8)[256 * 8: 256 * 8 + tail.numel()] = tail
     rows = [torch.empty_like(rt) for _ in range(world)]
     dist.all_gather(rows, rt, group=group)
-    allr = torch.stack(rows).cpu().numpy()
+    return rows_to_hists(torch.stack(rows).cpu().numpy())
+
+
+def rows_to_hists(allr: np.ndarray):
+    """[world, 258] int64 rows (exchange layout) -> (hists u64 [world, 256], tails)"""
     hists = allr[:, :256].view(np.uint64).copy()
-    tails = [allr[q, 256:257].view(np.uint8)[: int(allr[q, 257])].tobytes() for q in range(world)]
+    tails = [allr[q, 256:257].view(np.uint8)[: int(allr[q, 257])].tobytes() for q in range(allr.shape[0])]
     return hists, tails
+
+
+class DeviceExchange:
+    """The sharded pass 1 with the row built on the GPU (huff_enc_hist_row)
+    and all-gathered by RCCL in stream order: hist kernels -> row kernel ->
+    all_gather_into_tensor -> one copy of the world x 258 rows into pinned
+    host memory -> ONE host wait. No host round trip precedes the collective
+    (compare exchange(), which reads the weights back first)."""
+
+    def __init__(self, device: torch.device, group=None):
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.row = torch.empty(258, dtype=torch.int64, device=device)
+        self.rows = torch.empty(self.world * 258, dtype=torch.int64, device=device)
+        self.host = torch.empty(self.world * 258, dtype=torch.int64, pin_memory=True)
+        self.done = torch.cuda.Event()
+
+    def __call__(self, job):
+        job.hist_row(self.row.data_ptr())  # on the context stream = torch's current stream
+        dist.all_gather_into_tensor(self.rows, self.row, group=self.group)
+        self.host.copy_(self.rows, non_blocking=True)
+        self.done.record()
+        self.done.synchronize()
+        return rows_to_hists(self.host.numpy().reshape(self.world, 258))
 
 
 def plan(hists: np.ndarray, tails: List[bytes], code_len: np.ndarray, rank: int) -> ShardPlan:

@@ -171,6 +171,14 @@ int huff_enc_create(huff_ctx* ctx, const uint8_t* d_in, size_t n, huff_enc** out
 void huff_enc_free(huff_enc* e);
 /* pass 1: hist256 over the job (per-chunk + global); weights to host */
 int huff_enc_hist(huff_enc* e, uint64_t weights[256]);
+/* pass 1 for a sharded job without a host round trip (replaces
+ * the per-shard ByteWeights::threaded_from_bytes + merge, weights.rs:293-319):
+ * enqueues hist256 on the context stream and writes one row of 258 int64 to
+ * device memory d_row: [0, 256) the job's weights, [256] its last min(8, n)
+ * input bytes packed little-endian, [257] their count. The caller all-gathers
+ * the rows (RCCL, same stream order) and passes them to huff_enc_pack_shards
+ * (as hists / tails), which also takes this job's weights from hists[rank]. */
+int huff_enc_hist_row(huff_enc* e, int64_t* d_row);
 /* Total bits the tree assigns to this job (needs huff_enc_hist first). */
 int huff_enc_bits(huff_enc* e, const huff_tree* t, uint64_t* total_bits);
 /* pass 2: pack. The job's first symbol starts at global stream bit `bit_base`;

@@ -519,3 +519,56 @@ def test_file_path_matches_cli(H, O, ctx, golden):
         open(empty, "wb").close()
         with pytest.raises(H.HuffPanic, match="empty weights"):
             H.read_compress_write(empty, empty + ".hff", 100, ctx)
+
+
+def test_hist_row_and_device_exchange(H, O, ctx):
+    """the sharded pass 1 without a host round trip: huff_enc_hist_row's
+    device row (weights | tail bytes | count) equals the oracle, and the
+    RCCL path (DeviceExchange: row -> all_gather_into_tensor -> pinned copy,
+    a world-1 process group here) feeds huff_enc_pack_shards to the same bytes
+    as the single-GPU encode"""
+    import torch
+    import torch.distributed as dist
+    from huff_coding import device as D
+    from huff_coding import mgpu
+
+    row = torch.empty(258, dtype=torch.int64, device="cuda")
+    for n in (0, 5, 65536 * 3 + 7, (1 << 22) + 12345):
+        x = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
+        if n:
+            D.generate(ctx, "zipf", 21 + n, x.data_ptr(), n, cdf=D.zipf_cdf(1.2))
+        host = x[:n].cpu().numpy()
+        job = H.EncodeJob(ctx, x.data_ptr(), n)
+        job.hist_row(row.data_ptr())
+        torch.cuda.synchronize()
+        hists, tails = mgpu.rows_to_hists(row.cpu().numpy()[None, :])
+        assert (hists[0] == (O.fast_hist(host, 8) if n else 0)).all(), n
+        assert tails[0] == host[-8:].tobytes(), n
+
+    if not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29541")
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        n = (1 << 23) + 333
+        x = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
+        D.generate(ctx, "text", 5, x.data_ptr(), n)
+        host = x[:n].cpu().numpy()
+        job = H.EncodeJob(ctx, x.data_ptr(), n)
+        ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+        dx = mgpu.DeviceExchange(torch.device("cuda", 0))
+        out = torch.zeros(n + 128, dtype=torch.uint8, device="cuda")
+        for _ in range(2):
+            hists, tails = dx(job)
+            tree, base, bits = job.pack_shards(hists, 0, tails, out.data_ptr(), out.numel())
+            torch.cuda.synchronize()
+            code, ln = O.Tree.from_weights(O.weights_from_array(O.fast_hist(host, 8))).code_table()
+            want, wbits = O.fast_encode(host, code, ln, threads=8)
+            assert base == 0 and bits == wbits
+            assert (out[: (bits + 7) // 8].cpu().numpy() == want).all()
+            dec = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
+            job.decode(tree, out.data_ptr(), dec.data_ptr())
+            torch.cuda.synchronize()
+            assert torch.equal(dec[:n], x[:n])
+    finally:
+        dist.destroy_process_group()
