@@ -35,6 +35,11 @@ constexpr uint32_t kLaneSym = kIdx;              // symbols per lane per task
 constexpr uint32_t kTaskSym = 64 * kLaneSym;     // 4,096 symbols per wave task
 constexpr uint32_t kOutWords = kLaneSym / 4 + 2; // output dwords per lane (64 letters + overshoot)
 constexpr uint32_t kInCap = 4608;                // input stage bytes per wave (9 bits per symbol)
+// k_decode_fixed's per-wave stage: the task's input, then (after the decode)
+// its 64 output rows of 64 B, padded to 80 B so the row writes
+// (ds_write_b128, 8-lane groups) hit distinct banks
+constexpr uint32_t kRowBytes = 80;
+constexpr uint32_t kFxStage = kInCap > 64 * kRowBytes ? kInCap : 64 * kRowBytes;
 constexpr uint32_t kInPieces = kInCap / 16;      // 288 16-B pieces
 constexpr uint32_t kLoadRounds = (kInPieces + 63) / 64;  // 5
 constexpr uint32_t kWaveLds = kInCap + 64 * 4 * kOutWords;
@@ -370,7 +375,7 @@ __device__ __forceinline__ void decode_fixed_body(const DecodeArgs& a) {
     const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
     uint16_t* stab = reinterpret_cast<uint16_t*>(lds);
     const uint32_t tab_words = (nent + 1) / 2;
-    uint4* in_stage = reinterpret_cast<uint4*>(lds + ((tab_words + 3) & ~3u)) + wave * (kInCap / 16);
+    uint4* in_stage = reinterpret_cast<uint4*>(lds + ((tab_words + 3) & ~3u)) + wave * (kFxStage / 16);
     for (uint32_t i = t; i < tab_words; i += kThreads) lds[i] = reinterpret_cast<const uint32_t*>(a.stab)[i];
     __syncthreads();
 
@@ -416,6 +421,23 @@ __device__ __forceinline__ void decode_fixed_body(const DecodeArgs& a) {
         if (cur.len > kInCap) {
             if (cur.cnt) decode_fixed_global(GlobalWords{a.comp, a.comp_bytes, cur.b0 / 4}, rel, cur.cnt, dst, a.lut,
                                              a.lut_bits);
+        } else if (cur.nsym == kTaskSym) {  // wave-uniform: every lane has 64 letters
+            uint32_t o[16];
+            decode_fixed64<SLOW>(LdsWords{reinterpret_cast<const uint32_t*>(in_stage)}, rel, o, stab, K, a.lut,
+                                 a.lut_bits);
+            // transpose through the stage so every store instruction writes
+            // 1 KiB contiguous (16 B per lane): lane-strided 16-B pieces cost
+            // 4x the L2 write requests and stalled the TA (PMC)
+            wave_sync();  // the wave's stage reads are done
+            uint8_t* sb = reinterpret_cast<uint8_t*>(in_stage);
+            uint4* row = reinterpret_cast<uint4*>(sb + lane * kRowBytes);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) row[q] = make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
+            wave_sync();
+            uint4* d4 = reinterpret_cast<uint4*>(a.out + cur.sym0) + lane;
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                d4[64 * q] = *reinterpret_cast<const uint4*>(sb + (16 * q + (lane >> 2)) * kRowBytes + 16 * (lane & 3));
         } else if (cur.cnt) {
             uint32_t o[16];
             decode_fixed64<SLOW>(LdsWords{reinterpret_cast<const uint32_t*>(in_stage)}, rel, o, stab, K, a.lut,
@@ -437,9 +459,11 @@ __device__ __forceinline__ void decode_fixed_body(const DecodeArgs& a) {
     }
 }
 
-// 5 waves per SIMD fit the fast path's registers without spilling (90 VGPRs);
-// the long-code variant keeps the compiler's allocation
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(5, 8))) void k_decode_fixed(DecodeArgs a) {
+// The compiler's register allocation (~100 VGPRs, 4 waves per SIMD). Forcing
+// 5 waves per SIMD (amdgpu_waves_per_eu(5, 8)) together with the transposed
+// output stage decoded wrong letters in some tasks of co-resident workgroups
+// on the GPU (root cause not found; GPU tests catch it), so it is not forced.
+__global__ __launch_bounds__(kThreads) void k_decode_fixed(DecodeArgs a) {
     decode_fixed_body<false>(a);
 }
 __global__ __launch_bounds__(kThreads) void k_decode_fixed_slow(DecodeArgs a) { decode_fixed_body<true>(a); }
@@ -470,7 +494,7 @@ namespace huff::dev {
 
 size_t decode_fixed_lds_bytes(uint32_t stab_bits) {
     const size_t tab_words = ((1u << stab_bits) + 1) / 2;
-    return ((tab_words + 3) & ~size_t(3)) * 4 + static_cast<size_t>(kWaves) * kInCap;
+    return ((tab_words + 3) & ~size_t(3)) * 4 + static_cast<size_t>(kWaves) * kFxStage;
 }
 
 hipError_t launch_decode_fixed(const DecodeArgs& a, hipStream_t s) {
