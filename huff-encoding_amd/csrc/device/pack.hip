@@ -137,11 +137,11 @@ __device__ __forceinline__ void emit_codes_or(uint32_t* __restrict__ stage, uint
 
 __device__ __forceinline__ void store_segment(const uint32_t* __restrict__ stage, uint32_t s, uint64_t gbyte,
                                               uint64_t own_lo, uint64_t own_hi, uint8_t* __restrict__ out) {
-    uint4 v;
-    v.x = __builtin_bswap32(stage[4 * s + 0]);
-    v.y = __builtin_bswap32(stage[4 * s + 1]);
-    v.z = __builtin_bswap32(stage[4 * s + 2]);
-    v.w = __builtin_bswap32(stage[4 * s + 3]);
+    uint4 v = reinterpret_cast<const uint4*>(stage)[s];  // one ds_read_b128
+    v.x = __builtin_bswap32(v.x);
+    v.y = __builtin_bswap32(v.y);
+    v.z = __builtin_bswap32(v.z);
+    v.w = __builtin_bswap32(v.w);
     if (gbyte >= own_lo && gbyte + 16 <= own_hi) {
         *reinterpret_cast<uint4*>(out + gbyte) = v;
         return;
@@ -283,8 +283,9 @@ __global__ __launch_bounds__(kThreads) void k_pack(PackArgs a) {
             uint32_t keep = 0;
             if (!last && lane < 4) keep = stage[nseg_done * 4 + lane];
             wave_sync();
-            // clear what this round wrote; carry the partial segment to the front
-            for (uint32_t i = lane; i < used_words; i += 64) stage[i] = 0;
+            // clear what this round wrote (16-B stores); carry the partial segment to the front
+            for (uint32_t i = lane; i < (used_words + 3) / 4; i += 64)
+                reinterpret_cast<uint4*>(stage)[i] = make_uint4(0, 0, 0, 0);
             wave_sync();
             if (!last) {
                 if (lane < 4) stage[lane] = keep;

@@ -470,8 +470,8 @@ huff::Status huff_enc::pack(const huff_tree* t, uint64_t base, const uint8_t* pr
     a.sub_bit = static_cast<uint32_t*>(sub_bit.p);
     a.prev_tail_len = static_cast<uint32_t>(prev_tail_len);
     // one wave round: <= kPackWaveRound*maxlen bits + a < 128-bit carry (+ the
-    // word after the last, which the OR emit may touch with zero)
-    a.stage_words = (huff::dev::kPackWaveRound / 32 * std::max<uint32_t>(et.maxlen, 1) + 8 + 3) & ~3u;
+    // 128-bit window past the last unit, which the OR emit may touch with zero)
+    a.stage_words = (huff::dev::kPackWaveRound / 32 * std::max<uint32_t>(et.maxlen, 1) + 12 + 3) & ~3u;
     a.max_len = et.maxlen;
     const size_t lds = huff::dev::pack_lds_bytes(long_codes, a.stage_words);
     const uint32_t per_cu = std::max<uint32_t>(1, std::min<uint32_t>(8, static_cast<uint32_t>((160 * 1024) / lds)));
