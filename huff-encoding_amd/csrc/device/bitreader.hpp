@@ -27,6 +27,23 @@ __device__ __forceinline__ uint4 ld_nt(const uint4* p) {
     return make_uint4(v.x, v.y, v.z, v.w);
 }
 
+// Raw buffer resource over [p, p + bytes): loads at offsets past `bytes`
+// return zero without touching memory (the range check is per dword), so a
+// wave can issue loads for a partial or absent range unconditionally — a
+// bounds-checked load (a branch with a byte-wise fallback) makes the
+// compiler wait for every outstanding load right after it, which defeats
+// any prefetch. Dword 3 = the gfx9 default format word.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* p, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, static_cast<int>(bytes), 0x00020000);
+}
+// 16-byte buffer load; AUX 2 = nontemporal
+template <int AUX = 0>
+__device__ __forceinline__ uint4 buf_ld16(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, static_cast<int>(off), 0, AUX);
+    return make_uint4(static_cast<uint32_t>(v[0]), static_cast<uint32_t>(v[1]), static_cast<uint32_t>(v[2]),
+                      static_cast<uint32_t>(v[3]));
+}
+
 // inclusive prefix sum over the 64 lanes of a wave with DPP (no LDS round
 // trips): row_shr 1/2/4/8 within each 16-lane row, then row_bcast 15 / 31
 // carry the row totals upward. Lanes with no source read `old` = 0.

@@ -27,6 +27,7 @@ constexpr uint32_t kHistCopies = 8;     // XCD-group copies of the global weight
 constexpr uint32_t kLutMaxBits = 12;    // primary decode table index bits
 constexpr uint32_t kLutPtr = 0x80000000u;
 constexpr uint32_t kPackWaveRound = 2048;  // bytes per wave round in pack (64 lanes x 32 B)
+constexpr uint32_t kPackWaves = 8;         // waves per pack workgroup (short codes; long codes: 4)
 // multi-symbol decode entry: up to 3 letters in bits [0, 24), bits used in
 // [24, 29), letter count in [29, 31); kMsSlow: the first code is longer than
 // the table's index bits (decode it with the single-symbol tables)
@@ -160,6 +161,7 @@ hipError_t wide_weights(uint32_t width, const void* d_in, uint64_t n, void* d_so
                         uint64_t* d_counts, uint64_t* d_nruns, void* d_tmp, size_t* tmp_bytes, hipStream_t s);
 
 size_t pack_lds_bytes(bool long_codes, uint32_t stage_words);
+uint32_t pack_waves_per_group(bool long_codes);
 size_t decode_lds_bytes(uint32_t lut_bits, uint32_t rep_log2);
 constexpr uint32_t kDecodeSingle = 1;  // decode.hip k_decode_short
 constexpr uint32_t kDecodeRing = 7;    // decode_ring.hip k_decode_ring

@@ -35,8 +35,11 @@ namespace huff::dev {
 
 namespace {
 
-constexpr int kThreads = 256;
-constexpr int kWaves = kThreads / 64;
+// waves per workgroup: 8 for short codes (one 32 KiB table shared by 8
+// waves: 2 workgroups = 4 waves per SIMD fit the LDS), 4 for long codes (a
+// 64 KiB table)
+template <bool LONG>
+constexpr int pack_waves() { return LONG ? 4 : static_cast<int>(kPackWaves); }
 constexpr uint32_t kBPL = kPackWaveRound / 64;  // consecutive input bytes per lane per round
 static_assert(kBPL % 16 == 0, "lanes load whole 16-byte pieces");
 constexpr int kPieces = kBPL / 16;
@@ -154,15 +157,10 @@ __device__ __forceinline__ void store_segment(const uint32_t* __restrict__ stage
     }
 }
 
-__device__ __forceinline__ uint4 load_lane(const uint8_t* __restrict__ in, uint64_t n, uint64_t g) {
-    if (g + 16 <= n) return *reinterpret_cast<const uint4*>(in + g);
-    uint32_t w[4] = {0, 0, 0, 0};
-    for (int i = 0; g + i < n && i < 16; ++i) w[i >> 2] |= static_cast<uint32_t>(in[g + i]) << (8 * (i & 3));
-    return make_uint4(w[0], w[1], w[2], w[3]);
-}
-
 template <bool LONG, int G = 1>
-__global__ __launch_bounds__(kThreads) void k_pack(PackArgs a) {
+__global__ __launch_bounds__(pack_waves<LONG>() * 64) void k_pack(PackArgs a) {
+    constexpr int kWaves = pack_waves<LONG>();
+    constexpr int kThreads = kWaves * 64;
     using E = Entry<LONG>;
     using T = typename E::T;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -173,8 +171,8 @@ __global__ __launch_bounds__(kThreads) void k_pack(PackArgs a) {
     // replicate the table: thread t writes copy t%32 of letters t/32 + 8i
     const T* tg = reinterpret_cast<const T*>(LONG ? static_cast<const void*>(a.table.l) : static_cast<const void*>(a.table.s));
 #pragma unroll 4
-    for (int i = 0; i < 32; ++i) {
-        const uint32_t e = (t >> 5) + 8 * i;
+    for (int i = 0; i < 256 / (kThreads / 32); ++i) {
+        const uint32_t e = (t >> 5) + (kThreads / 32) * i;
         tab[(e << 5) | copy] = tg[e];
     }
     for (uint32_t i = lane; i < a.stage_words; i += 64) stage[i] = 0;
@@ -189,16 +187,16 @@ __global__ __launch_bounds__(kThreads) void k_pack(PackArgs a) {
         const uint64_t own_lo = cs >> 3;
         const uint64_t own_hi = (c + 1 == a.nchunks) ? (ce + 7) >> 3 : ce >> 3;
         const uint32_t nrounds = static_cast<uint32_t>((nsym + kPackWaveRound - 1) / kPackWaveRound);
-        const uint8_t* cin = a.in + sym0;
-        const uint64_t cn = nsym;
+        // the chunk's bytes through a buffer resource (rounded up to the 16-B
+        // granule of its end: bytes past n are masked by nvalid): loads past
+        // it, and whole rounds past the chunk, read zeros, so the loads run
+        // 2 rounds ahead unconditionally and stay in flight
+        const auto rin = buf_rsrc(a.in + sym0, static_cast<uint32_t>((nsym + 15) & ~15ull));
 
-        // loads run 2 rounds ahead
         auto load_round = [&](uint32_t r) {
             LaneIn x;
 #pragma unroll
-            for (int q = 0; q < kPieces; ++q)
-                x.v[q] = r < nrounds ? load_lane(cin, cn, static_cast<uint64_t>(r) * kPackWaveRound + lane * kBPL + 16 * q)
-                                     : make_uint4(0, 0, 0, 0);
+            for (int q = 0; q < kPieces; ++q) x.v[q] = buf_ld16(rin, r * kPackWaveRound + lane * kBPL + 16 * q);
             return x;
         };
         LaneIn v0 = load_round(0);
@@ -237,7 +235,7 @@ __global__ __launch_bounds__(kThreads) void k_pack(PackArgs a) {
         for (uint32_t r = 0; r < nrounds; ++r) {
             const LaneIn v = v0;
             v0 = v1;
-            if (r + 2 < nrounds) v1 = load_round(r + 2);
+            v1 = load_round(r + 2);
             const uint64_t s_in_chunk = static_cast<uint64_t>(r) * kPackWaveRound + lane * kBPL;
             const int nvalid = s_in_chunk >= nsym ? 0 : (nsym - s_in_chunk >= kBPL ? static_cast<int>(kBPL)
                                                                                      : static_cast<int>(nsym - s_in_chunk));
@@ -301,20 +299,23 @@ __global__ __launch_bounds__(kThreads) void k_pack(PackArgs a) {
 
 size_t pack_lds_bytes(bool long_codes, uint32_t stage_words) {
     const uint32_t table = long_codes ? Entry<true>::kTableWords : Entry<false>::kTableWords;
-    return static_cast<size_t>(table + kWaves * stage_words) * 4;
+    const uint32_t waves = long_codes ? pack_waves<true>() : pack_waves<false>();
+    return static_cast<size_t>(table + waves * stage_words) * 4;
 }
+
+uint32_t pack_waves_per_group(bool long_codes) { return long_codes ? pack_waves<true>() : pack_waves<false>(); }
 
 hipError_t launch_pack(bool long_codes, const PackArgs& a, hipStream_t s) {
     if (a.nchunks == 0) return hipSuccess;
     const size_t lds = pack_lds_bytes(long_codes, a.stage_words);
     if (long_codes) {
-        hipLaunchKernelGGL(k_pack<true>, dim3(a.grid), dim3(kThreads), lds, s, a);
+        hipLaunchKernelGGL(k_pack<true>, dim3(a.grid), dim3(pack_waves<true>() * 64), lds, s, a);
     } else if (a.max_len <= 8) {  // 4 codes per OR pair
-        hipLaunchKernelGGL((k_pack<false, 4>), dim3(a.grid), dim3(kThreads), lds, s, a);
+        hipLaunchKernelGGL((k_pack<false, 4>), dim3(a.grid), dim3(pack_waves<false>() * 64), lds, s, a);
     } else if (a.max_len <= 16) {
-        hipLaunchKernelGGL((k_pack<false, 2>), dim3(a.grid), dim3(kThreads), lds, s, a);
+        hipLaunchKernelGGL((k_pack<false, 2>), dim3(a.grid), dim3(pack_waves<false>() * 64), lds, s, a);
     } else {
-        hipLaunchKernelGGL((k_pack<false, 1>), dim3(a.grid), dim3(kThreads), lds, s, a);
+        hipLaunchKernelGGL((k_pack<false, 1>), dim3(a.grid), dim3(pack_waves<false>() * 64), lds, s, a);
     }
     return hipGetLastError();
 }

@@ -475,7 +475,8 @@ huff::Status huff_enc::pack(const huff_tree* t, uint64_t base, const uint8_t* pr
     a.max_len = et.maxlen;
     const size_t lds = huff::dev::pack_lds_bytes(long_codes, a.stage_words);
     const uint32_t per_cu = std::max<uint32_t>(1, std::min<uint32_t>(8, static_cast<uint32_t>((160 * 1024) / lds)));
-    a.grid = std::max<uint32_t>(1, std::min<uint32_t>((nchunks + 3) / 4, ctx->cu_count * per_cu));
+    const uint32_t wpg = huff::dev::pack_waves_per_group(long_codes);
+    a.grid = std::max<uint32_t>(1, std::min<uint32_t>((nchunks + wpg - 1) / wpg, ctx->cu_count * per_cu));
     HUFF_TRY(ctx->timed("pack", [&] { return huff::dev::launch_pack(long_codes, a, s); }));
     packed = true;
     packed_tree_id = t->id;
