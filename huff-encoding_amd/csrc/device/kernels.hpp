@@ -26,7 +26,7 @@ constexpr uint32_t kLongMaxLen = 57;    // u64 table entries: code << 6 | len
 constexpr uint32_t kHistCopies = 8;     // XCD-group copies of the global weights
 constexpr uint32_t kLutMaxBits = 12;    // primary decode table index bits
 constexpr uint32_t kLutPtr = 0x80000000u;
-constexpr uint32_t kPackWaveRound = 2048;  // bytes per wave round in pack (64 lanes x 32 B)
+constexpr uint32_t kPackWaveRound = 1024;  // bytes per wave round in pack (64 lanes x 16 B: ~80 VGPRs, 6 waves per SIMD)
 constexpr uint32_t kPackWaves = 8;         // waves per pack workgroup (short codes; long codes: 4)
 // multi-symbol decode entry: up to 3 letters in bits [0, 24), bits used in
 // [24, 29), letter count in [29, 31); kMsSlow: the first code is longer than

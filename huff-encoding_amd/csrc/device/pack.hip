@@ -4,10 +4,11 @@
 //
 // Work unit: one 64 KiB chunk per WAVE, whose first output bit is known
 // (chunk_start = exclusive scan of per-chunk bit counts). Workgroups are
-// persistent (4 waves, grid sized to residency) so the code table is copied
-// into LDS once per workgroup; each wave then walks its chunks in rounds of
-// 2 KiB (64 lanes x 32 consecutive bytes) with no workgroup barrier:
-//   1. 32 lookups per lane in the LDS code table, replicated 32x as
+// persistent (8 waves sharing one code table in LDS, grid sized to
+// residency: 3 workgroups = 6 waves per SIMD); each wave walks its chunks in
+// rounds of 1 KiB (64 lanes x 16 consecutive bytes) with no workgroup
+// barrier:
+//   1. 16 lookups per lane in the LDS code table, replicated 32x as
 //      [letter][copy] (lane l reads copy l % 32: bank-conflict-free on any
 //      data), summing the lane's bit count;
 //   2. a wave-wide exclusive scan of the lanes' bit counts (DPP row shifts
@@ -20,7 +21,8 @@
 //   4. complete 16-byte segments leave as one dwordx4 store per lane
 //      (byte-swapped: the stream is MSB-first); the partial last segment is
 //      carried to the next round.
-// Loads run 2 rounds (4 KiB per wave) ahead of the encoder.
+// Loads run 2 rounds ahead of the encoder through a buffer resource clamped
+// to the chunk (unconditional: out-of-range loads read zero), ~80 VGPRs.
 // A chunk's first output byte is shared with the previous chunk: the wave
 // recomputes the previous chunk's last <= 7 bits from the input bytes before
 // it (from prev_tail for the first chunk of a shard), so every output byte is
