@@ -45,13 +45,6 @@ constexpr uint32_t kLoadRounds = (kInPieces + 63) / 64;  // 5
 constexpr uint32_t kWaveLds = kInCap + 64 * 4 * kOutWords;
 static_assert(kChunk % kTaskSym == 0, "a task never straddles a chunk");
 
-__device__ __forceinline__ uint4 load16_guarded(const uint8_t* __restrict__ comp, uint64_t nbytes, uint64_t b) {
-    if (b + 16 <= nbytes) return *reinterpret_cast<const uint4*>(comp + b);
-    uint32_t w[4] = {0, 0, 0, 0};
-    for (uint32_t i = 0; i < 16 && b + i < nbytes; ++i) w[i >> 2] |= static_cast<uint32_t>(comp[b + i]) << (8 * (i & 3));
-    return make_uint4(w[0], w[1], w[2], w[3]);
-}
-
 struct Task {
     uint64_t sym0;      // first symbol
     uint32_t nsym;      // symbols in the task (<= kTaskSym)
@@ -85,7 +78,24 @@ __device__ __forceinline__ Task task_info(const DecodeArgs& a, uint64_t t, uint3
     uint64_t b1 = ((end + 7) >> 3) + 32;  // lookahead: window + the dword read ahead
     b1 = (b1 + 15) & ~15ull;
     k.len = static_cast<uint32_t>(b1 - k.b0 < 0xFFFFFFFFull ? b1 - k.b0 : 0xFFFFFFFFull);
+    k.len = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(k.len)));  // uniform (scalar)
     return k;
+}
+
+// The task's staged pieces (np = len / 16 when the range fits the stage)
+// through a buffer resource clamped to the stream's last 16-B granule:
+// unconditional loads (pieces past the range read zero), so they stay in
+// flight while the current task decodes — a bounds-checked load with a
+// byte-wise fallback made the compiler wait for them right after issue.
+template <uint32_t R>
+__device__ __forceinline__ void issue_task_loads(const DecodeArgs& a, const Task& k, uint32_t lane, uint4 (&pre)[R]) {
+    const uint32_t np = k.len <= kInCap ? k.len / 16 : 0u;
+    const uint64_t end16 = (a.comp_bytes + 15) & ~15ull;
+    const uint64_t avail = end16 > k.b0 ? end16 - k.b0 : 0;
+    const uint32_t nb = static_cast<uint32_t>(avail < 16ull * np ? avail : 16ull * np);
+    const auto rs = buf_rsrc(nb ? a.comp + k.b0 : a.comp, nb);
+#pragma unroll
+    for (uint32_t r = 0; r < R; ++r) pre[r] = buf_ld16(rs, (lane + 64 * r) * 16);
 }
 
 // dword sources for the lane decoder (stream order: the first byte is the
@@ -201,14 +211,7 @@ __global__ __launch_bounds__(kThreads) void k_decode_wave(DecodeArgs a) {
     // register staging of the next task's input
     uint4 pre[kLoadRounds];
     Task cur = task_info(a, task, lane);
-    auto issue = [&](const Task& k) {
-        const uint32_t np = k.len <= kInCap ? k.len / 16 : 0u;
-#pragma unroll
-        for (uint32_t r = 0; r < kLoadRounds; ++r) {
-            const uint32_t p = lane + 64 * r;
-            pre[r] = p < np ? load16_guarded(a.comp, a.comp_bytes, k.b0 + 16ull * p) : make_uint4(0, 0, 0, 0);
-        }
-    };
+    auto issue = [&](const Task& k) { issue_task_loads(a, k, lane, pre); };
     issue(cur);
 
     while (true) {
@@ -386,14 +389,7 @@ __device__ __forceinline__ void decode_fixed_body(const DecodeArgs& a) {
 
     uint4 pre[kLoadRounds];
     Task cur = task_info(a, task, lane);
-    auto issue = [&](const Task& k) {
-        const uint32_t np = k.len <= kInCap ? k.len / 16 : 0u;
-#pragma unroll
-        for (uint32_t r = 0; r < kLoadRounds; ++r) {
-            const uint32_t p = lane + 64 * r;
-            pre[r] = p < np ? load16_guarded(a.comp, a.comp_bytes, k.b0 + 16ull * p) : make_uint4(0, 0, 0, 0);
-        }
-    };
+    auto issue = [&](const Task& k) { issue_task_loads(a, k, lane, pre); };
     issue(cur);
 
     while (true) {
