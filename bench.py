@@ -161,24 +161,30 @@ def main():
     # stream order (one host wait per step); gloo rehearsal: host row exchange
     dx = mgpu.DeviceExchange(dev) if world > 1 and args.dist_backend == "nccl" else None
 
-    def step():
-        """pass 1 -> (N>1: one all_gather) -> pass 2 (native: tree, bit base, pack) -> decode"""
+    def encode():
+        """N=1: compress() in one native call (pass 1, tree, pass 2);
+        N>1: pass 1 -> one all_gather -> pass 2 (tree, bit base, pack)"""
+        if world == 1:
+            tree, bits = job.compress(state["out"].data_ptr(), state["cap"])
+            return tree, bits
         if dx is not None:
             hists, tails = dx(job)
-        elif world > 1:
-            hists, tails = mgpu.exchange(job.hist(), x[n - 8:n], device=dev)
         else:
-            hists, tails = job.hist()[None, :], [b""]
+            hists, tails = mgpu.exchange(job.hist(), x[n - 8:n], device=dev)
+        tree, _, bits = job.pack_shards(hists, rank, tails, state["out"].data_ptr(), state["cap"])
+        return tree, bits
+
+    def step():
+        """encode -> block-parallel decode"""
         try:
-            tree, base, bits = job.pack_shards(hists, rank, tails, state["out"].data_ptr(), state["cap"])
+            tree, bits = encode()
         except H.HuffError as e:  # compressed shard larger than the buffer: grow once, redo
             if getattr(e, "bits_needed", None) is None:
                 raise
             state["cap"] = (e.bit_base % 8 + e.bits_needed + 7) // 8 + 128
             state["out"] = torch.empty(state["cap"], dtype=torch.uint8, device="cuda")
-            tree, base, bits = job.pack_shards(hists, rank, tails, state["out"].data_ptr(), state["cap"])
+            tree, bits = encode()
         job.decode(tree, state["out"].data_ptr(), dec.data_ptr())
-        state["hists"] = hists
         return bits, tree
 
     for _ in range(args.warmup):
@@ -217,10 +223,10 @@ def main():
         copy_ms.append(a_ev.elapsed_time(b_ev))
     copy_gbps = 2 * n / (min(copy_ms) * 1e-3) / 1e9
 
-    _, ln = tree.code_table()
-    total = state["hists"].sum(axis=0, dtype=np.uint64)
-    state["fixed8"] = bool((ln[total > 0] == 8).all()) and os.environ.get("HUFF_DISABLE_FIXED8", "0") in ("", "0")
-    maxlen = int(ln[total > 0].max())  # the decode kernel the runtime picks (runtime.cpp, huff_enc::decode)
+    _, ln = tree.code_table()  # letters present in the input are exactly those with a code
+    present = np.asarray(ln) > 0
+    state["fixed8"] = bool((ln[present] == 8).all()) and os.environ.get("HUFF_DISABLE_FIXED8", "0") in ("", "0")
+    maxlen = int(ln[present].max())  # the decode kernel the runtime picks (runtime.cpp, huff_enc::decode)
     state["dec_kernel"] = "k_decode" if maxlen > 32 else "k_decode_fixed"
     ms_per_step = elapsed * 1e3 / args.steps
     value = world * n / (elapsed / args.steps) / 1e9

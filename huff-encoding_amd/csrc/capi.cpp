@@ -408,6 +408,23 @@ int huff_enc_pack_shards(huff_enc* e, const uint64_t* hists, uint32_t world, uin
     });
 }
 
+int huff_enc_compress(huff_enc* e, uint8_t* d_out, size_t out_cap, huff_tree** tree_out, uint64_t* bits_out) {
+    if (!e || !d_out || !tree_out) return fail(HUFF_E_INVALID_ARG, "null argument");
+    if (reinterpret_cast<uintptr_t>(d_out) & 15) return fail(HUFF_E_INVALID_ARG, "d_out must be 16-byte aligned");
+    *tree_out = nullptr;
+    return guarded([&]() -> huff::Status {
+        HUFF_TRY(e->hist());
+        auto t = std::make_unique<huff_tree>();
+        HUFF_TRY(huff::HuffTree::from_weights(huff::ByteWeights::from_counts(e->w), t->t));
+        uint64_t bits = 0;
+        huff::Status st = e->pack(t.get(), 0, nullptr, 0, d_out, out_cap, &bits);
+        if (bits_out) *bits_out = bits;
+        HUFF_TRY(st);
+        *tree_out = t.release();
+        return huff::Status::ok();
+    });
+}
+
 int huff_enc_decode(huff_enc* e, const huff_tree* t, const uint8_t* d_comp, uint8_t* d_out) {
     if (!e || !t || !d_comp || (!d_out && e->n)) return fail(HUFF_E_INVALID_ARG, "null argument");
     return guarded([&] {

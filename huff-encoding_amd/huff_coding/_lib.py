@@ -90,6 +90,7 @@ SIGNATURES = [
     ("huff_enc_bits", i, [vp, vp, u64p]),
     ("huff_enc_pack", i, [vp, vp, C.c_uint64, vp, sz, vp, sz, u64p]),
     ("huff_enc_pack_shards", i, [vp, vp, C.c_uint32, C.c_uint32, vp, vp, vp, sz, C.POINTER(vp), u64p, u64p]),
+    ("huff_enc_compress", i, [vp, vp, sz, C.POINTER(vp), u64p]),
     ("huff_enc_decode", i, [vp, vp, vp, vp]),
     ("huff_dev_decompress", i, [vp, vp, vp, sz, C.c_uint8, vp, sz, szp]),
     ("huff_dev_generate", i, [vp, i, C.c_uint64, C.c_uint64, u64p, vp, sz]),

@@ -97,6 +97,23 @@ class EncodeJob:
             raise
         return HuffTree(tree_h), base.value, bits.value
 
+    def compress(self, d_out: int, out_cap: int):
+        """compress() of the resident buffer in one native call: pass 1, the
+        tree of its weights, pass 2 at bit 0. Returns (HuffTree, bits);
+        HuffError(BUFFER_TOO_SMALL) carries .bits_needed"""
+        from . import HuffError, HuffTree
+
+        tree_h = C.c_void_p()
+        bits = C.c_uint64()
+        rc = load().huff_enc_compress(self.h, C.c_void_p(d_out), out_cap, C.byref(tree_h), C.byref(bits))
+        try:
+            _check(rc)
+        except HuffError as e:
+            e.bits_needed = bits.value
+            e.bit_base = 0
+            raise
+        return HuffTree(tree_h), bits.value
+
     def decode(self, tree, d_comp: int, d_out: int):
         """block-parallel decode of this job's pack output via its restart index"""
         _check(load().huff_enc_decode(self.h, tree.h, C.c_void_p(d_comp), C.c_void_p(d_out)))

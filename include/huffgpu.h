@@ -203,6 +203,12 @@ int huff_enc_pack_shards(huff_enc* e, const uint64_t* hists, uint32_t world, uin
                          const uint8_t* tails, const uint8_t* tail_lens,
                          uint8_t* d_out, size_t out_cap, huff_tree** tree_out,
                          uint64_t* bit_base_out, uint64_t* bits_out);
+/* compress() on a resident buffer in one call (comp.rs:391-397 + the tree of
+ * ByteWeights::from_bytes, weights.rs:265-279): pass 1, the host tree of
+ * the job's weights, pass 2 at bit 0 — no caller code between the passes.
+ * *tree_out receives the tree (free with huff_tree_free); on
+ * HUFF_E_BUFFER_TOO_SMALL *bits_out still holds the bits needed. */
+int huff_enc_compress(huff_enc* e, uint8_t* d_out, size_t out_cap, huff_tree** tree_out, uint64_t* bits_out);
 /* Block-parallel decode of what huff_enc_pack wrote (same job, same tree),
  * using its restart index: d_comp is the pack's d_out, d_out gets n bytes. */
 int huff_enc_decode(huff_enc* e, const huff_tree* t, const uint8_t* d_comp, uint8_t* d_out);

@@ -572,3 +572,36 @@ def test_hist_row_and_device_exchange(H, O, ctx):
             assert torch.equal(dec[:n], x[:n])
     finally:
         dist.destroy_process_group()
+
+
+def test_enc_compress_one_call(H, O, ctx):
+    """huff_enc_compress (pass 1 + tree + pass 2 in one native call) equals
+    the oracle's compress_with_tree(from_weights(from_bytes)) bytes, grows
+    on BUFFER_TOO_SMALL with the bits needed, and round-trips"""
+    import torch
+    from huff_coding import device as D
+
+    for n, kind in [(1, "uniform"), (4097, "zipf"), ((1 << 22) + 77, "text"), ((1 << 22) + 5, "uniform")]:
+        x = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
+        D.generate(ctx, kind, 31 + n, x.data_ptr(), n, cdf=D.zipf_cdf(1.2) if kind == "zipf" else None)
+        host = x[:n].cpu().numpy()
+        job = H.EncodeJob(ctx, x.data_ptr(), n)
+        small = torch.zeros(16, dtype=torch.uint8, device="cuda")
+        if n > 64:
+            with pytest.raises(H.HuffError) as e:
+                job.compress(small.data_ptr(), small.numel())
+            need = (e.value.bits_needed + 7) // 8
+        else:
+            need = n + 16
+        out = torch.zeros(need + 64, dtype=torch.uint8, device="cuda")
+        tree, bits = job.compress(out.data_ptr(), out.numel())
+        torch.cuda.synchronize()
+        ot = O.Tree.from_weights(O.weights_from_array(O.fast_hist(host, 8)))
+        assert tree.as_bin() == ot.as_bin()
+        code, ln = ot.code_table()
+        want, wbits = O.fast_encode(host, code, ln, threads=8)
+        assert bits == wbits and (out[: (bits + 7) // 8].cpu().numpy() == want).all(), (n, kind)
+        dec = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
+        job.decode(tree, out.data_ptr(), dec.data_ptr())
+        torch.cuda.synchronize()
+        assert torch.equal(dec[:n], x[:n])
