@@ -79,7 +79,22 @@ __global__ __launch_bounds__(kThreads) void k_bytemap(BytemapArgs a) {
     }
 }
 
+__global__ __launch_bounds__(256) void k_arith_index(uint64_t n, uint32_t nchunks, uint64_t base_bits,
+                                                     uint64_t* __restrict__ chunk_start, uint32_t* __restrict__ sub_bit) {
+    const uint64_t gid = static_cast<uint64_t>(blockIdx.x) * 256 + threadIdx.x;
+    const uint64_t stride = static_cast<uint64_t>(gridDim.x) * 256;
+    for (uint64_t c = gid; c <= nchunks; c += stride) chunk_start[c] = base_bits + c * kChunk * 8;
+    const uint64_t nsub = (n + kIdx - 1) / kIdx;
+    for (uint64_t g = gid; g < nsub; g += stride) sub_bit[g] = static_cast<uint32_t>(((g * kIdx) % kChunk) * 8);
+}
+
 }  // namespace
+
+hipError_t launch_arith_index(uint64_t n, uint32_t nchunks, uint64_t base_bits, uint64_t* chunk_start,
+                              uint32_t* sub_bit, hipStream_t s) {
+    hipLaunchKernelGGL(k_arith_index, dim3(1024), dim3(256), 0, s, n, nchunks, base_bits, chunk_start, sub_bit);
+    return hipGetLastError();
+}
 
 hipError_t launch_bytemap(const BytemapArgs& a, hipStream_t s) {
     if (a.n == 0 && !a.chunk_start) return hipSuccess;

@@ -113,6 +113,11 @@ struct BytemapArgs {
     uint64_t base_bits;
     uint32_t* sub_bit;            // may be null
 };
+// the arithmetic restart index of an all-8-bit stream (what k_bytemap writes
+// when asked), as its own launch: chunk_start[c] = base_bits + 8 c kChunk,
+// sub_bit[g] = 8 (g kIdx mod kChunk)
+hipError_t launch_arith_index(uint64_t n, uint32_t nchunks, uint64_t base_bits, uint64_t* chunk_start,
+                              uint32_t* sub_bit, hipStream_t s);
 
 // wider letters (wide.hip): W-byte keys, hash-table code lookup
 struct WideArgs {

@@ -434,12 +434,11 @@ huff::Status huff_enc::pack(const huff_tree* t, uint64_t base, const uint8_t* pr
             m.dst = d_out;
             m.n = n;
             for (int b = 0; b < 256; ++b) m.map[b] = static_cast<uint8_t>(et.code[b]);
-            m.chunk_start = static_cast<uint64_t*>(chunk_start.p);
             m.nchunks = nchunks;
             m.base_bits = 0;
-            m.sub_bit = static_cast<uint32_t*>(sub_bit.p);
             HUFF_TRY(ctx->timed("pack", [&] { return huff::dev::launch_bytemap(m, s); }));
             packed = true;
+            index_pending = true;  // arithmetic: written only if a consumer needs it
             packed_tree_id = t->id;
             bit_base = base;
             total_bits = tb;
@@ -479,9 +478,19 @@ huff::Status huff_enc::pack(const huff_tree* t, uint64_t base, const uint8_t* pr
     a.grid = std::max<uint32_t>(1, std::min<uint32_t>((nchunks + wpg - 1) / wpg, ctx->cu_count * per_cu));
     HUFF_TRY(ctx->timed("pack", [&] { return huff::dev::launch_pack(long_codes, a, s); }));
     packed = true;
+    index_pending = false;
     packed_tree_id = t->id;
     bit_base = base;
     total_bits = tb;
+    return huff::Status::ok();
+}
+
+huff::Status huff_enc::ensure_index() {
+    if (!index_pending) return huff::Status::ok();
+    HUFF_TRY(ctx->activate());
+    HIP_TRY(huff::dev::launch_arith_index(n, nchunks, bit_base & 7, static_cast<uint64_t*>(chunk_start.p),
+                                          static_cast<uint32_t*>(sub_bit.p), ctx->stream));
+    index_pending = false;
     return huff::Status::ok();
 }
 
@@ -501,6 +510,7 @@ huff::Status huff_enc::decode(const huff_tree* t, const uint8_t* d_comp, uint64_
         HUFF_TRY(ctx->timed("decode", [&] { return huff::dev::launch_bytemap(m, ctx->stream); }));
         return huff::Status::ok();
     }
+    HUFF_TRY(ensure_index());
     huff::dev::DecodeArgs a{};
     a.comp = d_comp;
     a.comp_bytes = comp_bytes;
@@ -545,6 +555,7 @@ huff::Status huff_enc::decode(const huff_tree* t, const uint8_t* d_comp, uint64_
 }
 
 huff::Status huff_enc::download_index(huff_index_host& idx) {
+    HUFF_TRY(ensure_index());
     idx.n = n;
     idx.chunk_start.resize(nchunks + 1);
     idx.sub_bit.resize((n + huff::dev::kIdx - 1) / huff::dev::kIdx);
@@ -568,6 +579,7 @@ huff::Status huff_enc::upload_index(const huff_index_host& idx) {
                                ctx->stream));
     HUFF_TRY(ctx->sync());
     packed = true;
+    index_pending = false;
     return huff::Status::ok();
 }
 

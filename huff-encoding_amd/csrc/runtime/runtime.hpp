@@ -148,6 +148,10 @@ struct huff_enc {
     bool packed = false;
     uint64_t packed_tree_id = 0;
     uint64_t bit_base = 0, total_bits = 0;
+    // the byte-map pack leaves the (arithmetic) restart index unwritten
+    // until a consumer needs it: decode through a bit decoder, or download
+    bool index_pending = false;
+    huff::Status ensure_index();
 
     huff::Status init(huff_ctx* c, const uint8_t* d, uint64_t nbytes);
     huff::Status hist();

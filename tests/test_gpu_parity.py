@@ -605,3 +605,28 @@ def test_enc_compress_one_call(H, O, ctx):
         job.decode(tree, out.data_ptr(), dec.data_ptr())
         torch.cuda.synchronize()
         assert torch.equal(dec[:n], x[:n])
+
+
+def test_bytemap_pack_then_bit_decoder(H, O, ctx, monkeypatch):
+    """the byte-map pack leaves its arithmetic restart index unwritten; a
+    decode through the bit decoders (fixed-8 disabled after the pack) must
+    write it first and still return the input"""
+    import torch
+    from huff_coding import device as D
+
+    for n in ((1 << 22) + 3, 65536 * 3):
+        x = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
+        D.generate(ctx, "uniform", 91 + n, x.data_ptr(), n)
+        job = H.EncodeJob(ctx, x.data_ptr(), n)
+        out = torch.zeros(n + 128, dtype=torch.uint8, device="cuda")
+        tree, bits = job.compress(out.data_ptr(), out.numel())
+        assert bits == 8 * n
+        monkeypatch.setenv("HUFF_DISABLE_FIXED8", "1")
+        for var in ("10", "1", "7"):
+            monkeypatch.setenv("HUFF_DEC_VARIANT", var)
+            dec = torch.zeros(n + 64, dtype=torch.uint8, device="cuda")
+            job.decode(tree, out.data_ptr(), dec.data_ptr())
+            torch.cuda.synchronize()
+            assert torch.equal(dec[:n], x[:n]), (n, var)
+        monkeypatch.delenv("HUFF_DISABLE_FIXED8")
+        monkeypatch.delenv("HUFF_DEC_VARIANT")
