@@ -60,16 +60,21 @@ __device__ __forceinline__ Task task_info(const DecodeArgs& a, uint64_t t, uint3
     k.nsym = static_cast<uint32_t>(a.n - k.sym0 < kTaskSym ? a.n - k.sym0 : kTaskSym);
     const uint32_t ls = lane * kLaneSym;
     k.cnt = ls >= k.nsym ? 0u : (k.nsym - ls < kLaneSym ? k.nsym - ls : kLaneSym);
-    const uint32_t c = static_cast<uint32_t>(k.sym0 / kChunk);
-    const uint64_t cs = a.chunk_start[c];
-    k.lane_bit = k.cnt ? cs + a.sub_bit[k.sym0 / kIdx + lane] : 0;
+    if (a.sub_abs64) {  // index-free streams: absolute start bit of every 64th symbol (k_mark_lds)
+        k.lane_bit = k.cnt ? a.sub_abs64[k.sym0 / kIdx + lane] : 0;
+    } else {
+        const uint32_t c = static_cast<uint32_t>(k.sym0 / kChunk);
+        k.lane_bit = k.cnt ? a.chunk_start[c] + a.sub_bit[k.sym0 / kIdx + lane] : 0;
+    }
     // readfirstlane returns int: widen through uint32_t (no sign extension)
     const uint32_t f_lo = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(k.lane_bit)));
     const uint32_t f_hi = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(k.lane_bit >> 32)));
     const uint64_t first = (static_cast<uint64_t>(f_hi) << 32) | f_lo;
     const uint64_t next = k.sym0 + kTaskSym;
     uint64_t end;
-    if (next < a.n) {
+    if (a.sub_abs64) {
+        end = next < a.n ? a.sub_abs64[next / kIdx] : a.end_bit;
+    } else if (next < a.n) {
         end = a.chunk_start[next / kChunk] + a.sub_bit[next / kIdx];
     } else {
         end = a.chunk_start[a.nchunks];

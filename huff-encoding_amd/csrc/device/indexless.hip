@@ -191,17 +191,31 @@ struct Staged {
     uint64_t base;  // bit position of w[0]'s most significant bit
 };
 
+// The block's range from its 16-B granule, 8 loads of 16 B per lane in
+// flight per batch through a buffer resource over the range rounded up to
+// its last 16-B granule (pieces past it, incl. the two zero words the lanes'
+// lookahead may read, come back zero): the one-dword-at-a-time loop this
+// replaces waited out a memory latency per dword.
 __device__ Staged stage_block(const IndexlessArgs& a, uint32_t* w) {
     const uint64_t seg0 = static_cast<uint64_t>(blockIdx.x) * kThreads;
     const uint64_t bit_lo = seg0 * a.seg_bits;
     const uint64_t seg_end = seg0 + kThreads < a.nseg ? seg0 + kThreads : a.nseg;
     const uint64_t bit_hi = seg_end * a.seg_bits < a.valid_bits ? seg_end * a.seg_bits : a.valid_bits;
-    const uint64_t byte_lo = (bit_lo >> 3) & ~3ull;
+    const uint64_t byte_lo = (bit_lo >> 3) & ~15ull;
     uint64_t byte_hi = ((bit_hi + 7) >> 3) + 32;
     if (byte_hi > a.comp_bytes) byte_hi = a.comp_bytes;
-    const uint32_t nw = static_cast<uint32_t>((byte_hi - byte_lo + 3) / 4);
-    const uint32_t* src = reinterpret_cast<const uint32_t*>(a.comp + byte_lo);
-    for (uint32_t i = threadIdx.x; i < nw + 2; i += blockDim.x) w[i] = i < nw ? src[i] : 0u;
+    const uint32_t nbytes = static_cast<uint32_t>(byte_hi - byte_lo);
+    const uint32_t np = (nbytes + 8 + 15) / 16;  // + the two zero words
+    const auto rs = buf_rsrc(a.comp + byte_lo, (nbytes + 15) & ~15u);
+    uint4* w4 = reinterpret_cast<uint4*>(w);
+    for (uint32_t p0 = threadIdx.x; p0 < np; p0 += 8 * kThreads) {
+        uint4 v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = buf_ld16(rs, (p0 + k * kThreads) * 16);
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            if (p0 + k * kThreads < np) w4[p0 + k * kThreads] = v[k];
+    }
     return Staged{w, byte_lo * 8};
 }
 
@@ -253,7 +267,7 @@ __global__ __launch_bounds__(kThreads) void k_spec_lds(IndexlessArgs a) {
     const uint32_t K = a.mlut_bits, Ks = a.lut_bits;
     uint32_t* mlut = lds;
     for (uint32_t i = threadIdx.x; i < (1u << K); i += blockDim.x) mlut[i] = a.mlut[i];
-    const Staged st = stage_block(a, mlut + (1u << K));
+    const Staged st = stage_block(a, mlut + (((1u << K) + 3) & ~3u));
     __syncthreads();
     const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
     if (i >= a.nseg) return;
@@ -285,14 +299,15 @@ __global__ __launch_bounds__(kThreads) void k_spec_lds(IndexlessArgs a) {
     a.c[i] = cnt;
 }
 
-// sub_abs[g] = start bit of symbol 256 g, from the settled segments
+// sub_abs[g] = start bit of symbol g << shift, from the settled segments
 __global__ __launch_bounds__(kThreads) void k_mark_lds(IndexlessArgs a, const uint64_t* __restrict__ off,
-                                                       uint64_t* __restrict__ sub_abs) {
+                                                       uint64_t* __restrict__ sub_abs, uint32_t shift) {
+    const uint64_t mask = (1ull << shift) - 1;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const uint32_t K = a.mlut_bits, Ks = a.lut_bits;
     uint32_t* mlut = lds;
     for (uint32_t i = threadIdx.x; i < (1u << K); i += blockDim.x) mlut[i] = a.mlut[i];
-    const Staged st = stage_block(a, mlut + (1u << K));
+    const Staged st = stage_block(a, mlut + (((1u << K) + 3) & ~3u));
     __syncthreads();
     const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
     if (i >= a.nseg) return;
@@ -302,11 +317,11 @@ __global__ __launch_bounds__(kThreads) void k_mark_lds(IndexlessArgs a, const ui
     LaneBits r;
     r.init(st, a.s[i]);
     while (j < jend) {
-        if ((j & 255) == 0) sub_abs[j >> 8] = r.pos;
+        if ((j & mask) == 0) sub_abs[j >> shift] = r.pos;
         r.refill();
         const uint32_t e = mlut[static_cast<uint32_t>(r.buf >> (64 - K))];
         const uint32_t cn = e >> 29;
-        if (!(e & kMsSlow) && (j & 255) + cn <= 256 && j + cn <= jend) {  // no mark inside the entry
+        if (!(e & kMsSlow) && (j & mask) + cn <= mask + 1 && j + cn <= jend) {  // no mark inside the entry
             r.consume((e >> 24) & 31u);
             j += cn;
             continue;
@@ -319,16 +334,17 @@ __global__ __launch_bounds__(kThreads) void k_mark_lds(IndexlessArgs a, const ui
 }  // namespace
 
 static size_t lds_staged_bytes(const IndexlessArgs& a) {
-    return static_cast<size_t>(1u << a.mlut_bits) * 4 + ((kThreads * a.seg_bits + 7) / 8 + 64 + 8 + 3) / 4 * 4;
+    return static_cast<size_t>(((1u << a.mlut_bits) + 3) & ~3u) * 4 + ((kThreads * a.seg_bits + 7) / 8 + 96 + 15) / 16 * 16;
 }
 
 static bool use_staged(const IndexlessArgs& a) { return a.mlut && a.max_len <= 32 && lds_staged_bytes(a) <= 160 * 1024; }
 
-hipError_t launch_indexless_mark(const IndexlessArgs& a, const uint64_t* off, uint64_t* sub_abs, hipStream_t st) {
+hipError_t launch_indexless_mark(const IndexlessArgs& a, const uint64_t* off, uint64_t* sub_abs, uint32_t shift,
+                                 hipStream_t st) {
     if (a.nseg == 0) return hipSuccess;
     if (!use_staged(a)) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_mark_lds, dim3((a.nseg + kThreads - 1) / kThreads), dim3(kThreads), lds_staged_bytes(a), st,
-                       a, off, sub_abs);
+                       a, off, sub_abs, shift);
     return hipGetLastError();
 }
 

@@ -84,6 +84,10 @@ struct DecodeArgs {
     uint32_t cu_count;            // persistent grid of k_decode_wave
     uint64_t n;
     uint8_t* out;
+    // k_decode_fixed on an index-free stream: absolute start bit of every
+    // kIdx-th symbol (instead of chunk_start + sub_bit) and the stream's end
+    const uint64_t* sub_abs64;
+    uint64_t end_bit;
 };
 
 struct IndexlessArgs {
@@ -206,7 +210,10 @@ hipError_t launch_indexless_fix(const IndexlessArgs& a, const uint64_t* xin, uin
 hipError_t launch_indexless_settle(const IndexlessArgs& a, uint64_t* x, hipStream_t s);
 hipError_t launch_indexless_emit(const IndexlessArgs& a, const uint64_t* off, uint8_t* out, hipStream_t s);
 // restart index for the ring decoder: sub_abs[g] = start bit of symbol 256 g
-hipError_t launch_indexless_mark(const IndexlessArgs& a, const uint64_t* off, uint64_t* sub_abs, hipStream_t s);
+// sub_abs[g] = start bit of symbol g << shift (shift 8: the ring/wide
+// decoders' 256-symbol runs; 6: k_decode_fixed's kIdx = 64)
+hipError_t launch_indexless_mark(const IndexlessArgs& a, const uint64_t* off, uint64_t* sub_abs, uint32_t shift,
+                                 hipStream_t s);
 bool indexless_staged(const IndexlessArgs& a);  // k_spec/k_mark LDS variants apply
 hipError_t launch_bytemap(const BytemapArgs& a, hipStream_t s);
 hipError_t launch_find_first(const uint8_t* in, uint64_t n, const uint8_t* missing_mask, unsigned long long* pos,

@@ -745,6 +745,15 @@ Status parse_block_size(const char* s, size_t* out) {
 // ---------------------------------------------------------------------------
 namespace huff {
 
+}  // namespace huff
+
+huff::IndexlessSync& huff_ctx::indexless_ws() {
+    if (!idx_ws) idx_ws = std::make_shared<huff::IndexlessSync>();
+    return *idx_ws;
+}
+
+namespace huff {
+
 Status indexless_sync(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_bytes, uint64_t valid_bits,
                       const huff_tree* t, IndexlessSync& st) {
     const DecTables* dt = st.dt;
@@ -802,10 +811,10 @@ Status indexless_sync(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_bytes,
     return ctx->sync();
 }
 
-Status indexless_mark(huff_ctx* ctx, IndexlessSync& st, DevBuf& sub_abs) {
-    HUFF_TRY(sub_abs.ensure(((st.total + dev::kSub - 1) / dev::kSub) * 8 + 8));
+Status indexless_mark(huff_ctx* ctx, IndexlessSync& st, DevBuf& sub_abs, uint32_t shift) {
+    HUFF_TRY(sub_abs.ensure(((st.total + (1ull << shift) - 1) >> shift) * 8 + 8));
     HIP_TRY(dev::launch_indexless_mark(st.a, static_cast<const uint64_t*>(st.off.p),
-                                       static_cast<uint64_t*>(sub_abs.p), ctx->stream));
+                                       static_cast<uint64_t*>(sub_abs.p), shift, ctx->stream));
     return Status::ok();
 }
 
@@ -840,7 +849,7 @@ Status decode_indexless_dev(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_
         HIP_TRY(dev::launch_bytemap(m, ctx->stream));
         return Status::ok();
     }
-    IndexlessSync st;
+    IndexlessSync& st = ctx->indexless_ws();
     st.dt = dt;
     HUFF_TRY(indexless_sync(ctx, d_comp, comp_bytes, valid_bits, t, st));
     const uint64_t total = st.total;
@@ -849,26 +858,27 @@ Status decode_indexless_dev(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_
     hipStream_t strm = ctx->stream;
     const bool aligned16 = !(reinterpret_cast<uintptr_t>(d_comp) & 15) && !(reinterpret_cast<uintptr_t>(out_at()) & 15);
     if (dev::indexless_staged(st.a) && total && aligned16) {
-        // a restart index for the ring decoder, then the ordinary restart-index decode
-        DevBuf sub_abs;
-        HUFF_TRY(indexless_mark(ctx, st, sub_abs));
+        // a restart point every 64 symbols, then the fixed-count decoder
+        DevBuf& sub_abs = ctx->idx_sub_abs;
+        HUFF_TRY(indexless_mark(ctx, st, sub_abs, 6));
         dev::DecodeArgs d{};
         d.comp = d_comp;
         d.comp_bytes = comp_bytes;
         d.lut = static_cast<const uint32_t*>(ctx->d_lut.p);
         d.lut_bits = dt->bits;
         d.lut_words = static_cast<uint32_t>(dt->lut.size());
-        d.sub_abs = static_cast<const uint64_t*>(sub_abs.p);
+        d.sub_abs64 = static_cast<const uint64_t*>(sub_abs.p);
+        d.end_bit = valid_bits;
         d.nchunks = static_cast<uint32_t>((total + dev::kChunk - 1) / dev::kChunk);
         d.max_len = dt->maxdepth;
-        d.mlut = st.a.mlut;
-        d.mlut_bits = st.a.mlut_bits;
-        d.variant = dev::kDecodeRing;
+        d.stab = reinterpret_cast<const uint16_t*>(static_cast<const uint32_t*>(ctx->d_lut.p) + dt->soff);
+        d.stab_bits = dt->sbits;
+        d.cu_count = static_cast<uint32_t>(ctx->cu_count);
         d.n = total;
         d.out = out_at();
-        HIP_TRY(dev::launch_decode_ring(d, strm));
+        HIP_TRY(dev::launch_decode_fixed(d, strm));
         HIP_TRY(hipEventRecord(ctx->lut_free, strm));
-        return ctx->sync();  // sub_abs is freed on return
+        return Status::ok();
     }
     HIP_TRY(dev::launch_indexless_emit(st.a, static_cast<const uint64_t*>(st.off.p), out_at(), strm));
     HIP_TRY(hipEventRecord(ctx->lut_free, strm));

@@ -104,6 +104,10 @@ struct DevBuf {
     ~DevBuf() { release(); }
 };
 
+namespace huff {
+struct IndexlessSync;
+}
+
 struct huff_ctx {
     int device = 0;
     int cu_count = 256;
@@ -117,6 +121,11 @@ struct huff_ctx {
     PinnedBuf pin_lut;   // decode table upload
     DevBuf d_in, d_out;  // staging of the host-pointer API
     DevBuf d_lut;
+    // index-free decode workspace, kept across calls (per-call allocations
+    // of its ~100 MB per GiB of stream cost more than the kernels)
+    std::shared_ptr<huff::IndexlessSync> idx_ws;
+    DevBuf idx_sub_abs;
+    huff::IndexlessSync& indexless_ws();
     uint64_t lut_tree_id = 0;
 
     // kernel timing
@@ -191,8 +200,8 @@ struct IndexlessSync {
 };
 Status indexless_sync(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_bytes, uint64_t valid_bits,
                       const huff_tree* t, IndexlessSync& st);
-// sub_abs[g] = first bit of symbol 256 g (needs dev::indexless_staged(st.a))
-Status indexless_mark(huff_ctx* ctx, IndexlessSync& st, DevBuf& sub_abs);
+// sub_abs[g] = first bit of symbol g << shift (needs dev::indexless_staged(st.a))
+Status indexless_mark(huff_ctx* ctx, IndexlessSync& st, DevBuf& sub_abs, uint32_t shift = 8);
 Status decode_indexless_host(huff_ctx* ctx, const uint8_t* comp, size_t len, uint64_t valid_bits,
                              const huff_tree* t, std::vector<uint8_t>& out);
 }  // namespace huff

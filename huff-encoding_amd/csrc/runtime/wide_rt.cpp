@@ -290,7 +290,7 @@ Status wdecode_indexless_dev(huff_ctx* ctx, const huff_wtree* t, const uint8_t* 
     const huff_tree* shape = t->shape_tree();
     const DecTables* dt = nullptr;
     HUFF_TRY(ctx->upload_dec_tables(shape, &dt));
-    IndexlessSync st;
+    IndexlessSync& st = ctx->indexless_ws();
     st.dt = dt;
     HUFF_TRY(indexless_sync(ctx, d_comp, comp_bytes, valid_bits, shape, st));
     *n_out = st.total;
@@ -298,13 +298,13 @@ Status wdecode_indexless_dev(huff_ctx* ctx, const huff_wtree* t, const uint8_t* 
     if (st.total > cap_letters) return Status::err(HUFF_E_BUFFER_TOO_SMALL, "output buffer too small");
     if (!dev::indexless_staged(st.a))
         return Status::err(HUFF_E_CODE_TOO_LONG, "index-free decode of letters wider than a byte needs codes <= 32 bits");
-    DevBuf sub_abs;
+    DevBuf& sub_abs = ctx->idx_sub_abs;
     HUFF_TRY(indexless_mark(ctx, st, sub_abs));
     HIP_TRY(hipEventRecord(ctx->lut_free, ctx->stream));
     huff_wenc e;
     HUFF_TRY(e.init(ctx, t->t.width(), nullptr, st.total));
     HUFF_TRY(e.decode(t, d_comp, comp_bytes, d_out, static_cast<const uint64_t*>(sub_abs.p)));
-    return ctx->sync();  // sub_abs is freed on return
+    return ctx->sync();
 }
 
 Status wdecompress_host(huff_ctx* ctx, const huff_wcompress_data* cd, uint8_t* out, size_t cap_letters,
