@@ -88,7 +88,18 @@ struct DecodeArgs {
     // kIdx-th symbol (instead of chunk_start + sub_bit) and the stream's end
     const uint64_t* sub_abs64;
     uint64_t end_bit;
+    // k_decode_fixed: pad the input stage (one 16-B piece per 8) — for mean
+    // code lengths near 4, 8 or 12 bits the lanes' streams start a multiple of
+    // 8 dwords apart and every refill would hit the same few LDS banks
+    uint32_t pad_stage;
 };
+// whether k_decode_fixed should pad its stage for this mean code length
+inline bool fixed_decode_pad(uint64_t bits, uint64_t nsym) {
+    if (nsym == 0) return false;
+    const double stride = 2.0 * static_cast<double>(bits) / static_cast<double>(nsym);  // dwords per 64 symbols
+    const double r = stride - 8.0 * static_cast<double>(static_cast<uint64_t>(stride / 8.0 + 0.5));
+    return stride >= 7.5 && stride <= 24.5 && r > -0.5 && r < 0.5;
+}
 
 struct IndexlessArgs {
     const uint8_t* comp;

@@ -543,6 +543,7 @@ huff::Status huff_enc::decode(const huff_tree* t, const uint8_t* d_comp, uint64_
         (reinterpret_cast<uintptr_t>(d_out) & 15))
         a.variant = (total_bits < 7 * n) ? huff::dev::kDecodeRing : huff::dev::kDecodeSingle;
     a.cu_count = static_cast<uint32_t>(ctx->cu_count);
+    a.pad_stage = huff::dev::fixed_decode_pad(total_bits, n);
     a.mlut = static_cast<const uint32_t*>(ctx->d_lut.p) + dt->moff;
     a.mlut_bits = dt->mbits;
     a.stab = reinterpret_cast<const uint16_t*>(static_cast<const uint32_t*>(ctx->d_lut.p) + dt->soff);
@@ -874,6 +875,7 @@ Status decode_indexless_dev(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_
         d.stab = reinterpret_cast<const uint16_t*>(static_cast<const uint32_t*>(ctx->d_lut.p) + dt->soff);
         d.stab_bits = dt->sbits;
         d.cu_count = static_cast<uint32_t>(ctx->cu_count);
+        d.pad_stage = dev::fixed_decode_pad(valid_bits, total);
         d.n = total;
         d.out = out_at();
         HIP_TRY(dev::launch_decode_fixed(d, strm));
