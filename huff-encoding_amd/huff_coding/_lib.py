@@ -17,6 +17,9 @@ except Exception:  # pragma: no cover - torch is part of the image
 
 _PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.path.join(_PKG, "lib", "libhuffgpu.so")
+# A/B measurements load an alternative in-tree build (e.g. lib/ab/libhuffgpu.so)
+if os.environ.get("HUFF_LIB_AB"):
+    LIB_PATH = os.path.join(_PKG, "lib", os.environ["HUFF_LIB_AB"], "libhuffgpu.so")
 
 HUFF_OK = 0
 E_INVALID_ARG = 1
