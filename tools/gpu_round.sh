@@ -23,6 +23,10 @@ for w in uniform zipf text; do
   timeout -k 10 400 python bench.py --workload $w > "$out/bench_$w.json" 2> "$out/bench_$w.err"
 done
 HUFF_DISABLE_FIXED8=1 timeout -k 10 300 python bench.py --no-cpu-baseline > "$out/bench_uniform_general.json" 2> "$out/bench_uniform_general.err"
+# the per-GPU shard sizes of BASELINE configs[3] (16 GiB / 8) and configs[4] (64 GiB / 8)
+timeout -k 10 300 python bench.py --no-cpu-baseline --bytes-per-gpu $((2<<30)) > "$out/bench_uniform_2GiB.json" 2> "$out/bench_uniform_2GiB.err"
+timeout -k 10 400 python bench.py --no-cpu-baseline --workload text --steps 5 --warmup 2 --bytes-per-gpu $((8<<30)) > "$out/bench_text_8GiB.json" 2> "$out/bench_text_8GiB.err"
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$out/smoke.log" 2>&1
 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
   --master-port 29533 bench.py --gpus 2 --steps 5 --warmup 2 --workload text --bytes-per-gpu $((1<<28)) \
   --dist-backend gloo > "$out/bench_2rank_gloo.json" 2> "$out/bench_2rank_gloo.err"
