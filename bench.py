@@ -248,7 +248,9 @@ def main():
                           "GBps": round(b / (avg * 1e-3) / 1e9, 1)}
     dom = max(kernels, key=lambda k: kernels[k]["avg_ms"])
     ach = kernels[dom]["GBps"]
-    traffic, traffic_src = dominant_traffic(kind, dom, state.get("fixed8"), state.get("dec_kernel"))
+    # the committed PMC summaries are per launch of a 1 GiB job: other sizes get none
+    traffic, traffic_src = (dominant_traffic(kind, dom, state.get("fixed8"), state.get("dec_kernel"))
+                            if n == 1 << 30 else (None, None))
     enc_ms = sum(kernels[k]["avg_ms"] for k in ("hist", "chunk_bits", "scan", "pack") if k in kernels)
     result = {
         "metric": METRIC,
