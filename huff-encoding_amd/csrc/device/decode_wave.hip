@@ -38,8 +38,11 @@ constexpr uint32_t kInCap = 4608;                // input stage bytes per wave (
 // k_decode_fixed's per-wave stage: the task's input, then (after the decode)
 // its 64 output rows of 64 B, padded to 80 B so the row writes
 // (ds_write_b128, 8-lane groups) hit distinct banks
-constexpr uint32_t kRowBytes = 80;
-constexpr uint32_t kFxStage = kInCap * 9 / 8 > 64 * kRowBytes ? kInCap * 9 / 8 : 64 * kRowBytes;  // input padded 1/8
+constexpr uint32_t kRowBytes = 64;  // 16-B pieces XOR-swizzled by (row >> 1) & 3: conflict-free ds_write_b128
+template <bool PAD>
+constexpr uint32_t fx_stage_bytes() { return PAD ? kInCap * 9 / 8 : kInCap; }  // input padded 1/8 when PAD
+static_assert(64 * kRowBytes <= kInCap, "the output rows fit the stage");
+__device__ __forceinline__ uint32_t row_piece(uint32_t row, uint32_t q) { return row * kRowBytes + 16 * (q ^ ((row >> 1) & 3)); }
 constexpr uint32_t kInPieces = kInCap / 16;      // 288 16-B pieces
 constexpr uint32_t kLoadRounds = (kInPieces + 63) / 64;  // 5
 constexpr uint32_t kWaveLds = kInCap + 64 * 4 * kOutWords;
@@ -401,7 +404,7 @@ __device__ __forceinline__ void decode_fixed_body(const DecodeArgs& a) {
     const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
     uint16_t* stab = reinterpret_cast<uint16_t*>(lds);
     const uint32_t tab_words = (nent + 1) / 2;
-    uint4* in_stage = reinterpret_cast<uint4*>(lds + ((tab_words + 3) & ~3u)) + wave * (kFxStage / 16);
+    uint4* in_stage = reinterpret_cast<uint4*>(lds + ((tab_words + 3) & ~3u)) + wave * (fx_stage_bytes<PAD>() / 16);
     for (uint32_t i = t; i < tab_words; i += kThreads) lds[i] = reinterpret_cast<const uint32_t*>(a.stab)[i];
     __syncthreads();
 
@@ -410,12 +413,13 @@ __device__ __forceinline__ void decode_fixed_body(const DecodeArgs& a) {
     uint64_t task = static_cast<uint64_t>(blockIdx.x) * kWaves + wave;
     if (task >= ntasks) return;
 
-    uint4 pre[kLoadRounds];
     Task cur = task_info(a, task, lane);
-    auto issue = [&](const Task& k) { issue_task_loads(a, k, lane, pre); };
-    issue(cur);
 
+    // no software prefetch of the next task: its 20 registers would cost a
+    // wave per SIMD; the other resident waves hide the load latency instead
     while (true) {
+        uint4 pre[kLoadRounds];
+        issue_task_loads(a, cur, lane, pre);
         const uint32_t np = cur.len <= kInCap ? cur.len / 16 : 0u;
 #pragma unroll
         for (uint32_t r = 0; r < kLoadRounds; ++r) {
@@ -427,12 +431,7 @@ __device__ __forceinline__ void decode_fixed_body(const DecodeArgs& a) {
             }
         }
         const uint64_t nxt_task = task + step;
-        Task nxt;
         const bool more = nxt_task < ntasks;
-        if (more) {
-            nxt = task_info(a, nxt_task, lane);
-            issue(nxt);
-        }
         wave_sync();
 
         const uint32_t rel = static_cast<uint32_t>(cur.lane_bit - cur.b0 * 8);
@@ -449,14 +448,14 @@ __device__ __forceinline__ void decode_fixed_body(const DecodeArgs& a) {
             // 4x the L2 write requests and stalled the TA (PMC)
             wave_sync();  // the wave's stage reads are done
             uint8_t* sb = reinterpret_cast<uint8_t*>(in_stage);
-            uint4* row = reinterpret_cast<uint4*>(sb + lane * kRowBytes);
 #pragma unroll
-            for (int q = 0; q < 4; ++q) row[q] = make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
+            for (int q = 0; q < 4; ++q)
+                *reinterpret_cast<uint4*>(sb + row_piece(lane, q)) = make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
             wave_sync();
             uint4* d4 = reinterpret_cast<uint4*>(a.out + cur.sym0) + lane;
 #pragma unroll
             for (int q = 0; q < 4; ++q)
-                d4[64 * q] = *reinterpret_cast<const uint4*>(sb + (16 * q + (lane >> 2)) * kRowBytes + 16 * (lane & 3));
+                d4[64 * q] = *reinterpret_cast<const uint4*>(sb + row_piece(16 * q + (lane >> 2), lane & 3));
         } else if (cur.cnt) {
             uint32_t o[16];
             decode_fixed64_stage<SLOW, PAD>(in_stage, rel, o, stab, K, a.lut,
@@ -474,7 +473,7 @@ __device__ __forceinline__ void decode_fixed_body(const DecodeArgs& a) {
         if (!more) break;
         wave_sync();  // the input stage is reused by the next task
         task = nxt_task;
-        cur = nxt;
+        cur = task_info(a, task, lane);
     }
 }
 
@@ -513,14 +512,14 @@ hipError_t launch_decode_wave(const DecodeArgs& a, hipStream_t s) {
 
 namespace huff::dev {
 
-size_t decode_fixed_lds_bytes(uint32_t stab_bits) {
+size_t decode_fixed_lds_bytes(uint32_t stab_bits, bool pad) {
     const size_t tab_words = ((1u << stab_bits) + 1) / 2;
-    return ((tab_words + 3) & ~size_t(3)) * 4 + static_cast<size_t>(kWaves) * kFxStage;
+    return ((tab_words + 3) & ~size_t(3)) * 4 + static_cast<size_t>(kWaves) * (pad ? fx_stage_bytes<true>() : fx_stage_bytes<false>());
 }
 
 hipError_t launch_decode_fixed(const DecodeArgs& a, hipStream_t s) {
     if (a.n == 0) return hipSuccess;
-    const size_t lds = decode_fixed_lds_bytes(a.stab_bits);
+    const size_t lds = decode_fixed_lds_bytes(a.stab_bits, a.pad_stage != 0);
     const uint64_t ntasks = (a.n + kTaskSym - 1) / kTaskSym;
     const bool slow = a.max_len > a.stab_bits;
     // persistent grid = resident workgroups (registers and LDS both limit)
