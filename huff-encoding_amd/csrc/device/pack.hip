@@ -167,7 +167,11 @@ __global__ __launch_bounds__(pack_waves<LONG>() * 64) void k_pack(PackArgs a) {
     using T = typename E::T;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     T* tab = reinterpret_cast<T*>(lds);
-    const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6, copy = t & 31;
+    // the wave index read into an SGPR: the chunk, its buffer resource and
+    // the round bounds are then scalar (a VGPR resource made every buffer load
+    // a waterfall loop)
+    const uint32_t t = threadIdx.x, lane = t & 63, copy = t & 31;
+    const uint32_t wave = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(t >> 6)));
     uint32_t* stage = lds + E::kTableWords + wave * a.stage_words;
 
     // replicate the table: thread t writes copy t%32 of letters t/32 + 8i
@@ -252,12 +256,19 @@ __global__ __launch_bounds__(pack_waves<LONG>() * 64) void k_pack(PackArgs a) {
                 wv[4 * q + 3] = v.v[q].w;
             }
             T ent[kBPL];
+            if ((r + 1ull) * kPackWaveRound <= nsym) {  // whole round (wave-uniform): no per-letter masks
 #pragma unroll
-            for (int k = 0; k < static_cast<int>(kBPL); ++k) {
-                const uint32_t b = (wv[k >> 2] >> (8 * (k & 3))) & 0xFFu;
-                ent[k] = (k < nvalid) ? tab[(b << 5) | copy] : T(0);
-                bits += static_cast<uint32_t>(ent[k] & E::kMask);
+                for (int k = 0; k < static_cast<int>(kBPL); ++k)
+                    ent[k] = tab[(((wv[k >> 2] >> (8 * (k & 3))) & 0xFFu) << 5) | copy];
+            } else {
+#pragma unroll
+                for (int k = 0; k < static_cast<int>(kBPL); ++k) {
+                    const uint32_t b = (wv[k >> 2] >> (8 * (k & 3))) & 0xFFu;
+                    ent[k] = (k < nvalid) ? tab[(b << 5) | copy] : T(0);
+                }
             }
+#pragma unroll
+            for (int k = 0; k < static_cast<int>(kBPL); ++k) bits += static_cast<uint32_t>(ent[k] & E::kMask);
             // wave exclusive scan of the bit counts
             const uint32_t incl = wave_scan_incl(bits);
             const uint32_t tot = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(incl), 63));
