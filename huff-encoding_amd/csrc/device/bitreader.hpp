@@ -36,6 +36,12 @@ __device__ __forceinline__ uint4 ld_nt(const uint4* p) {
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* p, uint32_t bytes) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, static_cast<int>(bytes), 0x00020000);
 }
+// the wave's index in its workgroup, in an SGPR: values derived from it (the
+// wave's chunk or task, a buffer resource over its range) stay scalar; from a
+// VGPR every buffer load over such a resource compiles to a waterfall loop
+__device__ __forceinline__ uint32_t wave_index() {
+    return static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6)));
+}
 // 16-byte buffer load; AUX 2 = nontemporal
 template <int AUX = 0>
 __device__ __forceinline__ uint4 buf_ld16(__amdgpu_buffer_rsrc_t r, uint32_t off) {

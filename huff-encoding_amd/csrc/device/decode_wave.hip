@@ -36,8 +36,7 @@ constexpr uint32_t kTaskSym = 64 * kLaneSym;     // 4,096 symbols per wave task
 constexpr uint32_t kOutWords = kLaneSym / 4 + 2; // output dwords per lane (64 letters + overshoot)
 constexpr uint32_t kInCap = 4608;                // input stage bytes per wave (9 bits per symbol)
 // k_decode_fixed's per-wave stage: the task's input, then (after the decode)
-// its 64 output rows of 64 B, padded to 80 B so the row writes
-// (ds_write_b128, 8-lane groups) hit distinct banks
+// its 64 output rows of 64 B
 constexpr uint32_t kRowBytes = 64;  // 16-B pieces XOR-swizzled by (row >> 1) & 3: conflict-free ds_write_b128
 template <bool PAD>
 constexpr uint32_t fx_stage_bytes() { return PAD ? kInCap * 9 / 8 : kInCap; }  // input padded 1/8 when PAD
@@ -211,7 +210,7 @@ __global__ __launch_bounds__(kThreads) void k_decode_wave(DecodeArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const uint32_t K = a.mlut_bits;
     const uint32_t nent = 1u << K;
-    const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const uint32_t t = threadIdx.x, lane = t & 63, wave = wave_index();
     uint32_t* mlut = lds;
     uint8_t* wbase = reinterpret_cast<uint8_t*>(lds + nent) + wave * kWaveLds;
     uint4* in_stage = reinterpret_cast<uint4*>(wbase);
@@ -401,7 +400,7 @@ __device__ __forceinline__ void decode_fixed_body(const DecodeArgs& a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const uint32_t K = a.stab_bits;
     const uint32_t nent = 1u << K;
-    const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const uint32_t t = threadIdx.x, lane = t & 63, wave = wave_index();
     uint16_t* stab = reinterpret_cast<uint16_t*>(lds);
     const uint32_t tab_words = (nent + 1) / 2;
     uint4* in_stage = reinterpret_cast<uint4*>(lds + ((tab_words + 3) & ~3u)) + wave * (fx_stage_bytes<PAD>() / 16);

@@ -167,11 +167,8 @@ __global__ __launch_bounds__(pack_waves<LONG>() * 64) void k_pack(PackArgs a) {
     using T = typename E::T;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     T* tab = reinterpret_cast<T*>(lds);
-    // the wave index read into an SGPR: the chunk, its buffer resource and
-    // the round bounds are then scalar (a VGPR resource made every buffer load
-    // a waterfall loop)
-    const uint32_t t = threadIdx.x, lane = t & 63, copy = t & 31;
-    const uint32_t wave = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(t >> 6)));
+    // wave_index(): the chunk, its buffer resource and the round bounds are scalar
+    const uint32_t t = threadIdx.x, lane = t & 63, copy = t & 31, wave = wave_index();
     uint32_t* stage = lds + E::kTableWords + wave * a.stage_words;
 
     // replicate the table: thread t writes copy t%32 of letters t/32 + 8i

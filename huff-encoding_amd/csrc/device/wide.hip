@@ -201,7 +201,7 @@ __device__ __forceinline__ void wbits_chunk(const WideArgs& a, const KeyStore<T>
     }
     if (miss != ~0ull) atomicMin(a.first_missing, static_cast<unsigned long long>(miss));
     // exclusive scan of the 256 runs' bit counts
-    const uint32_t lane = t & 63, wave = t >> 6;
+    const uint32_t lane = t & 63, wave = wave_index();
     const uint32_t incl = wave_scan_incl(bits);
     if (lane == 63) wsum[wave] = incl;
     __syncthreads();
