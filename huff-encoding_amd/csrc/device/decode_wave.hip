@@ -22,6 +22,7 @@
 // Roofline: HBM-bound; algorithmic traffic ceil(bits/8) (read) + n (write)
 // + 4 B per 64 symbols of index.
 #include <algorithm>
+#include <cstdlib>
 
 #include "bitreader.hpp"
 
@@ -54,6 +55,7 @@ struct Task {
     uint32_t cnt;       // this lane's symbols
     uint64_t b0;        // first staged byte (16-B aligned)
     uint32_t len;       // staged bytes
+    uint64_t end;       // the task's end bit (= the next task's first bit)
 };
 
 __device__ __forceinline__ Task task_info(const DecodeArgs& a, uint64_t t, uint32_t lane) {
@@ -81,6 +83,7 @@ __device__ __forceinline__ Task task_info(const DecodeArgs& a, uint64_t t, uint3
     } else {
         end = a.chunk_start[a.nchunks];
     }
+    k.end = end;
     k.b0 = (first >> 3) & ~15ull;
     uint64_t b1 = ((end + 7) >> 3) + 32;  // lookahead: window + the dword read ahead
     b1 = (b1 + 15) & ~15ull;
@@ -90,15 +93,18 @@ __device__ __forceinline__ Task task_info(const DecodeArgs& a, uint64_t t, uint3
 }
 
 // The task's staged pieces (np = len / 16 when the range fits the stage)
-// through a buffer resource clamped to the stream's last 16-B granule:
+// through a buffer resource clamped to the stream's last dword:
 // unconditional loads (pieces past the range read zero), so they stay in
 // flight while the current task decodes — a bounds-checked load with a
 // byte-wise fallback made the compiler wait for them right after issue.
 template <uint32_t R>
 __device__ __forceinline__ void issue_task_loads(const DecodeArgs& a, const Task& k, uint32_t lane, uint4 (&pre)[R]) {
     const uint32_t np = k.len <= kInCap ? k.len / 16 : 0u;
-    const uint64_t end16 = (a.comp_bytes + 15) & ~15ull;
-    const uint64_t avail = end16 > k.b0 ? end16 - k.b0 : 0;
+    // the stream is only 4-B aligned: the readable range ends at the dword
+    // holding its last byte (the buffer range check is per dword, so a 16-B
+    // piece straddling the end returns its readable dwords and zeros)
+    const uint64_t end4 = (a.comp_bytes + 3) & ~3ull;
+    const uint64_t avail = end4 > k.b0 ? end4 - k.b0 : 0;
     const uint32_t nb = static_cast<uint32_t>(avail < 16ull * np ? avail : 16ull * np);
     const auto rs = buf_rsrc(nb ? a.comp + k.b0 : a.comp, nb);
 #pragma unroll
@@ -300,10 +306,12 @@ __global__ __launch_bounds__(kThreads) void k_decode_wave(DecodeArgs a) {
 
 // nb (valid window bits) lives in the low 6 bits of X; the bits above are
 // don't-care (X -= entry borrows only from them)
+// Invariant: the window's valid bits end at stream bit 32 rp, so the lane's
+// position after its 64 letters is 32 rp - nb (*end_rel, for the self-check).
 template <bool SLOW, class Words>
 __device__ __forceinline__ void decode_fixed64(const Words& src, uint32_t rel, uint32_t (&o)[16],
                                                const uint16_t* __restrict__ stab, uint32_t K,
-                                               const uint32_t* __restrict__ glut, uint32_t Ks) {
+                                               const uint32_t* __restrict__ glut, uint32_t Ks, uint32_t* end_rel) {
     uint32_t rp = rel >> 5;
     const uint32_t sh = rel & 31;
     uint64_t buf = static_cast<uint64_t>(src(rp) << sh) << 32;
@@ -351,25 +359,27 @@ __device__ __forceinline__ void decode_fixed64(const Words& src, uint32_t rel, u
         FX_LOOKUP(i);
         FX_LOOKUP(i + 1);
     }
+    *end_rel = 32 * rp - (X & 63u);
 #undef FX_LOOKUP
 #undef FX_REFILL
 }
 
 template <bool SLOW, bool PAD>
-__device__ __forceinline__ void decode_fixed64_stage(const uint4* in_stage, uint32_t rel, uint32_t (&o)[16],
+__device__ __forceinline__ void decode_fixed64_stage(const uint32_t* stage, uint32_t rel, uint32_t (&o)[16],
                                                      const uint16_t* __restrict__ stab, uint32_t K,
-                                                     const uint32_t* __restrict__ glut, uint32_t Ks) {
+                                                     const uint32_t* __restrict__ glut, uint32_t Ks,
+                                                     uint32_t* end_rel) {
     if constexpr (PAD)
-        decode_fixed64<SLOW>(PaddedLdsWords{reinterpret_cast<const uint32_t*>(in_stage)}, rel, o, stab, K, glut, Ks);
+        decode_fixed64<SLOW>(PaddedLdsWords{stage}, rel, o, stab, K, glut, Ks, end_rel);
     else
-        decode_fixed64<SLOW>(LdsWords{reinterpret_cast<const uint32_t*>(in_stage)}, rel, o, stab, K, glut, Ks);
+        decode_fixed64<SLOW>(LdsWords{stage}, rel, o, stab, K, glut, Ks, end_rel);
 }
 
 // fallback for a task whose compressed range exceeds the stage: a compact
 // loop straight from global memory, one letter per lookup stored as a byte
 template <class Words>
-__device__ __forceinline__ void decode_fixed_global(const Words& src, uint32_t rel, uint32_t cnt, uint8_t* dst,
-                                                 const uint32_t* __restrict__ glut, uint32_t Ks) {
+__device__ __forceinline__ uint32_t decode_fixed_global(const Words& src, uint32_t rel, uint32_t cnt, uint8_t* dst,
+                                                     const uint32_t* __restrict__ glut, uint32_t Ks) {
     uint32_t rp = rel >> 5;
     const uint32_t sh = rel & 31;
     uint64_t buf = ((static_cast<uint64_t>(src(rp)) << 32) | src(rp + 1)) << sh;
@@ -393,17 +403,66 @@ __device__ __forceinline__ void decode_fixed_global(const Words& src, uint32_t r
         nb -= l1;
         dst[j] = static_cast<uint8_t>(e1);
     }
+    return 32 * rp - nb;  // end position (valid bits end at 32 rp)
 }
 
-template <bool SLOW, bool PAD>
+// 16-B LDS stage accesses: one may_alias vector type for every 16-B write
+// and read of the stage, which the lane decoders also read as dwords
+typedef uint32_t u32x4_alias __attribute__((ext_vector_type(4), may_alias));
+__device__ __forceinline__ void st_stage16(void* p, uint4 v) {
+    *reinterpret_cast<u32x4_alias*>(p) = u32x4_alias{v.x, v.y, v.z, v.w};
+}
+__device__ __forceinline__ uint4 ld_stage16(const void* p) {
+    const u32x4_alias v = *reinterpret_cast<const u32x4_alias*>(p);
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+// Self-check (CHECK builds: HUFF_DEC_VARIANT 11-13): every lane's letters
+// must end exactly where the next lane's restart entry (or, for the task's
+// last lane, the next task's first bit) begins. A mismatch is counted in
+// err[0]; the first one records (task, lane, expected, got) in err[1..6]. No
+// trap and no device printf (a call would change the body's register
+// allocation): the kernel drains and the host reports HUFF_E_CORRUPT.
+__device__ __forceinline__ void fx_report(uint32_t* err, uint64_t task, uint32_t lane, uint64_t want, uint64_t got) {
+    if (atomicAdd(err, 1u) == 0) {
+        err[1] = static_cast<uint32_t>(task);
+        err[2] = lane;
+        err[3] = static_cast<uint32_t>(want);
+        err[4] = static_cast<uint32_t>(want >> 32);
+        err[5] = static_cast<uint32_t>(got);
+        err[6] = static_cast<uint32_t>(got >> 32);
+    }
+}
+template <bool CHECK>
+__device__ __forceinline__ void fx_check(const DecodeArgs& a, const Task& k, uint64_t task, uint32_t lane,
+                                         uint64_t got_abs, bool active) {
+    if constexpr (CHECK) {
+        const uint32_t nlo = static_cast<uint32_t>(__shfl_down(static_cast<int>(k.lane_bit), 1));
+        const uint32_t nhi = static_cast<uint32_t>(__shfl_down(static_cast<int>(k.lane_bit >> 32), 1));
+        const uint32_t ncnt = static_cast<uint32_t>(__shfl_down(static_cast<int>(k.cnt), 1));
+        const uint64_t want = (lane < 63 && ncnt) ? ((static_cast<uint64_t>(nhi) << 32) | nlo) : k.end;
+        if (active && got_abs != want) fx_report(a.err, task, lane, want, got_abs);
+    }
+}
+
+template <bool SLOW, bool PAD, bool CHECK, bool CANARY = false>
 __device__ __forceinline__ void decode_fixed_body(const DecodeArgs& a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    // diagnostics (k_decode_fixed_w5): a private array that lives in scratch,
+    // filled at entry and verified after every task
+    volatile uint32_t canary[CANARY ? 16 : 1];
+    const uint32_t ctag = (blockIdx.x << 8) | threadIdx.x;
+    if constexpr (CANARY)
+        for (int i = 0; i < 16; ++i) canary[(i * 5 + (a.n & 1)) & 15] = ctag * 2654435761u + i;
     const uint32_t K = a.stab_bits;
     const uint32_t nent = 1u << K;
     const uint32_t t = threadIdx.x, lane = t & 63, wave = wave_index();
     uint16_t* stab = reinterpret_cast<uint16_t*>(lds);
     const uint32_t tab_words = (nent + 1) / 2;
-    uint4* in_stage = reinterpret_cast<uint4*>(lds + ((tab_words + 3) & ~3u)) + wave * (fx_stage_bytes<PAD>() / 16);
+    // the wave's stage: dword view for the lane decoders, byte view for the
+    // 16-B pieces (all 16-B accesses through u32x4_alias)
+    uint32_t* stage = lds + ((tab_words + 3) & ~3u) + wave * (fx_stage_bytes<PAD>() / 4);
+    uint8_t* sb = reinterpret_cast<uint8_t*>(stage);
     for (uint32_t i = t; i < tab_words; i += kThreads) lds[i] = reinterpret_cast<const uint32_t*>(a.stab)[i];
     __syncthreads();
 
@@ -415,7 +474,11 @@ __device__ __forceinline__ void decode_fixed_body(const DecodeArgs& a) {
     Task cur = task_info(a, task, lane);
 
     // no software prefetch of the next task: its 20 registers would cost a
-    // wave per SIMD; the other resident waves hide the load latency instead
+    // wave per SIMD; the other resident waves hide the load latency instead.
+    // Stage ordering within the wave (no workgroup barrier: a wave's LDS ops
+    // execute in issue order, wave_sync() = lgkmcnt(0) + a compiler barrier):
+    //   stage writes (input) -> sync -> lane reads -> sync -> row writes
+    //   (output transpose) -> sync -> row reads -> sync -> next task's writes
     while (true) {
         uint4 pre[kLoadRounds];
         issue_task_loads(a, cur, lane, pre);
@@ -425,8 +488,9 @@ __device__ __forceinline__ void decode_fixed_body(const DecodeArgs& a) {
             const uint32_t p = lane + 64 * r;
             if (p < np) {
                 const uint4 v = pre[r];
-                in_stage[PAD ? padded_piece(p) : p] = make_uint4(__builtin_bswap32(v.x), __builtin_bswap32(v.y), __builtin_bswap32(v.z),
-                                         __builtin_bswap32(v.w));
+                st_stage16(sb + 16 * (PAD ? padded_piece(p) : p),
+                           make_uint4(__builtin_bswap32(v.x), __builtin_bswap32(v.y), __builtin_bswap32(v.z),
+                                      __builtin_bswap32(v.w)));
             }
         }
         const uint64_t nxt_task = task + step;
@@ -436,29 +500,32 @@ __device__ __forceinline__ void decode_fixed_body(const DecodeArgs& a) {
         const uint32_t rel = static_cast<uint32_t>(cur.lane_bit - cur.b0 * 8);
         uint8_t* dst = a.out + cur.sym0 + lane * kLaneSym;
         if (cur.len > kInCap) {
-            if (cur.cnt) decode_fixed_global(GlobalWords{a.comp, a.comp_bytes, cur.b0 / 4}, rel, cur.cnt, dst, a.lut,
-                                             a.lut_bits);
+            uint32_t e = 0;
+            if (cur.cnt) e = decode_fixed_global(GlobalWords{a.comp, a.comp_bytes, cur.b0 / 4}, rel, cur.cnt, dst,
+                                                 a.lut, a.lut_bits);
+            fx_check<CHECK>(a, cur, task, lane, cur.b0 * 8 + e, cur.cnt != 0);
         } else if (cur.nsym == kTaskSym) {  // wave-uniform: every lane has 64 letters
             uint32_t o[16];
-            decode_fixed64_stage<SLOW, PAD>(in_stage, rel, o, stab, K, a.lut,
-                                 a.lut_bits);
+            uint32_t e = 0;
+            decode_fixed64_stage<SLOW, PAD>(stage, rel, o, stab, K, a.lut, a.lut_bits, &e);
+            fx_check<CHECK>(a, cur, task, lane, cur.b0 * 8 + e, true);
             // transpose through the stage so every store instruction writes
             // 1 KiB contiguous (16 B per lane): lane-strided 16-B pieces cost
             // 4x the L2 write requests and stalled the TA (PMC)
             wave_sync();  // the wave's stage reads are done
-            uint8_t* sb = reinterpret_cast<uint8_t*>(in_stage);
 #pragma unroll
             for (int q = 0; q < 4; ++q)
-                *reinterpret_cast<uint4*>(sb + row_piece(lane, q)) = make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
+                st_stage16(sb + row_piece(lane, q), make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]));
             wave_sync();
             uint4* d4 = reinterpret_cast<uint4*>(a.out + cur.sym0) + lane;
 #pragma unroll
-            for (int q = 0; q < 4; ++q)
-                d4[64 * q] = *reinterpret_cast<const uint4*>(sb + row_piece(16 * q + (lane >> 2), lane & 3));
+            for (int q = 0; q < 4; ++q) d4[64 * q] = ld_stage16(sb + row_piece(16 * q + (lane >> 2), lane & 3));
         } else if (cur.cnt) {
             uint32_t o[16];
-            decode_fixed64_stage<SLOW, PAD>(in_stage, rel, o, stab, K, a.lut,
-                                 a.lut_bits);
+            uint32_t e = 0;
+            decode_fixed64_stage<SLOW, PAD>(stage, rel, o, stab, K, a.lut, a.lut_bits, &e);
+            // a lane with fewer than 64 letters decodes past its end: only full lanes are checked
+            fx_check<CHECK>(a, cur, task, lane, cur.b0 * 8 + e, cur.cnt == kLaneSym);
             if (cur.cnt == kLaneSym) {
                 uint4* d4 = reinterpret_cast<uint4*>(dst);
 #pragma unroll
@@ -468,6 +535,13 @@ __device__ __forceinline__ void decode_fixed_body(const DecodeArgs& a) {
                 for (uint32_t i = 0; i < kLaneSym; ++i)
                     if (i < cur.cnt) dst[i] = static_cast<uint8_t>(o[i >> 2] >> (8 * (i & 3)));
             }
+        } else {
+            fx_check<CHECK>(a, cur, task, lane, 0, false);  // keeps the shuffles wave-uniform
+        }
+        if constexpr (CANARY) {
+            uint32_t nbad = 0;
+            for (int i = 0; i < 16; ++i) nbad += canary[(i * 5 + (a.n & 1)) & 15] != ctag * 2654435761u + i;
+            if (nbad) atomicAdd(a.err + 7, nbad);
         }
         if (!more) break;
         wave_sync();  // the input stage is reused by the next task
@@ -476,16 +550,35 @@ __device__ __forceinline__ void decode_fixed_body(const DecodeArgs& a) {
     }
 }
 
-// The compiler's register allocation (~100 VGPRs, 4 waves per SIMD). Forcing
-// 5 waves per SIMD (amdgpu_waves_per_eu(5, 8)) together with the transposed
-// output stage decoded wrong letters in some tasks of co-resident workgroups
-// on the GPU (root cause not found; GPU tests catch it), so it is not forced.
+// Production kernels: the compiler's register allocation (k_decode_fixed 63
+// VGPRs / 8 waves per SIMD; the padded and slow variants 93-112 / 4-5 waves).
 template <bool PAD>
 __global__ __launch_bounds__(kThreads) void k_decode_fixed(DecodeArgs a) {
-    decode_fixed_body<false, PAD>(a);
+    decode_fixed_body<false, PAD, false>(a);
 }
 template <bool PAD>
-__global__ __launch_bounds__(kThreads) void k_decode_fixed_slow(DecodeArgs a) { decode_fixed_body<true, PAD>(a); }
+__global__ __launch_bounds__(kThreads) void k_decode_fixed_slow(DecodeArgs a) { decode_fixed_body<true, PAD, false>(a); }
+
+// Self-checking builds of the same body (HUFF_DEC_VARIANT): 11 = the
+// compiler's allocation; 12 = forced to >= 5 waves per SIMD (the occupancy a
+// round-1 experiment reported wrong letters at); 13 = 8 waves per SIMD (at
+// most 64 VGPRs), so the body spills more to scratch. They exist to prove the decoder's correctness
+// does not depend on register allocation or occupancy (tests/test_gpu_decode_check.py).
+template <bool SLOW, bool PAD>
+__global__ __launch_bounds__(kThreads) void k_decode_fixed_chk(DecodeArgs a) { decode_fixed_body<SLOW, PAD, true>(a); }
+template <bool SLOW, bool PAD>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(5, 8))) void k_decode_fixed_chk5(DecodeArgs a) {
+    decode_fixed_body<SLOW, PAD, true>(a);
+}
+template <bool SLOW, bool PAD>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_decode_fixed_chk_spill(DecodeArgs a) {
+    decode_fixed_body<SLOW, PAD, true>(a);
+}
+// diagnostics: the production body (no check) forced to >= 5 waves per SIMD
+template <bool SLOW, bool PAD>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(5, 8))) void k_decode_fixed_w5(DecodeArgs a) {
+    decode_fixed_body<SLOW, PAD, false, true>(a);
+}
 
 }  // namespace
 
@@ -521,15 +614,31 @@ hipError_t launch_decode_fixed(const DecodeArgs& a, hipStream_t s) {
     const size_t lds = decode_fixed_lds_bytes(a.stab_bits, a.pad_stage != 0);
     const uint64_t ntasks = (a.n + kTaskSym - 1) / kTaskSym;
     const bool slow = a.max_len > a.stab_bits;
+    const bool pad = a.pad_stage != 0;
+    using K = void (*)(DecodeArgs);
+    // [check mode][slow][pad]
+    static const K table[5][2][2] = {
+        {{k_decode_fixed<false>, k_decode_fixed<true>}, {k_decode_fixed_slow<false>, k_decode_fixed_slow<true>}},
+        {{k_decode_fixed_chk<false, false>, k_decode_fixed_chk<false, true>},
+         {k_decode_fixed_chk<true, false>, k_decode_fixed_chk<true, true>}},
+        {{k_decode_fixed_chk5<false, false>, k_decode_fixed_chk5<false, true>},
+         {k_decode_fixed_chk5<true, false>, k_decode_fixed_chk5<true, true>}},
+        {{k_decode_fixed_chk_spill<false, false>, k_decode_fixed_chk_spill<false, true>},
+         {k_decode_fixed_chk_spill<true, false>, k_decode_fixed_chk_spill<true, true>}},
+        {{k_decode_fixed_w5<false, false>, k_decode_fixed_w5<false, true>},
+         {k_decode_fixed_w5<true, false>, k_decode_fixed_w5<true, true>}},
+    };
+    if (a.check_mode > 4 || (a.check_mode && !a.err)) return hipErrorInvalidValue;
+    K kern = table[a.check_mode][slow][pad];
     // persistent grid = resident workgroups (registers and LDS both limit)
     int per_cu = 0;
-    auto* kern = slow ? (a.pad_stage ? k_decode_fixed_slow<true> : k_decode_fixed_slow<false>)
-                      : (a.pad_stage ? k_decode_fixed<true> : k_decode_fixed<false>);
     hipError_t err = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kThreads, lds);
     if (err != hipSuccess || per_cu < 1) per_cu = 1;
+    if (a.check_mode)  // diagnostics of the check builds: HUFF_DEC_GRID caps the persistent grid
+        if (const char* g = std::getenv("HUFF_DEC_GRID")) per_cu = -std::max(1, std::atoi(g));
     const uint64_t want = (ntasks + kWaves - 1) / kWaves;
-    const uint32_t grid = static_cast<uint32_t>(
-        std::max<uint64_t>(1, std::min<uint64_t>(want, uint64_t(a.cu_count ? a.cu_count : 256) * per_cu)));
+    const uint64_t cap = per_cu < 0 ? uint64_t(-per_cu) : uint64_t(a.cu_count ? a.cu_count : 256) * per_cu;
+    const uint32_t grid = static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>(want, cap)));
     hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), lds, s, a);
     return hipGetLastError();
 }

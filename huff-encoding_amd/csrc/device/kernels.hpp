@@ -92,6 +92,11 @@ struct DecodeArgs {
     // code lengths near 4, 8 or 12 bits the lanes' streams start a multiple of
     // 8 dwords apart and every refill would hit the same few LDS banks
     uint32_t pad_stage;
+    // k_decode_fixed self-check builds (0: production kernel; 1: checked;
+    // 2: checked, >= 5 waves per SIMD forced; 3: checked, 8 waves per
+    // SIMD forced). err: u32[8] mismatch count + first (task, lane, want, got)
+    uint32_t check_mode;
+    uint32_t* err;
 };
 // whether k_decode_fixed should pad its stage for this mean code length
 inline bool fixed_decode_pad(uint64_t bits, uint64_t nsym) {
@@ -187,6 +192,9 @@ constexpr uint32_t kDecodeSingle = 1;  // decode.hip k_decode_short
 constexpr uint32_t kDecodeRing = 7;    // decode_ring.hip k_decode_ring
 constexpr uint32_t kDecodeWave = 9;    // decode_wave.hip k_decode_wave (codes <= 32 bits)
 constexpr uint32_t kDecodeFixed = 10;  // decode_wave.hip k_decode_fixed (codes <= 32 bits)
+constexpr uint32_t kDecodeFixedCheck = 11;       // k_decode_fixed with the lane-end self-check
+constexpr uint32_t kDecodeFixedCheck5 = 12;      //  ... forced to >= 5 waves per SIMD
+constexpr uint32_t kDecodeFixedCheckSpill = 13;  //  ... forced to 8 waves per SIMD (spills)
 
 // Pass 1's totals straight to pinned host memory (device-visible pointer):
 // host[b] = (tag << 48) | total_b. host == nullptr: the totals stay in gw.

@@ -51,6 +51,38 @@ bool fixed8_disabled() {
     return e && *e && *e != '0';
 }
 
+uint32_t decode_check_mode() {
+    const char* e = std::getenv("HUFF_DEC_VARIANT");  // read per call: tests flip it
+    if (!e) return 0;
+    const int v = std::atoi(e);
+    if (v == static_cast<int>(dev::kDecodeFixedCheck)) return 1;
+    if (v == static_cast<int>(dev::kDecodeFixedCheck5)) return 2;
+    if (v == static_cast<int>(dev::kDecodeFixedCheckSpill)) return 3;
+    if (v == 14) return 4;  // diagnostics: the unchecked body forced to >= 5 waves per SIMD
+    return 0;
+}
+
+// a checked k_decode_fixed launch: zero the mismatch record before, read it
+// after (a host wait: test builds only)
+Status run_checked_decode(huff_ctx* ctx, dev::DecodeArgs& a, const std::function<hipError_t()>& launch) {
+    if (!a.check_mode) return hip_status(launch(), "decode");
+    HUFF_TRY(ctx->d_err.ensure(32));
+    a.err = static_cast<uint32_t*>(ctx->d_err.p);
+    HIP_TRY(hipMemsetAsync(a.err, 0, 32, ctx->stream));
+    HIP_TRY(launch());
+    uint32_t e[8] = {};
+    HIP_TRY(hipMemcpyAsync(e, a.err, 32, hipMemcpyDeviceToHost, ctx->stream));
+    HUFF_TRY(ctx->sync());
+    if (e[7]) return Status::err(HUFF_E_CORRUPT, "decode diagnostics: " + std::to_string(e[7]) +
+                                 " scratch canary words changed under the decoder");
+    if (e[0] == 0) return Status::ok();
+    const uint64_t want = (static_cast<uint64_t>(e[4]) << 32) | e[3], got = (static_cast<uint64_t>(e[6]) << 32) | e[5];
+    return Status::err(HUFF_E_CORRUPT, "decode self-check: " + std::to_string(e[0]) + " lane(s) did not end at their "
+                       "successor's restart point; first: task " + std::to_string(e[1]) + " lane " +
+                       std::to_string(e[2]) + " ended at bit " + std::to_string(got) + ", expected " +
+                       std::to_string(want));
+}
+
 // multi-symbol table index bits: 12 (16 KiB); 11 and 10 measured slower on
 // Zipf (its 12-bit codes fall to the single-symbol path) and no faster on text
 static uint32_t ms_bits() { return dev::kMsMaxBits; }
@@ -440,6 +472,7 @@ huff::Status huff_enc::pack(const huff_tree* t, uint64_t base, const uint8_t* pr
             packed = true;
             index_pending = true;  // arithmetic: written only if a consumer needs it
             packed_tree_id = t->id;
+            remember_tree(t);
             bit_base = base;
             total_bits = tb;
             return huff::Status::ok();
@@ -480,6 +513,7 @@ huff::Status huff_enc::pack(const huff_tree* t, uint64_t base, const uint8_t* pr
     packed = true;
     index_pending = false;
     packed_tree_id = t->id;
+    remember_tree(t);
     bit_base = base;
     total_bits = tb;
     return huff::Status::ok();
@@ -496,6 +530,9 @@ huff::Status huff_enc::ensure_index() {
 
 huff::Status huff_enc::decode(const huff_tree* t, const uint8_t* d_comp, uint64_t comp_bytes, uint8_t* d_out) {
     if (!packed) return huff::Status::err(HUFF_E_STATE, "no restart index: pack (or upload an index) first");
+    if (!codes_match(t))
+        return huff::Status::err(HUFF_E_STATE, "decode tree differs from the tree the stream was packed (or its index "
+                                               "uploaded) with");
     if (reinterpret_cast<uintptr_t>(d_comp) & 3)
         return huff::Status::err(HUFF_E_INVALID_ARG, "compressed stream must be 4-byte aligned");
     HUFF_TRY(ctx->activate());
@@ -531,7 +568,9 @@ huff::Status huff_enc::decode(const huff_tree* t, const uint8_t* d_comp, uint64_
     //   text          0.56   0.61                0.90  -
     //   8-bit codes   0.74   1.06                -     0.94
     // HUFF_DEC_VARIANT=1|7|9|10 forces one (tests, measurements).
+    // HUFF_DEC_VARIANT=11|12|13: k_decode_fixed's self-checking builds
     a.variant = huff::dev::kDecodeFixed;
+    a.check_mode = huff::decode_check_mode();
     if (const char* env = std::getenv("HUFF_DEC_VARIANT")) {
         const int v = std::atoi(env);
         if (v == static_cast<int>(huff::dev::kDecodeRing) || v == static_cast<int>(huff::dev::kDecodeSingle) ||
@@ -550,7 +589,11 @@ huff::Status huff_enc::decode(const huff_tree* t, const uint8_t* d_comp, uint64_
     a.stab_bits = dt->sbits;
     a.n = n;
     a.out = d_out;
-    HUFF_TRY(ctx->timed("decode", [&] { return huff::dev::launch_decode(a, ctx->stream); }));
+    if (a.check_mode) {
+        HUFF_TRY(huff::run_checked_decode(ctx, a, [&] { return huff::dev::launch_decode(a, ctx->stream); }));
+    } else {
+        HUFF_TRY(ctx->timed("decode", [&] { return huff::dev::launch_decode(a, ctx->stream); }));
+    }
     HIP_TRY(hipEventRecord(ctx->lut_free, ctx->stream));
     return huff::Status::ok();
 }
@@ -580,8 +623,23 @@ huff::Status huff_enc::upload_index(const huff_index_host& idx) {
                                ctx->stream));
     HUFF_TRY(ctx->sync());
     packed = true;
+    packed_any_tree = true;  // the caller vouches for the tree (huff_enc_upload_index)
     index_pending = false;
     return huff::Status::ok();
+}
+
+void huff_enc::remember_tree(const huff_tree* t) {
+    const huff::EncTables& et = t->enc_tables();
+    std::memcpy(packed_len, et.len, sizeof packed_len);
+    std::memcpy(packed_code, et.code, sizeof packed_code);
+    packed_any_tree = false;
+}
+
+bool huff_enc::codes_match(const huff_tree* t) const {
+    if (packed_any_tree) return true;
+    const huff::EncTables& et = t->enc_tables();
+    return std::memcmp(packed_len, et.len, sizeof packed_len) == 0 &&
+           std::memcmp(packed_code, et.code, sizeof packed_code) == 0;
 }
 
 // ---------------------------------------------------------------------------
@@ -878,7 +936,8 @@ Status decode_indexless_dev(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_
         d.pad_stage = dev::fixed_decode_pad(valid_bits, total);
         d.n = total;
         d.out = out_at();
-        HIP_TRY(dev::launch_decode_fixed(d, strm));
+        d.check_mode = decode_check_mode();
+        HUFF_TRY(run_checked_decode(ctx, d, [&] { return dev::launch_decode_fixed(d, strm); }));
         HIP_TRY(hipEventRecord(ctx->lut_free, strm));
         return Status::ok();
     }

@@ -55,6 +55,8 @@ void build_multi_table(const HuffTree& t, uint32_t mbits, DecTables& out);
 
 // HUFF_DISABLE_FIXED8=1 forces the general kernels even for all-8-bit codes
 bool fixed8_disabled();
+// HUFF_DEC_VARIANT=11|12|13 -> k_decode_fixed self-check mode 1|2|3 (else 0)
+uint32_t decode_check_mode();
 
 Status build_dec_tables(const HuffTree& t, DecTables& out);
 
@@ -121,6 +123,7 @@ struct huff_ctx {
     PinnedBuf pin_lut;   // decode table upload
     DevBuf d_in, d_out;  // staging of the host-pointer API
     DevBuf d_lut;
+    DevBuf d_err;        // k_decode_fixed self-check record (check builds)
     // index-free decode workspace, kept across calls (per-call allocations
     // of its ~100 MB per GiB of stream cost more than the kernels)
     std::shared_ptr<huff::IndexlessSync> idx_ws;
@@ -156,6 +159,13 @@ struct huff_enc {
     // state of the last pack (for decode)
     bool packed = false;
     uint64_t packed_tree_id = 0;
+    // code lengths and codes of the tree the stream was packed with (or whose
+    // index was uploaded): decode refuses a tree with other codes
+    uint8_t packed_len[256] = {};
+    uint64_t packed_code[256] = {};
+    bool packed_any_tree = false;  // an index uploaded without a tree
+    void remember_tree(const huff_tree* t);
+    bool codes_match(const huff_tree* t) const;
     uint64_t bit_base = 0, total_bits = 0;
     // the byte-map pack leaves the (arithmetic) restart index unwritten
     // until a consumer needs it: decode through a bit decoder, or download
@@ -185,6 +195,7 @@ Status decompress_host(huff_ctx* ctx, const huff_compress_data* cd, uint8_t* out
 Status file_compress(huff_ctx* ctx, const char* src, const char* dst, size_t block_size);
 Status file_decompress(huff_ctx* ctx, const char* src, const char* dst, size_t block_size);
 Status parse_block_size(const char* s, size_t* out);
+Status run_checked_decode(huff_ctx* ctx, dev::DecodeArgs& a, const std::function<hipError_t()>& launch);
 // decode without a restart index: valid_bits of the stream at d_comp; the
 // symbols land in `out` (grown as needed), their count in *nsym
 Status decode_indexless_dev(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_bytes, uint64_t valid_bits,

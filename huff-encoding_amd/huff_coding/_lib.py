@@ -40,6 +40,7 @@ E_PADDING = 15
 E_TREE_LEN = 16
 E_NO_DEVICE = 17
 E_STATE = 18
+E_CORRUPT = 19
 
 # every exported function: (name, restype, argtypes)
 u8p = C.POINTER(C.c_uint8)

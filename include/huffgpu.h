@@ -53,7 +53,10 @@ enum huff_status {
     HUFF_E_PADDING = 15,        /* panic "padding bits cannot be larger than 7" comp.rs:59 */
     HUFF_E_TREE_LEN = 16,       /* panic "stored tree length must be at least 2" :153-155 */
     HUFF_E_NO_DEVICE = 17,      /* no GPU / HIP unavailable: the product never falls back */
-    HUFF_E_STATE = 18           /* call order violated (e.g. pack before hist)            */
+    HUFF_E_STATE = 18,          /* call order violated (e.g. pack before hist), or a decode
+                                 * tree whose codes differ from the packed tree's          */
+    HUFF_E_CORRUPT = 19         /* decode self-check (HUFF_DEC_VARIANT 11-13) found a lane
+                                 * that did not end at its successor's restart point        */
 };
 
 /* Message of the last failing call on this thread (reference wording). */
