@@ -445,15 +445,9 @@ __device__ __forceinline__ void fx_check(const DecodeArgs& a, const Task& k, uin
     }
 }
 
-template <bool SLOW, bool PAD, bool CHECK, bool CANARY = false>
+template <bool SLOW, bool PAD, bool CHECK>
 __device__ __forceinline__ void decode_fixed_body(const DecodeArgs& a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    // diagnostics (k_decode_fixed_w5): a private array that lives in scratch,
-    // filled at entry and verified after every task
-    volatile uint32_t canary[CANARY ? 16 : 1];
-    const uint32_t ctag = (blockIdx.x << 8) | threadIdx.x;
-    if constexpr (CANARY)
-        for (int i = 0; i < 16; ++i) canary[(i * 5 + (a.n & 1)) & 15] = ctag * 2654435761u + i;
     const uint32_t K = a.stab_bits;
     const uint32_t nent = 1u << K;
     const uint32_t t = threadIdx.x, lane = t & 63, wave = wave_index();
@@ -538,11 +532,6 @@ __device__ __forceinline__ void decode_fixed_body(const DecodeArgs& a) {
         } else {
             fx_check<CHECK>(a, cur, task, lane, 0, false);  // keeps the shuffles wave-uniform
         }
-        if constexpr (CANARY) {
-            uint32_t nbad = 0;
-            for (int i = 0; i < 16; ++i) nbad += canary[(i * 5 + (a.n & 1)) & 15] != ctag * 2654435761u + i;
-            if (nbad) atomicAdd(a.err + 7, nbad);
-        }
         if (!more) break;
         wave_sync();  // the input stage is reused by the next task
         task = nxt_task;
@@ -577,7 +566,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(8, 8))
 // diagnostics: the production body (no check) forced to >= 5 waves per SIMD
 template <bool SLOW, bool PAD>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(5, 8))) void k_decode_fixed_w5(DecodeArgs a) {
-    decode_fixed_body<SLOW, PAD, false, true>(a);
+    decode_fixed_body<SLOW, PAD, false>(a);
 }
 
 }  // namespace

@@ -76,8 +76,7 @@ def main():
     ctx = H.Context(0)
     out = []
     M = 1 << 20
-    cases = [("geo", 16 * M, "14", None), ("geo", 64 * M, "14", None), ("text", 16 * M, "14", None),
-             ("text", 64 * M, "14", None), ("geo", 16 * M, "14", 256)]
+    cases = [("geo", 16 * M, "14", None), ("geo", 64 * M, "14", None)]
     for kind, n, var, grid in cases:
         r = run(ctx, kind, n, var, grid)
         print(json.dumps(r), flush=True)
