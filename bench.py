@@ -5,15 +5,21 @@ BASELINE.json metric: "encode+decode GB/s on 1 GiB bytes at 1/2/4/8 MI355X;
 % HBM roofline". One step = one pass of the hot path over the rank's bytes,
 inputs resident in HBM when the timed region starts:
 
-    hist256 (pass 1) -> [N>1: all_gather of u64[256] weights + 8 tail bytes
-    over RCCL] -> host HuffTree -> chunk bits + scan -> pack (pass 2)
-    -> block-parallel decode
+    hist256 (pass 1) -> [N>1: ONE RCCL all-gather of a 258 x int64 row
+    (weights + 8 tail bytes) inside the library, huff_mgpu_compress] ->
+    host HuffTree -> chunk bits + scan -> pack (pass 2) -> block-parallel decode
 
-Weak scaling: every rank holds 1 GiB (its slice of one global synthetic
-stream, generated on device by offset), all ranks share one tree built from
-the summed weights, rank r encodes at global bit offset O_r = sum_{q<r} bits_q
-so the concatenated rank outputs are the single-stream compress_with_tree
-bytes. value = (bytes of all ranks) / (max over ranks of the step time).
+--scaling weak (default): every rank holds --bytes-per-gpu (1 GiB), its slice
+of one global synthetic stream generated on device by offset; value = bytes
+of all ranks / max over ranks of the step time.
+--scaling strong: --total-bytes (1 GiB) split N ways (SURVEY §8d's 1/2/4/8
+curve); a 512 MiB buffer is rewritten between timed steps so no rank's shard
+sits in the 256 MiB Infinity Cache; each step is bracketed by barriers and
+its time summed.
+
+At N=1 the headline is configs[1] (1 GiB uniform); a side result carries
+configs[2] (1 GiB Zipf(1.2), the general pack/decode kernels) with its own
+kernels, roofline and cpu_baseline (--side none skips it).
 
 Run: python bench.py [--gpus N --steps K --warmup W --workload uniform|zipf|text]
      N>1: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N
@@ -40,11 +46,34 @@ from huff_coding import mgpu  # noqa: E402
 METRIC = "encode+decode GB/s on 1 GiB bytes at 1/2/4/8 MI355X; % HBM roofline"
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 SEEDS = {"uniform": 0x5EED0001, "zipf": 0x5EED0002, "text": 0x5EED0005}
-WORKLOADS = {
-    "uniform": "1 GiB uniform-random bytes per GPU (BASELINE configs[1]), encode+decode, bit-exact",
-    "zipf": "1 GiB Zipf(alpha=1.2) bytes per GPU (BASELINE configs[2]), encode+decode",
-    "text": "1 GiB synthetic English-like text per GPU (stand-in for configs[4] enwik8), encode+decode",
-}
+CONFIG_OF = {"uniform": "BASELINE configs[1]", "zipf": "BASELINE configs[2]",
+             "text": "stand-in for configs[4] enwik8"}
+
+
+def human(n: int) -> str:
+    for unit, s in (("GiB", 30), ("MiB", 20), ("KiB", 10)):
+        if n >= 1 << s and n % (1 << s) == 0:
+            return f"{n >> s} {unit}"
+    return f"{n} B"
+
+
+def enwik8_path():
+    """$ENWIK8: the real text when the box has it"""
+    p = os.environ.get("ENWIK8")
+    return p if p and os.path.isfile(p) else None
+
+
+def cpu_info():
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"nproc": os.cpu_count(), "affinity": len(os.sched_getaffinity(0)), "cpu_model": model}
 
 
 def cpu_baseline(workload: str, target_s: float):
@@ -81,6 +110,7 @@ def cpu_baseline(workload: str, target_s: float):
         _, back, fe, fd = O.fast_roundtrip(data, fast_threads)
     assert np.array_equal(back, data)
     return {"value": round(n / (e + d) / 1e9, 6), "unit": "GB/s", "cores": 12, "kind": "port",
+            "host": cpu_info(),
             "sample": f"{n} B of the same {workload} stream; encode {n / e / 1e9:.4f} GB/s (12-thread "
                       f"histogram + 1-thread bit-serial encode), decode {n / d / 1e9:.4f} GB/s (1-thread "
                       f"tree walk); oracle/huff_oracle.c restatement of huff_coding (Rust not buildable here)",
@@ -115,13 +145,255 @@ def dominant_traffic(kind, phase, fixed8, dec_kernel):
     return int(sum(t[n]["hbm_bytes"] for n in names)), os.path.relpath(path, ROOT)
 
 
+class Setup:
+    def __init__(self, args, world, rank, local):
+        self.args, self.world, self.rank, self.local = args, world, rank, local
+        self.ctx = H.Context(local)
+        self.stream = torch.cuda.current_stream()
+        self.ctx.set_stream(self.stream.cuda_stream)
+        self.nccl = args.dist_backend == "nccl"
+        self.dev = torch.device("cuda", local) if self.nccl else None
+        self.comm, self.comm_note = None, None
+        if world > 1 and self.nccl:
+            self.comm, self.comm_note = self.native_comm()
+        self.dx = mgpu.DeviceExchange(self.dev) if world > 1 and self.nccl and self.comm is None else None
+        self.flush = (torch.empty(512 << 20, dtype=torch.uint8, device="cuda")
+                      if args.scaling == "strong" else None)
+        self.ceil = None
+
+    def native_comm(self):
+        """the library's own RCCL communicator (huff_comm) on every rank, or
+        none on any (then torch's RCCL group carries the one all-gather; the
+        JSON says which ran). Ranks agree before and after the collective init."""
+        uid, note = None, None
+        if self.rank == 0:
+            try:
+                uid = mgpu.NativeComm.unique_id()
+            except Exception as e:
+                note = f"huff_comm_unique_id failed: {e}"
+        obj = [uid]
+        dist.broadcast_object_list(obj, src=0)
+        comm = None
+        if obj[0] is not None:
+            try:
+                comm = mgpu.NativeComm(self.ctx, self.world, self.rank, obj[0])
+            except Exception as e:
+                note = f"huff_comm_init failed on rank {self.rank}: {e}"
+        ok = torch.tensor([1 if comm is not None else 0], device=self.dev)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        if int(ok.item()) == 0:
+            if comm is not None:
+                comm.close()
+            return None, (note or "huff_comm unavailable on another rank") + "; torch RCCL all_gather used"
+        return comm, None
+
+    def barrier(self):
+        if self.world > 1:
+            dist.barrier()
+
+    def max_over_ranks(self, v: float) -> float:
+        if self.world == 1:
+            return v
+        t = torch.tensor([v], dtype=torch.float64, device=self.dev or "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+
+def make_input(s: Setup, kind: str, n: int):
+    x = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
+    src = "synthetic (counter-based generator on device; see DESIGN.md)"
+    ew = enwik8_path() if kind == "text" else None
+    if ew:  # configs[4]: the real enwik8, tiled to the shard (each rank at its global offset)
+        raw = np.fromfile(ew, dtype=np.uint8)
+        start = (s.rank * n) % raw.size
+        reps = (start + n + raw.size - 1) // raw.size
+        host = np.tile(raw, reps)[start:start + n]
+        x[:n].copy_(torch.from_numpy(host))
+        src = f"enwik8 from $ENWIK8 ({raw.size} B) tiled to {n} B per rank"
+    else:
+        D.generate(s.ctx, kind, SEEDS[kind], x.data_ptr(), n, offset=s.rank * n,
+                   cdf=D.zipf_cdf(1.2) if kind == "zipf" else None)
+    return x, src
+
+
+def run_workload(s: Setup, kind: str, n: int, with_cpu: bool):
+    args, world, rank = s.args, s.world, s.rank
+    ctx = s.ctx
+    x, data_src = make_input(s, kind, n)
+    job = H.EncodeJob(ctx, x.data_ptr(), n)
+    dec = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
+    state = {"out": torch.empty(n + 128, dtype=torch.uint8, device="cuda"), "cap": n + 128}
+
+    def encode():
+        """N=1: compress() in one native call (pass 1, tree, pass 2);
+        N>1: huff_mgpu_compress (pass 1, RCCL all-gather, tree, bit base, pass 2)"""
+        if world == 1:
+            return job.compress(state["out"].data_ptr(), state["cap"])
+        if s.comm is not None:
+            tree, _, bits, _ = s.comm.compress(job, state["out"].data_ptr(), state["cap"])
+            return tree, bits
+        if s.dx is not None:
+            hists, tails = s.dx(job)
+        else:
+            hists, tails = mgpu.exchange(job.hist(), x[n - 8:n], device=s.dev)
+        tree, _, bits = job.pack_shards(hists, rank, tails, state["out"].data_ptr(), state["cap"])
+        return tree, bits
+
+    def encode_grow():
+        try:
+            return encode()
+        except H.HuffError as e:  # compressed shard larger than the buffer: grow once, redo
+            if getattr(e, "bits_needed", None) is None:
+                raise
+            state["cap"] = (e.bit_base % 8 + e.bits_needed + 7) // 8 + 128
+            state["out"] = torch.empty(state["cap"], dtype=torch.uint8, device="cuda")
+            return encode()
+
+    def step():
+        tree, bits = encode_grow()
+        job.decode(tree, state["out"].data_ptr(), dec.data_ptr())
+        return bits, tree
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if not args.no_verify:
+        assert torch.equal(dec[:n], x[:n]), "decode(encode(x)) != x"
+
+    # timed region: K steps (weak: back to back; strong: each step alone,
+    # after a 512 MiB rewrite that evicts the Infinity Cache)
+    ctx.set_timing(True)
+    ctx.reset_timing()
+    bits, tree = 0, None
+    if s.flush is None:
+        s.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            bits, tree = step()
+        torch.cuda.synchronize()
+        s.barrier()
+        elapsed = time.perf_counter() - t0
+    else:
+        elapsed = 0.0
+        for i in range(args.steps):
+            s.flush.fill_(i & 0xFF)  # torch's stream: outside the library's kernel timing
+            s.barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            bits, tree = step()
+            torch.cuda.synchronize()
+            s.barrier()
+            elapsed += time.perf_counter() - t0
+    elapsed = s.max_over_ranks(elapsed)
+    kstats = {k: ctx.kernel_time(k) for k in ("hist", "chunk_bits", "scan", "pack", "decode")}
+    ctx.set_timing(False)
+
+    # end-to-end encode and decode apart (same K, same buffers)
+    s.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        tree, bits = encode_grow()
+    torch.cuda.synchronize()
+    t_enc = s.max_over_ranks(time.perf_counter() - t0)
+    s.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        job.decode(tree, state["out"].data_ptr(), dec.data_ptr())
+    torch.cuda.synchronize()
+    t_dec = s.max_over_ranks(time.perf_counter() - t0)
+
+    _, ln = tree.code_table()  # letters present in the input are exactly those with a code
+    present = np.asarray(ln) > 0
+    fixed8 = bool((ln[present] == 8).all()) and os.environ.get("HUFF_DISABLE_FIXED8", "0") in ("", "0")
+    maxlen = int(ln[present].max())  # the decode kernel the runtime picks (runtime.cpp, huff_enc::decode)
+    dec_kernel = "k_decode" if maxlen > 32 else "k_decode_fixed"
+    ms_per_step = elapsed * 1e3 / args.steps
+    value = world * n / (elapsed / args.steps) / 1e9
+    comp_bytes = (bits + 7) // 8
+    nchunks = (n + 65535) // 65536
+    algo = {  # algorithmic bytes per launch (DESIGN.md §3)
+        "hist": n,
+        "chunk_bits": nchunks * (1024 + 8),
+        "scan": nchunks * 16,
+        "pack": n + comp_bytes,
+        "decode": comp_bytes + n,
+    }
+    kernels = {}
+    for k, b in algo.items():
+        ms, cnt = kstats[k]
+        if cnt:
+            avg = ms / cnt
+            kernels[k] = {"avg_ms": round(avg, 5), "launches": cnt, "algo_bytes": b,
+                          "GBps": round(b / (avg * 1e-3) / 1e9, 1)}
+    dom = max(kernels, key=lambda k: kernels[k]["avg_ms"])
+    ach = kernels[dom]["GBps"]
+    # the committed PMC summaries are per launch of a 1 GiB job: other sizes get none
+    traffic, traffic_src = (dominant_traffic(kind, dom, fixed8, dec_kernel) if n == 1 << 30 else (None, None))
+    enc_ms = sum(kernels[k]["avg_ms"] for k in ("hist", "chunk_bits", "scan", "pack") if k in kernels)
+    if s.ceil is None:  # measured HBM ceilings of this GPU, same run (huff_dev_calibrate)
+        s.ceil = D.calibrate(ctx, x.data_ptr(), dec.data_ptr(), n & ~15, 5)
+    read_ceil, copy_ceil = s.ceil
+    collective = None
+    if world > 1:
+        how = ("huff_mgpu_compress (library RCCL communicator)" if s.comm is not None
+               else "torch.distributed " + ("RCCL" if s.nccl else "gloo (rehearsal)"))
+        collective = f"all_gather int64[258] (weights + tail bytes) per rank via {how}"
+    r = {
+        "metric": METRIC,
+        "value": round(value, 3),
+        "unit": "GB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": args.scaling,
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": data_src,
+        "config": {"workload": f"{human(n * world)} {kind} bytes"
+                               + (f" ({human(n)} per GPU)" if world > 1 else "")
+                               + f" ({CONFIG_OF[kind]}), encode+decode, bit-exact",
+                   "bytes_per_gpu": n, "global_bytes": n * world,
+                   "compressed_bytes_per_gpu": comp_bytes, "bits_per_byte": round(bits / n, 4),
+                   "kernel_path": "fixed8 byte map (all codes 8 bits)" if fixed8 else "general bit pack/decode",
+                   "parallelism": f"shard{world}", "collective": collective},
+        "roofline": {"bound": "hbm", "kernel": dom, "achieved": ach, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                     "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": traffic, "traffic_source": traffic_src,
+                     "ceilings_measured": {"read_GBps": round(read_ceil, 1), "copy_GBps": round(copy_ceil, 1),
+                                           "how": "huff_dev_calibrate: 16-B nontemporal stream, best of 5"},
+                     "frac_of_copy_ceiling": round(ach / copy_ceil, 4)},
+        "kernels": kernels,
+        "e2e": {"encode_GBps": round(world * n / (t_enc / args.steps) / 1e9, 1),
+                "decode_GBps": round(world * n / (t_dec / args.steps) / 1e9, 1),
+                "encode_ms": round(t_enc * 1e3 / args.steps, 4), "decode_ms": round(t_dec * 1e3 / args.steps, 4),
+                "note": "encode = pass 1 + host tree + pass 2 (+ the collective at N>1); decode = restart-index decode"},
+        "kernel_enc_GBps": round(n / (enc_ms * 1e-3) / 1e9, 1),
+        "host_gap_ms": round(ms_per_step - sum(k["avg_ms"] for k in kernels.values()), 4),
+        "kernel_dec_GBps": kernels.get("decode", {}).get("GBps"),
+    }
+    if s.comm_note:
+        r["config"]["collective_note"] = s.comm_note
+    if with_cpu:
+        r["cpu_baseline"] = cpu_baseline(kind, args.cpu_seconds)
+    del x, dec, state, job
+    torch.cuda.empty_cache()
+    return r
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", default="uniform", choices=sorted(WORKLOADS))
-    ap.add_argument("--bytes-per-gpu", type=int, default=1 << 30)
+    ap.add_argument("--workload", default="uniform", choices=sorted(SEEDS))
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"])
+    ap.add_argument("--bytes-per-gpu", type=int, default=1 << 30, help="weak scaling: bytes per rank")
+    ap.add_argument("--total-bytes", type=int, default=1 << 30, help="strong scaling: bytes over all ranks")
+    ap.add_argument("--side", default="zipf", choices=["zipf", "text", "none"],
+                    help="N=1: a second workload reported under 'side' (configs[2] by default)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-verify", action="store_true")
@@ -138,149 +410,19 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group("gloo")
-
-    ctx = H.Context(local)
-    stream = torch.cuda.current_stream()
-    ctx.set_stream(stream.cuda_stream)
-    n = args.bytes_per_gpu
-    kind = args.workload
-
-    x = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
-    D.generate(ctx, kind, SEEDS[kind], x.data_ptr(), n, offset=rank * n,
-               cdf=D.zipf_cdf(1.2) if kind == "zipf" else None)
-    job = H.EncodeJob(ctx, x.data_ptr(), n)
-    dec = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
-    state = {"out": None, "cap": 0}
-
-    dev = torch.device("cuda", local) if args.dist_backend == "nccl" else None
-
-    state["out"] = torch.empty(n + 128, dtype=torch.uint8, device="cuda")
-    state["cap"] = n + 128
-
-    # N>1 over RCCL: the pass-1 row is built on the GPU and all-gathered in
-    # stream order (one host wait per step); gloo rehearsal: host row exchange
-    dx = mgpu.DeviceExchange(dev) if world > 1 and args.dist_backend == "nccl" else None
-
-    def encode():
-        """N=1: compress() in one native call (pass 1, tree, pass 2);
-        N>1: pass 1 -> one all_gather -> pass 2 (tree, bit base, pack)"""
-        if world == 1:
-            tree, bits = job.compress(state["out"].data_ptr(), state["cap"])
-            return tree, bits
-        if dx is not None:
-            hists, tails = dx(job)
-        else:
-            hists, tails = mgpu.exchange(job.hist(), x[n - 8:n], device=dev)
-        tree, _, bits = job.pack_shards(hists, rank, tails, state["out"].data_ptr(), state["cap"])
-        return tree, bits
-
-    def step():
-        """encode -> block-parallel decode"""
-        try:
-            tree, bits = encode()
-        except H.HuffError as e:  # compressed shard larger than the buffer: grow once, redo
-            if getattr(e, "bits_needed", None) is None:
-                raise
-            state["cap"] = (e.bit_base % 8 + e.bits_needed + 7) // 8 + 128
-            state["out"] = torch.empty(state["cap"], dtype=torch.uint8, device="cuda")
-            tree, bits = encode()
-        job.decode(tree, state["out"].data_ptr(), dec.data_ptr())
-        return bits, tree
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if not args.no_verify:
-        ok = torch.equal(dec[:n], x[:n])
-        assert ok, "decode(encode(x)) != x"
-    ctx.set_timing(True)
-    ctx.reset_timing()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    bits = 0
-    for _ in range(args.steps):
-        bits, tree = step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev or "cpu")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
-
-    # measured streaming-copy ceiling of this GPU, same run (SURVEY §8d):
-    # device-to-device copy of the n input bytes, best of 5, 2n bytes moved
-    copy_ms = []
-    for _ in range(5):
-        a_ev, b_ev = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        a_ev.record()
-        dec[:n].copy_(x[:n])
-        b_ev.record()
-        b_ev.synchronize()
-        copy_ms.append(a_ev.elapsed_time(b_ev))
-    copy_gbps = 2 * n / (min(copy_ms) * 1e-3) / 1e9
-
-    _, ln = tree.code_table()  # letters present in the input are exactly those with a code
-    present = np.asarray(ln) > 0
-    state["fixed8"] = bool((ln[present] == 8).all()) and os.environ.get("HUFF_DISABLE_FIXED8", "0") in ("", "0")
-    maxlen = int(ln[present].max())  # the decode kernel the runtime picks (runtime.cpp, huff_enc::decode)
-    state["dec_kernel"] = "k_decode" if maxlen > 32 else "k_decode_fixed"
-    ms_per_step = elapsed * 1e3 / args.steps
-    value = world * n / (elapsed / args.steps) / 1e9
-    comp_bytes = (bits + 7) // 8
-    nchunks = (n + 65535) // 65536
-    algo = {  # algorithmic bytes per launch
-        "hist": n,
-        "chunk_bits": nchunks * (1024 + 8),
-        "scan": nchunks * 16,
-        "pack": n + comp_bytes,
-        "decode": comp_bytes + n,
-    }
-    kernels = {}
-    for k, b in algo.items():
-        ms, cnt = ctx.kernel_time(k)
-        if cnt:
-            avg = ms / cnt
-            kernels[k] = {"avg_ms": round(avg, 5), "launches": cnt, "algo_bytes": b,
-                          "GBps": round(b / (avg * 1e-3) / 1e9, 1)}
-    dom = max(kernels, key=lambda k: kernels[k]["avg_ms"])
-    ach = kernels[dom]["GBps"]
-    # the committed PMC summaries are per launch of a 1 GiB job: other sizes get none
-    traffic, traffic_src = (dominant_traffic(kind, dom, state.get("fixed8"), state.get("dec_kernel"))
-                            if n == 1 << 30 else (None, None))
-    enc_ms = sum(kernels[k]["avg_ms"] for k in ("hist", "chunk_bits", "scan", "pack") if k in kernels)
-    result = {
-        "metric": METRIC,
-        "value": round(value, 3),
-        "unit": "GB/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(ms_per_step, 4),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "u8",
-        "data": "synthetic (counter-based generator on device; see DESIGN.md)",
-        "config": {"workload": WORKLOADS[kind], "bytes_per_gpu": n, "global_bytes": n * world,
-                   "compressed_bytes_per_gpu": comp_bytes, "bits_per_byte": round(bits / n, 4),
-                   "kernel_path": "fixed8 byte map (all codes 8 bits)" if state.get("fixed8") else "general bit pack/decode",
-                   "parallelism": f"shard{world}", "collective": (f"all_gather int64[258] (weights + tail bytes) over {'RCCL' if args.dist_backend == 'nccl' else 'gloo (rehearsal)'}" if world > 1 else None)},
-        "roofline": {"bound": "hbm", "kernel": dom, "achieved": ach, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                     "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": traffic, "traffic_source": traffic_src,
-                     "copy_ceiling_measured": round(copy_gbps, 1), "frac_of_copy_ceiling": round(ach / copy_gbps, 4)},
-        "kernels": kernels,
-        "kernel_enc_GBps": round(n / (enc_ms * 1e-3) / 1e9, 1),
-        "host_gap_ms": round(ms_per_step - sum(k["avg_ms"] for k in kernels.values()), 4),
-        "kernel_dec_GBps": kernels.get("decode", {}).get("GBps"),
-    }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(kind, args.cpu_seconds)
+    s = Setup(args, world, rank, local)
+    if args.scaling == "strong":
+        n = (args.total_bytes // world) & ~0xFFFF
+    else:
+        n = args.bytes_per_gpu
+    with_cpu = rank == 0 and world == 1 and not args.no_cpu_baseline
+    result = run_workload(s, args.workload, n, with_cpu)
+    if world == 1 and args.side != "none" and args.side != args.workload:
+        result["side"] = {args.side: run_workload(s, args.side, n, with_cpu)}
     if rank == 0:
         print(json.dumps(result), flush=True)
+    if s.comm is not None:
+        s.comm.close()
     if world > 1:
         dist.destroy_process_group()
 

@@ -2,6 +2,7 @@
 //
 // Each entry point converts huff::Status into an int code plus the
 // thread-local last-error message; nothing throws across the ABI.
+#include <algorithm>
 #include <cstring>
 #include <exception>
 #include <new>
@@ -464,6 +465,41 @@ int huff_dev_generate(huff_ctx* ctx, int kind, uint64_t seed, uint64_t offset, c
         hipStreamSynchronize(ctx->stream);
         if (d_cdf) hipFree(d_cdf);
         if (er != hipSuccess) return huff::Status::err(HUFF_E_HIP, hipGetErrorString(er));
+        return huff::Status::ok();
+    });
+}
+
+int huff_dev_calibrate(huff_ctx* ctx, const uint8_t* d_src, uint8_t* d_dst, size_t n, int iters,
+                       double* read_gbps, double* copy_gbps) {
+    if (!ctx || !d_src || !d_dst || !read_gbps || !copy_gbps || iters < 1 || n < 16 ||
+        (reinterpret_cast<uintptr_t>(d_src) & 15) || (reinterpret_cast<uintptr_t>(d_dst) & 15))
+        return fail(HUFF_E_INVALID_ARG, "calibrate: null, misaligned or too small");
+    return guarded([&]() -> huff::Status {
+        HUFF_TRY(ctx->activate());
+        const uint64_t m = n & ~uint64_t(15);
+        hipEvent_t a, b;
+        HIP_TRY_RT(hipEventCreate(&a));
+        HIP_TRY_RT(hipEventCreate(&b));
+        unsigned* sink = nullptr;
+        HIP_TRY_RT(hipMalloc(&sink, 16));
+        float best[2] = {1e30f, 1e30f};  // [read, copy] over the two shapes of each
+        hipError_t er = hipSuccess;
+        for (int mode = 0; mode < 4 && er == hipSuccess; ++mode)
+            for (int it = 0; it < iters + 1 && er == hipSuccess; ++it) {  // + 1 warm-up launch
+                hipEventRecord(a, ctx->stream);
+                er = huff::dev::launch_calib(mode, d_src, d_dst, m, sink, static_cast<uint32_t>(ctx->cu_count), ctx->stream);
+                hipEventRecord(b, ctx->stream);
+                hipEventSynchronize(b);
+                float ms = 0;
+                hipEventElapsedTime(&ms, a, b);
+                if (it) best[mode / 2] = std::min(best[mode / 2], ms);
+            }
+        hipFree(sink);
+        hipEventDestroy(a);
+        hipEventDestroy(b);
+        if (er != hipSuccess) return huff::Status::err(HUFF_E_HIP, hipGetErrorString(er));
+        *read_gbps = static_cast<double>(m) / (best[0] * 1e-3) / 1e9;
+        *copy_gbps = 2.0 * static_cast<double>(m) / (best[1] * 1e-3) / 1e9;
         return huff::Status::ok();
     });
 }

@@ -239,5 +239,10 @@ hipError_t launch_find_first(const uint8_t* in, uint64_t n, const uint8_t* missi
                              hipStream_t s);
 hipError_t launch_generate(int kind, uint64_t seed, uint64_t offset, const uint64_t* cdf, uint8_t* out, uint64_t n,
                            hipStream_t s);
+// HBM calibration (synth.hip, measurement only): modes 0/1 = streaming read
+// of src (grid-stride / one-shot), 2/3 = streaming copy src -> dst (grid-
+// stride / one-shot); n a multiple of 16, pointers 16-B aligned
+hipError_t launch_calib(int mode, const uint8_t* src, uint8_t* dst, uint64_t n, unsigned* sink, uint32_t cu_count,
+                        hipStream_t s);
 
 }  // namespace huff::dev

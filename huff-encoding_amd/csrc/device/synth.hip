@@ -2,6 +2,8 @@
 // code). Counter-based, so byte i of a stream depends only on (kind, seed,
 // offset + i) and the CPU checker regenerates the same bytes
 // (oracle/huff_oracle.c orc_gen_*). Never timed.
+#include <algorithm>
+
 #include "kernels.hpp"
 
 namespace huff::dev {
@@ -104,4 +106,96 @@ hipError_t launch_generate(int kind, uint64_t seed, uint64_t offset, const uint6
     return hipGetLastError();
 }
 
+}  // namespace huff::dev
+
+// ---------------------------------------------------------------------------
+// HBM calibration (measurement only, not the path): the streaming read and
+// copy ceilings bench.py reports beside the spec peak, measured in the same
+// run. Two shapes each (tools/calib.hip's best): a grid-stride loop with four
+// 16-B nontemporal loads in flight per lane over a grid of n/16 KiB
+// workgroups, and a one-shot grid (read: 16 loads per lane, 64 KiB per
+// workgroup; copy: the k_bytemap shape, 4 pieces per lane, 16 KiB per
+// workgroup, nontemporal stores). The caller keeps the best of each kind.
+// ---------------------------------------------------------------------------
+namespace huff::dev {
+namespace {
+typedef unsigned int calib_u32x4 __attribute__((ext_vector_type(4)));
+
+__global__ __launch_bounds__(256) void k_calib_read(const calib_u32x4* __restrict__ p, uint64_t nvec, unsigned* sink) {
+    const uint64_t stride = static_cast<uint64_t>(gridDim.x) * 256;
+    uint64_t i = static_cast<uint64_t>(blockIdx.x) * 256 + threadIdx.x;
+    unsigned acc = 0;
+    for (; i + 3 * stride < nvec; i += 4 * stride) {
+        calib_u32x4 v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = __builtin_nontemporal_load(p + i + k * stride);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) acc ^= v[k].x ^ v[k].y ^ v[k].z ^ v[k].w;
+    }
+    for (; i < nvec; i += stride) {
+        const calib_u32x4 v = p[i];
+        acc ^= v.x ^ v.y ^ v.z ^ v.w;
+    }
+    if (acc == 0x9E3779B9u) sink[0] = acc;  // keeps the loads
+}
+
+__global__ __launch_bounds__(256) void k_calib_read_blk(const calib_u32x4* __restrict__ p, uint64_t nvec, unsigned* sink) {
+    const uint64_t base = static_cast<uint64_t>(blockIdx.x) * 256 * 16 + threadIdx.x;
+    calib_u32x4 v[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const uint64_t i = base + k * 256;
+        v[k] = i < nvec ? __builtin_nontemporal_load(p + i) : calib_u32x4{0, 0, 0, 0};
+    }
+    unsigned acc = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) acc ^= v[k].x ^ v[k].y ^ v[k].z ^ v[k].w;
+    if (acc == 0x9E3779B9u) sink[0] = acc;
+}
+
+__global__ __launch_bounds__(256) void k_calib_copy(const calib_u32x4* __restrict__ p, calib_u32x4* __restrict__ q,
+                                                    uint64_t nvec) {
+    const uint64_t stride = static_cast<uint64_t>(gridDim.x) * 256;
+    uint64_t i = static_cast<uint64_t>(blockIdx.x) * 256 + threadIdx.x;
+    for (; i + 3 * stride < nvec; i += 4 * stride) {
+        calib_u32x4 v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = __builtin_nontemporal_load(p + i + k * stride);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) __builtin_nontemporal_store(v[k], q + i + k * stride);
+    }
+    for (; i < nvec; i += stride) q[i] = p[i];
+}
+
+__global__ __launch_bounds__(256) void k_calib_copy_blk(const calib_u32x4* __restrict__ p, calib_u32x4* __restrict__ q,
+                                                        uint64_t nvec) {
+    const uint64_t base = static_cast<uint64_t>(blockIdx.x) * 256 * 4 + threadIdx.x;
+    calib_u32x4 v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint64_t i = base + k * 256;
+        v[k] = i < nvec ? __builtin_nontemporal_load(p + i) : calib_u32x4{0, 0, 0, 0};
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint64_t i = base + k * 256;
+        if (i < nvec) __builtin_nontemporal_store(v[k], q + i);
+    }
+}
+}  // namespace
+
+hipError_t launch_calib(int mode, const uint8_t* src, uint8_t* dst, uint64_t n, unsigned* sink, uint32_t,
+                        hipStream_t s) {
+    const uint64_t nvec = n / 16;
+    const auto* p = reinterpret_cast<const calib_u32x4*>(src);
+    auto* q = reinterpret_cast<calib_u32x4*>(dst);
+    const uint32_t g4 = static_cast<uint32_t>(std::max<uint64_t>(1, nvec / 1024));
+    switch (mode) {
+        case 0: hipLaunchKernelGGL(k_calib_read, dim3(g4), dim3(256), 0, s, p, nvec, sink); break;
+        case 1: hipLaunchKernelGGL(k_calib_read_blk, dim3((nvec + 4095) / 4096), dim3(256), 0, s, p, nvec, sink); break;
+        case 2: hipLaunchKernelGGL(k_calib_copy, dim3(g4), dim3(256), 0, s, p, q, nvec); break;
+        default: hipLaunchKernelGGL(k_calib_copy_blk, dim3((nvec + 1023) / 1024), dim3(256), 0, s, p, q, nvec); break;
+    }
+    return hipGetLastError();
+}
 }  // namespace huff::dev

@@ -1,0 +1,141 @@
+// mgpu.cpp — multi-GPU sharded compress behind the C ABI.
+//
+// One process (or thread) per GPU, each with its own huff_ctx. A huff_comm is
+// an RCCL communicator over xGMI owned next to the context: the caller makes
+// a unique id on rank 0 (huff_comm_unique_id), hands its 128 bytes to every
+// rank over any channel it has (MPI, TCP, a file), and each rank joins with
+// huff_comm_init. huff_mgpu_compress then runs the whole sharded encode of
+// the rank's job in one call:
+//
+//   pass 1 (hist256 + row kernel)  -> ncclAllGather of a 258 x int64 row per
+//   rank on the context stream     -> one device-to-host copy, ONE host wait
+//   -> host tree of the summed weights (identical on every rank)
+//   -> this rank's bit base = sum of the previous ranks' bits, its shared
+//      first byte completed from the previous ranks' tail bytes -> pass 2.
+//
+// This replaces the reference's weights merge (huff/src/comp.rs:161-172,
+// weights.rs:293-319: ByteWeights of the whole input = the sum of the
+// per-part weights) with one collective; the all-gather (not an all-reduce)
+// also gives every rank every rank's bit count, so no second collective
+// computes the bit bases. Messages are 2 KiB per rank: latency-bound.
+#include <rccl/rccl.h>
+
+#include <cstring>
+#include <memory>
+#include <vector>
+
+#include "../capi_util.hpp"
+#include "runtime.hpp"
+#include "huffgpu.h"
+
+using huff::capi::fail;
+using huff::capi::guarded;
+
+struct huff_comm {
+    huff_ctx* ctx = nullptr;
+    ncclComm_t comm = nullptr;
+    int world = 0, rank = 0;
+    DevBuf row, rows;    // this rank's row, the gathered rows (device)
+    PinnedBuf host_rows; // the gathered rows (host)
+    ~huff_comm() {
+        if (comm) ncclCommDestroy(comm);
+    }
+};
+
+namespace {
+
+huff::Status nccl_status(ncclResult_t r, const char* what) {
+    if (r == ncclSuccess) return huff::Status::ok();
+    return huff::Status::err(HUFF_E_HIP, std::string(what) + ": " + ncclGetErrorString(r));
+}
+#define NCCL_TRY(expr) HUFF_TRY(nccl_status((expr), #expr))
+
+constexpr size_t kRowWords = 258;  // huff_enc_hist_row: 256 weights, tail bytes, tail count
+
+}  // namespace
+
+extern "C" {
+
+int huff_comm_unique_id(uint8_t id[HUFF_COMM_ID_BYTES]) {
+    if (!id) return fail(HUFF_E_INVALID_ARG, "null argument");
+    return guarded([&]() -> huff::Status {
+        static_assert(sizeof(ncclUniqueId) == HUFF_COMM_ID_BYTES, "RCCL unique id size");
+        ncclUniqueId u;
+        NCCL_TRY(ncclGetUniqueId(&u));
+        std::memcpy(id, &u, sizeof u);
+        return huff::Status::ok();
+    });
+}
+
+int huff_comm_init(huff_ctx* ctx, const uint8_t id[HUFF_COMM_ID_BYTES], int world, int rank, huff_comm** out) {
+    if (!ctx || !id || !out || world < 1 || rank < 0 || rank >= world)
+        return fail(HUFF_E_INVALID_ARG, "null or out-of-range argument");
+    *out = nullptr;
+    return guarded([&]() -> huff::Status {
+        HUFF_TRY(ctx->activate());
+        auto c = std::make_unique<huff_comm>();
+        c->ctx = ctx;
+        c->world = world;
+        c->rank = rank;
+        ncclUniqueId u;
+        std::memcpy(&u, id, sizeof u);
+        NCCL_TRY(ncclCommInitRank(&c->comm, world, u, rank));
+        HUFF_TRY(c->row.ensure(kRowWords * 8));
+        HUFF_TRY(c->rows.ensure(kRowWords * 8 * static_cast<size_t>(world)));
+        HUFF_TRY(c->host_rows.ensure(kRowWords * 8 * static_cast<size_t>(world)));
+        *out = c.release();
+        return huff::Status::ok();
+    });
+}
+
+void huff_comm_free(huff_comm* c) { delete c; }
+
+int huff_comm_world(const huff_comm* c, int* world, int* rank) {
+    if (!c || !world || !rank) return fail(HUFF_E_INVALID_ARG, "null argument");
+    *world = c->world;
+    *rank = c->rank;
+    return HUFF_OK;
+}
+
+int huff_mgpu_compress(huff_comm* c, huff_enc* e, uint8_t* d_out, size_t out_cap, huff_tree** tree_out,
+                       uint64_t* bit_base_out, uint64_t* bits_out, uint64_t* owned_bytes_out) {
+    if (!c || !e || !d_out || !tree_out || e->ctx != c->ctx)
+        return fail(HUFF_E_INVALID_ARG, "null argument, or a job of another context");
+    if (reinterpret_cast<uintptr_t>(d_out) & 15) return fail(HUFF_E_INVALID_ARG, "d_out must be 16-byte aligned");
+    *tree_out = nullptr;
+    return guarded([&]() -> huff::Status {
+        huff_ctx* ctx = c->ctx;
+        HUFF_TRY(ctx->activate());
+        const size_t world = static_cast<size_t>(c->world);
+        // pass 1 + the row, then the collective, in stream order
+        HUFF_TRY(e->hist_row(static_cast<long long*>(c->row.p)));
+        NCCL_TRY(ncclAllGather(c->row.p, c->rows.p, kRowWords, ncclInt64, c->comm, ctx->stream));
+        HIP_TRY_RT(hipMemcpyAsync(c->host_rows.p, c->rows.p, kRowWords * 8 * world, hipMemcpyDeviceToHost,
+                                  ctx->stream));
+        HUFF_TRY(ctx->sync());
+        const int64_t* rows = static_cast<const int64_t*>(c->host_rows.p);
+        std::vector<uint64_t> hists(world * 256);
+        std::vector<uint8_t> tails(world * 8), tail_lens(world);
+        for (size_t q = 0; q < world; ++q) {
+            std::memcpy(&hists[q * 256], rows + q * kRowWords, 256 * 8);
+            std::memcpy(&tails[q * 8], rows + q * kRowWords + 256, 8);  // little-endian: stream order
+            tail_lens[q] = static_cast<uint8_t>(rows[q * kRowWords + 257]);
+        }
+        uint64_t base = 0, bits = 0;
+        huff_tree* t = nullptr;
+        const int rc = huff_enc_pack_shards(e, hists.data(), static_cast<uint32_t>(world),
+                                            static_cast<uint32_t>(c->rank), tails.data(), tail_lens.data(), d_out,
+                                            out_cap, &t, &base, &bits);
+        if (bit_base_out) *bit_base_out = base;
+        if (bits_out) *bits_out = bits;
+        if (rc != HUFF_OK) return huff::Status::err(rc, huff::capi::last_error());
+        // the rank owns its first (shared) byte and leaves its partial last
+        // byte to the next rank, except the last rank (mgpu.owned_bytes)
+        const uint64_t end = (base & 7) + bits;
+        if (owned_bytes_out) *owned_bytes_out = c->rank + 1 == c->world ? (end + 7) / 8 : end / 8;
+        *tree_out = t;
+        return huff::Status::ok();
+    });
+}
+
+}  // extern "C"

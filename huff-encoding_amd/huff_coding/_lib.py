@@ -97,7 +97,13 @@ SIGNATURES = [
     ("huff_enc_compress", i, [vp, vp, sz, C.POINTER(vp), u64p]),
     ("huff_enc_decode", i, [vp, vp, vp, vp]),
     ("huff_dev_decompress", i, [vp, vp, vp, sz, C.c_uint8, vp, sz, szp]),
+    ("huff_comm_unique_id", i, [vp]),
+    ("huff_comm_init", i, [vp, vp, i, i, C.POINTER(vp)]),
+    ("huff_comm_free", None, [vp]),
+    ("huff_comm_world", i, [vp, C.POINTER(i), C.POINTER(i)]),
+    ("huff_mgpu_compress", i, [vp, vp, vp, sz, C.POINTER(vp), u64p, u64p, u64p]),
     ("huff_dev_generate", i, [vp, i, C.c_uint64, C.c_uint64, u64p, vp, sz]),
+    ("huff_dev_calibrate", i, [vp, vp, vp, sz, i, C.POINTER(C.c_double), C.POINTER(C.c_double)]),
     ("huff_dev_alloc", i, [vp, sz, C.POINTER(vp)]),
     ("huff_dev_free", i, [vp, vp]),
     ("huff_memcpy_htod", i, [vp, vp, vp, sz]),

@@ -141,6 +141,15 @@ def generate(ctx, kind: str, seed: int, d_out: int, n: int, offset: int = 0, cdf
     _check(load().huff_dev_generate(ctx.h, k, seed, offset, cp, C.c_void_p(d_out), n))
 
 
+def calibrate(ctx, d_src: int, d_dst: int, n: int, iters: int = 5):
+    """measured HBM ceilings of this GPU (not a reference function): best-of-
+    iters GB/s of a streaming read of n bytes and of a streaming copy (2n
+    bytes moved); d_src / d_dst 16-B aligned device buffers of >= n bytes"""
+    r, c = C.c_double(), C.c_double()
+    _check(load().huff_dev_calibrate(ctx.h, C.c_void_p(d_src), C.c_void_p(d_dst), n, iters, C.byref(r), C.byref(c)))
+    return r.value, c.value
+
+
 def zipf_cdf(alpha: float = 1.2) -> np.ndarray:
     """P(rank k) ~ k^-alpha, k=1..256, byte = k-1; cdf[k-1] = floor(2^64 * P(<=k))
     (same definition as oracle/huff_oracle.c orc_zipf_cdf; an input table)."""

@@ -124,3 +124,80 @@ def encode_shard_plan(job, shard_tail: bytes, rank: int, device=None, group=None
     tree = tree_from_weights(hists.sum(axis=0, dtype=np.uint64))
     _, ln = tree.code_table()
     return tree, plan(hists, tails, ln, rank)
+
+
+class NativeComm:
+    """The library's own RCCL communicator (huff_comm, include/huffgpu.h) and
+    the one-call sharded compress a Rust/C host would bind. rank 0 makes the
+    id (unique_id()); the caller distributes its 128 bytes (here: through the
+    torch.distributed process group that launched the ranks)."""
+
+    ID_BYTES = 128
+
+    def __init__(self, ctx, world: int, rank: int, uid: bytes):
+        import ctypes as C
+
+        from ._lib import load
+
+        from . import _check
+
+        if len(uid) != self.ID_BYTES:
+            raise ValueError("RCCL unique id must be 128 bytes")
+        self.ctx, self.world, self.rank = ctx, world, rank
+        self.h = C.c_void_p()
+        self._id = C.create_string_buffer(bytes(uid), self.ID_BYTES)
+        _check(load().huff_comm_init(ctx.h, self._id, world, rank, C.byref(self.h)))
+
+    @staticmethod
+    def unique_id() -> bytes:
+        import ctypes as C
+
+        from ._lib import load
+
+        from . import _check
+
+        buf = C.create_string_buffer(NativeComm.ID_BYTES)
+        _check(load().huff_comm_unique_id(buf))
+        return buf.raw
+
+    @classmethod
+    def from_process_group(cls, ctx, group=None):
+        """every rank of the torch.distributed group joins one huff_comm"""
+        world, rank = dist.get_world_size(group), dist.get_rank(group)
+        obj = [cls.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0, group=group)
+        return cls(ctx, world, rank, obj[0])
+
+    def compress(self, job, d_out: int, out_cap: int):
+        """huff_mgpu_compress: (HuffTree, bit_base, bits, owned_bytes); a short
+        buffer raises HuffError with .bits_needed / .bit_base"""
+        import ctypes as C
+
+        from ._lib import load
+
+        from . import HuffError, HuffTree, _check
+
+        tree_h = C.c_void_p()
+        base, bits, owned = C.c_uint64(), C.c_uint64(), C.c_uint64()
+        rc = load().huff_mgpu_compress(self.h, job.h, C.c_void_p(d_out), out_cap, C.byref(tree_h), C.byref(base),
+                                       C.byref(bits), C.byref(owned))
+        try:
+            _check(rc)
+        except HuffError as e:
+            e.bits_needed = bits.value
+            e.bit_base = base.value
+            raise
+        return HuffTree(tree_h), base.value, bits.value, owned.value
+
+    def close(self):
+        from ._lib import load
+
+        if getattr(self, "h", None):
+            load().huff_comm_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

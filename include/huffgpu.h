@@ -216,6 +216,37 @@ int huff_enc_compress(huff_enc* e, uint8_t* d_out, size_t out_cap, huff_tree** t
  * using its restart index: d_comp is the pack's d_out, d_out gets n bytes. */
 int huff_enc_decode(huff_enc* e, const huff_tree* t, const uint8_t* d_comp, uint8_t* d_out);
 
+/* ------------------------------------------------------------------------ */
+/* multi-GPU: sharded compress over an RCCL communicator  */
+/* ------------------------------------------------------------------------ */
+/* One process (or thread) per GPU, each with its own huff_ctx. The RCCL
+ * communicator (xGMI) lives next to the context; rank 0 makes the id and the
+ * caller hands its bytes to every rank over any channel it has. */
+#define HUFF_COMM_ID_BYTES 128
+typedef struct huff_comm huff_comm;
+int huff_comm_unique_id(uint8_t id[HUFF_COMM_ID_BYTES]);
+/* collective: every rank of `world` calls it with the same id; blocks until all joined */
+int huff_comm_init(huff_ctx* ctx, const uint8_t id[HUFF_COMM_ID_BYTES], int world, int rank, huff_comm** out);
+void huff_comm_free(huff_comm* c);
+int huff_comm_world(const huff_comm* c, int* world, int* rank);
+/* Collective sharded compress (replaces huff/src/comp.rs:161-172 + weights.rs:
+ * 293-319, the per-part weights merged into ByteWeights of the whole input):
+ * job `e` (a huff_enc of this rank's context) is shard `rank` of `world`
+ * contiguous shards of one stream. Pass 1 on the shard, ONE ncclAllGather of a
+ * 258 x int64 row per rank (weights + last <= 8 input bytes) on the context
+ * stream, the tree of the summed weights on the host (identical on every
+ * rank), this shard's bit base (sum of the previous shards' bits) and pass 2
+ * at that base. Writes ceil((bit_base%8 + bits)/8) bytes at d_out; d_out[0]
+ * is global stream byte bit_base/8. *owned_bytes_out = the prefix of d_out
+ * this rank contributes to the concatenated stream (its partial last byte is
+ * completed and owned by rank + 1; the last rank owns its zero-padded final
+ * byte): the ranks' owned prefixes, concatenated in rank order, are
+ * compress_with_tree over the whole stream (comp.rs:419-451). Decode the
+ * shard with huff_enc_decode(e, *tree_out, d_out, ...). On
+ * HUFF_E_BUFFER_TOO_SMALL *bits_out / *bit_base_out still hold the need. */
+int huff_mgpu_compress(huff_comm* c, huff_enc* e, uint8_t* d_out, size_t out_cap, huff_tree** tree_out,
+                       uint64_t* bit_base_out, uint64_t* bits_out, uint64_t* owned_bytes_out);
+
 /* decompress (comp.rs:487-519) of a device-resident stream that has no
  * restart index (e.g. written by the reference CPU path): comp_bytes bytes at
  * d_comp (4-B aligned), the last holding `padding` pad bits (the walk reads
@@ -230,6 +261,13 @@ int huff_dev_decompress(huff_ctx* ctx, const huff_tree* t, const uint8_t* d_comp
  * Byte i of the stream depends only on (kind, seed, offset + i). */
 int huff_dev_generate(huff_ctx* ctx, int kind, uint64_t seed, uint64_t offset, const uint64_t* cdf,
                       uint8_t* d_out, size_t n);
+
+/* HBM calibration (measurement only, not a reference function): best-of-
+ * `iters` GB/s (1e9) of a streaming 16-B nontemporal read of n bytes at d_src
+ * and of a streaming copy d_src -> d_dst (2n bytes moved); both 16-B aligned.
+ * bench.py's measured ceilings beside the 8 TB/s spec peak. */
+int huff_dev_calibrate(huff_ctx* ctx, const uint8_t* d_src, uint8_t* d_dst, size_t n, int iters,
+                       double* read_gbps, double* copy_gbps);
 
 /* device memory helpers for callers without another allocator */
 int huff_dev_alloc(huff_ctx* ctx, size_t bytes, void** d_ptr);

@@ -630,3 +630,43 @@ def test_bytemap_pack_then_bit_decoder(H, O, ctx, monkeypatch):
             assert torch.equal(dec[:n], x[:n]), (n, var)
         monkeypatch.delenv("HUFF_DISABLE_FIXED8")
         monkeypatch.delenv("HUFF_DEC_VARIANT")
+
+
+@pytest.mark.parametrize("kind", ["zipf", "uniform"])
+def test_native_comm_world1_mgpu_compress(H, O, ctx, kind):
+    """huff_comm (the library's RCCL communicator) + huff_mgpu_compress through
+    ctypes as a world-1 group: the same bytes, tree and decode as the
+    single-GPU compress, and the owned prefix is the whole stream"""
+    import torch
+    from huff_coding import device as D
+    from huff_coding import mgpu
+
+    n = (1 << 24) + 777
+    x = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
+    D.generate(ctx, kind, 0x5EED0002, x.data_ptr(), n, cdf=D.zipf_cdf(1.2) if kind == "zipf" else None)
+    comm = mgpu.NativeComm(ctx, 1, 0, mgpu.NativeComm.unique_id())
+    job = H.EncodeJob(ctx, x.data_ptr(), n)
+    out = torch.zeros(n + 128, dtype=torch.uint8, device="cuda")
+    tree, base, bits, owned = comm.compress(job, out.data_ptr(), out.numel())
+    assert base == 0 and owned == (bits + 7) // 8
+    ref_job = H.EncodeJob(ctx, x.data_ptr(), n)
+    ref = torch.zeros(n + 128, dtype=torch.uint8, device="cuda")
+    rtree, rbits = ref_job.compress(ref.data_ptr(), ref.numel())
+    assert tree.as_bin() == rtree.as_bin() and bits == rbits
+    torch.cuda.synchronize()
+    assert torch.equal(out[:owned], ref[:owned])
+    host = x[:n].cpu().numpy()
+    ot = O.Tree.from_weights(O.weights_from_array(O.fast_hist(host, 8)))
+    code, ln = ot.code_table()
+    want, wb = O.fast_encode(host, code, ln, threads=8)
+    assert wb == bits and (out[:owned].cpu().numpy() == want).all()
+    dec = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
+    job.decode(tree, out.data_ptr(), dec.data_ptr())
+    torch.cuda.synchronize()
+    assert torch.equal(dec[:n], x[:n])
+    # a short buffer reports what it needs
+    small = torch.zeros(64, dtype=torch.uint8, device="cuda")
+    with pytest.raises(H.HuffError) as ei:
+        comm.compress(job, small.data_ptr(), 64)
+    assert ei.value.bits_needed == bits
+    comm.close()
