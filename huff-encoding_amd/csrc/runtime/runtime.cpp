@@ -800,9 +800,6 @@ Status parse_block_size(const char* s, size_t* out) {
 // ---------------------------------------------------------------------------
 // index-free decode
 // ---------------------------------------------------------------------------
-namespace huff {
-
-}  // namespace huff
 
 huff::IndexlessSync& huff_ctx::indexless_ws() {
     if (!idx_ws) idx_ws = std::make_shared<huff::IndexlessSync>();

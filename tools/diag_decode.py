@@ -77,6 +77,9 @@ def main():
     out = []
     M = 1 << 20
     cases = [("geo", 16 * M, "14", None), ("geo", 64 * M, "14", None)]
+    if len(sys.argv) > 1:  # kind:n:variant ... (n in MiB)
+        cases = [(c.split(":")[0], int(c.split(":")[1]) * M, c.split(":")[2],
+                  int(c.split(":")[3]) if len(c.split(":")) > 3 else None) for c in sys.argv[1:]]
     for kind, n, var, grid in cases:
         r = run(ctx, kind, n, var, grid)
         print(json.dumps(r), flush=True)
