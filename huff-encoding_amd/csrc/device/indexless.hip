@@ -6,23 +6,32 @@
 // segment start has the residue of a true codeword boundary).
 //  k_spec : lane i decodes speculatively from bit i*S until the first codeword
 //           boundary >= (i+1)*S: exit x[i] and symbol count c[i].
-//  k_fix  : (repeated until stable) lane i restarts from its predecessor's
-//           exit x[i-1] with a second cursor on its old path; the cursor that
-//           is behind advances; when both sit on the same boundary the paths
-//           have merged (exit unchanged, count corrected), otherwise the new
-//           exit is published and the successor re-checks next round.
+//  k_fix  : (kFixRounds launches, each a no-op once the previous round
+//           changed nothing) lane i restarts from its predecessor's exit
+//           x[i-1] with a second cursor on its old path; the cursor that is
+//           behind advances; when both sit on the same boundary the paths have
+//           merged (exit unchanged, count corrected, and the merge point and
+//           index shift against the speculative path recorded), otherwise the
+//           new exit is published and the successor re-checks next round.
 //           Huffman codes resynchronise within a few codewords in practice, so
-//           one or two rounds settle; a bounded host loop falls back to a
-//           sequential sweep (k_settle) for codes that never synchronise.
+//           one or two rounds settle; k_settle (a sequential sweep) runs only
+//           when the last round still changed an exit — decided on the
+//           device, so the host does not wait between rounds.
 //  scan   : exclusive scan of c[] -> output offsets (k_scan, hist.hip).
-//  k_mark : (codes <= 32 bits) lane i walks its settled segment once more and
-//           records the start bit of every symbol whose index is a multiple
-//           of 256: the restart index the ring decoder (decode_ring.hip) then
-//           decodes from, as it does for streams this encoder wrote.
+//  k_mark : (codes <= 32 bits) the start bit of every symbol whose index is a
+//           multiple of 2^shift: the restart index the fixed-count decoder
+//           then decodes from. k_spec leaves samples on its path (the first
+//           boundary past every kSampBits bits, with its symbol count), so a
+//           mark is found by decoding forward from the nearest sample — about
+//           a quarter of the symbols, where walking the whole segment again
+//           cost more than the speculative pass itself (1.27 vs 0.91 ms per
+//           GiB of Zipf bytes).
 //  k_emit : (longer codes) lane i decodes c[i] symbols from its settled start.
 // k_spec and k_mark stage each workgroup's 256 segments in LDS (k_*_lds).
 // A codeword that would cross B is dropped, as the reference's walk drops an
 // incomplete final code (comp.rs:493-516).
+#include <algorithm>
+
 #include "bitreader.hpp"
 
 namespace huff::dev {
@@ -80,23 +89,15 @@ __global__ __launch_bounds__(kThreads) void k_spec(Seg g, uint64_t* __restrict__
     c[i] = cnt;
 }
 
-__global__ __launch_bounds__(kThreads) void k_fix(Seg g, uint64_t* __restrict__ s, const uint64_t* __restrict__ xin,
-                                                  uint64_t* __restrict__ xout, uint64_t* __restrict__ c,
-                                                  unsigned int* __restrict__ changed) {
-    extern __shared__ uint32_t plut[];
-    load_prim(plut, g);
-    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-    if (i >= g.nseg) return;
-    if (i == 0) {
-        xout[0] = xin[0];
-        return;
-    }
-    const uint64_t ns = xin[i - 1];
+// round r of the fix-up, in place on x (a lane may read its predecessor's exit
+// from this round or the last: either is a boundary of a valid path, and a
+// changed exit sets flags[r], so the next round looks again)
+__device__ __forceinline__ void fix_one(const Seg& g, uint64_t* __restrict__ s, uint64_t* __restrict__ x,
+                                        uint64_t* __restrict__ c, uint32_t* __restrict__ tm, int32_t* __restrict__ dl,
+                                        unsigned int* __restrict__ flags, int r, uint64_t i, const uint32_t* plut) {
+    const uint64_t ns = x[i - 1];
     const uint64_t old_s = s[i];
-    if (ns == old_s) {
-        xout[i] = xin[i];
-        return;
-    }
+    if (ns == old_s) return;
     const BitSrc src{reinterpret_cast<const uint32_t*>(g.comp), g.comp, g.comp_bytes};
     const Lut lut{plut, g.lut, g.K};
     const uint64_t end = (i + 1 == g.nseg) ? g.B : ((i + 1) * g.S < g.B ? (i + 1) * g.S : g.B);
@@ -109,14 +110,25 @@ __global__ __launch_bounds__(kThreads) void k_fix(Seg g, uint64_t* __restrict__ 
         if (a.pos == b.pos) {  // merged: same exit, count corrected
             s[i] = ns;
             c[i] = c[i] - cb + ca;
-            xout[i] = xin[i];
+            // the old path met the speculative one at old-local tm1 with shift
+            // dl1; the new path meets the old one at (ca, cb)
+            const uint32_t tm1 = tm[i];
+            if (tm1 != kNoMerge) {
+                const int64_t sh = static_cast<int64_t>(ca) - static_cast<int64_t>(cb);
+                const int64_t t2 = static_cast<int64_t>(tm1) + sh;
+                tm[i] = static_cast<uint32_t>(t2 > static_cast<int64_t>(ca) ? t2 : static_cast<int64_t>(ca));
+                dl[i] = dl[i] + static_cast<int32_t>(sh);
+            }
             return;
         }
         if (a.pos >= end || !a_alive) {  // new exit
             s[i] = ns;
             c[i] = ca;
-            xout[i] = a.pos;
-            if (a.pos != xin[i]) atomicOr(changed, 1u);
+            tm[i] = kNoMerge;
+            if (a.pos != x[i]) {
+                x[i] = a.pos;
+                atomicOr(flags + r, 1u);
+            }
             return;
         }
         if (a.pos < b.pos || !b_alive) {
@@ -129,8 +141,24 @@ __global__ __launch_bounds__(kThreads) void k_fix(Seg g, uint64_t* __restrict__ 
     }
 }
 
-// sequential fallback: settle every segment in order (one lane)
-__global__ void k_settle(Seg g, uint64_t* __restrict__ s, uint64_t* __restrict__ x, uint64_t* __restrict__ c) {
+// grid-stride: nearly every lane finds its start settled already (the staged
+// speculative pass fixes the segments inside each workgroup)
+__global__ __launch_bounds__(kThreads) void k_fix(Seg g, uint64_t* __restrict__ s, uint64_t* __restrict__ x,
+                                                  uint64_t* __restrict__ c, uint32_t* __restrict__ tm,
+                                                  int32_t* __restrict__ dl, unsigned int* __restrict__ flags, int r) {
+    if (r > 0 && __builtin_nontemporal_load(flags + r - 1) == 0) return;  // converged: nothing to do
+    extern __shared__ uint32_t plut[];
+    load_prim(plut, g);
+    for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < g.nseg;
+         i += static_cast<uint64_t>(gridDim.x) * blockDim.x)
+        if (i) fix_one(g, s, x, c, tm, dl, flags, r, i, plut);
+}
+
+// sequential fallback: settle every segment in order (one lane), only when
+// the last fix-up round still changed an exit
+__global__ void k_settle(Seg g, uint64_t* __restrict__ s, uint64_t* __restrict__ x, uint64_t* __restrict__ c,
+                         uint32_t* __restrict__ tm, const unsigned int* __restrict__ flags) {
+    if (__builtin_nontemporal_load(flags + kFixRounds - 1) == 0) return;
     extern __shared__ uint32_t plut[];
     load_prim(plut, g);
     if (threadIdx.x != 0) return;
@@ -150,6 +178,7 @@ __global__ void k_settle(Seg g, uint64_t* __restrict__ s, uint64_t* __restrict__
         s[i] = ns;
         x[i] = rd.pos;
         c[i] = cnt;
+        tm[i] = kNoMerge;
     }
 }
 
@@ -202,7 +231,7 @@ __device__ Staged stage_block(const IndexlessArgs& a, uint32_t* w) {
     const uint64_t seg_end = seg0 + kThreads < a.nseg ? seg0 + kThreads : a.nseg;
     const uint64_t bit_hi = seg_end * a.seg_bits < a.valid_bits ? seg_end * a.seg_bits : a.valid_bits;
     const uint64_t byte_lo = (bit_lo >> 3) & ~15ull;
-    uint64_t byte_hi = ((bit_hi + 7) >> 3) + 32;
+    uint64_t byte_hi = ((bit_hi + 7) >> 3) + 64;  // lookahead: a chunk's overshoot past the last end
     if (byte_hi > a.comp_bytes) byte_hi = a.comp_bytes;
     const uint32_t nbytes = static_cast<uint32_t>(byte_hi - byte_lo);
     const uint32_t np = (nbytes + 8 + 15) / 16;  // + the two zero words
@@ -248,103 +277,295 @@ struct LaneBits {
     }
 };
 
-// one code from the single-symbol tables (global, L2-resident: only segment
-// ends and codes longer than the multi table's index take this path)
-__device__ __forceinline__ uint32_t single_code(const LaneBits& r, const uint32_t* glut, uint32_t Ks) {
-    uint32_t e = glut[static_cast<uint32_t>(r.buf >> (64 - Ks))];
-    uint32_t d = Ks;
-    while (e & kLutPtr) {
-        const uint32_t idx = static_cast<uint32_t>((r.buf >> (56 - d)) & 0xFFu);
-        e = glut[(e & ~kLutPtr) + idx];
-        d += 8;
+// The staged kernels walk the stream one code per lookup in unrolled chunks
+// of 8 (u16 single-symbol table in LDS, as k_decode_fixed; no branch inside a
+// chunk), then settle where the walk should have stopped from the chunk's 8
+// code lengths kept in registers: a data-dependent loop per code (and a slow
+// path per lookup) cost ~40 VALU and ~40 SALU per step in the multi-symbol
+// form this replaces (PMC: 344 K VALU per SIMD per GiB).
+constexpr int kChunkSteps = 8;
+
+// lane cursor over the staged range: 64-bit window, valid bits in the low 6
+// bits of X (X -= entry borrows only above them), refilled unconditionally
+// every two codes (the next dword is read one refill ahead)
+struct Cursor {
+    const uint32_t* w;
+    uint64_t buf;
+    uint32_t X, rp, nextw;
+    __device__ __forceinline__ void init(const Staged& st, uint64_t p) {
+        w = st.w;
+        const uint64_t rel = p - st.base;
+        rp = static_cast<uint32_t>(rel >> 5);
+        const uint32_t sh = static_cast<uint32_t>(rel & 31);
+        buf = static_cast<uint64_t>(__builtin_bswap32(w[rp]) << sh) << 32;
+        X = 32 - sh;
+        rp += 1;
+        nextw = __builtin_bswap32(w[rp]);
     }
-    return e;  // (len << 8) | letter
+    __device__ __forceinline__ void refill() {
+        buf |= (static_cast<uint64_t>(nextw) << 32) >> (X & 63);
+        rp += (X & 32) ? 0u : 1u;
+        X |= 32;
+        nextw = __builtin_bswap32(w[rp]);
+    }
+    // the length of the next code, consumed; codes longer than the table's
+    // index (kSsSlow) through the global multi-level table
+    template <bool SLOW>
+    __device__ __forceinline__ uint32_t step(const uint16_t* stab, uint32_t K, const uint32_t* glut, uint32_t Kg) {
+        uint32_t e = stab[static_cast<uint32_t>(buf >> 32) >> (32 - K)];
+        if (SLOW && (e & kSsSlow)) {
+            refill();
+            uint32_t e1 = glut[static_cast<uint32_t>(buf >> (64 - Kg))];
+            uint32_t d = Kg;
+            while (e1 & kLutPtr) {
+                const uint32_t idx = static_cast<uint32_t>((buf >> (56 - d)) & 0xFFu);
+                e1 = glut[(e1 & ~kLutPtr) + idx];
+                d += 8;
+            }
+            const uint32_t l1 = (e1 >> 8) & 0xFFu;
+            buf <<= l1;
+            X -= l1;
+            refill();
+            return l1;
+        }
+        buf <<= (e & 63u);
+        X -= e;
+        return e & 63u;
+    }
+    template <bool SLOW>
+    __device__ __forceinline__ void chunk(uint32_t (&L)[kChunkSteps], const uint16_t* stab, uint32_t K,
+                                          const uint32_t* glut, uint32_t Kg) {
+#pragma unroll
+        for (int k = 0; k < kChunkSteps; ++k) {
+            if ((k & 1) == 0) refill();
+            L[k] = step<SLOW>(stab, K, glut, Kg);
+        }
+    }
+};
+
+// LDS: [single-symbol table][staged input]
+__device__ __forceinline__ const uint16_t* load_stab(const IndexlessArgs& a, uint32_t* lds) {
+    const uint32_t words = ((1u << a.stab_bits) + 1) / 2;
+    for (uint32_t i = threadIdx.x; i < words; i += blockDim.x) lds[i] = reinterpret_cast<const uint32_t*>(a.stab)[i];
+    return reinterpret_cast<const uint16_t*>(lds);
+}
+__device__ __forceinline__ uint32_t stab_words(const IndexlessArgs& a) {
+    return ((((1u << a.stab_bits) + 1) / 2) + 3) & ~3u;
 }
 
-// LDS: [multi table 1 << K][staged input]
+template <bool SLOW>
 __global__ __launch_bounds__(kThreads) void k_spec_lds(IndexlessArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    const uint32_t K = a.mlut_bits, Ks = a.lut_bits;
-    uint32_t* mlut = lds;
-    for (uint32_t i = threadIdx.x; i < (1u << K); i += blockDim.x) mlut[i] = a.mlut[i];
-    const Staged st = stage_block(a, mlut + (((1u << K) + 3) & ~3u));
+    const uint16_t* stab = load_stab(a, lds);
+    const Staged st = stage_block(a, lds + stab_words(a));
     __syncthreads();
-    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-    if (i >= a.nseg) return;
+    const uint64_t i0 = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    const bool live = i0 < a.nseg;  // no early return: the fix-up below has a barrier
+    const uint64_t i = live ? i0 : a.nseg - 1;
+    const uint32_t K = a.stab_bits, Kg = a.lut_bits;
     const uint64_t B = a.valid_bits;
     const uint64_t start = i * a.seg_bits;
     const uint64_t end = (i + 1 == a.nseg) ? B : (start + a.seg_bits < B ? start + a.seg_bits : B);
-    LaneBits r;
-    r.init(st, start);
-    uint64_t cnt = 0;
-    while (r.pos < end) {
-        r.refill();
-        const uint32_t e = mlut[static_cast<uint32_t>(r.buf >> (64 - K))];
-        const uint32_t used = (e >> 24) & 31u;
-        if (!(e & kMsSlow) && r.pos + used < end) {  // every code of the entry ends before `end`
-            r.consume(used);
-            cnt += e >> 29;
-            continue;
+    Cursor c;
+    c.init(st, start);
+    uint64_t cur = start, cnt = 0;
+    // samples: a boundary of this path at or after every kSampBits bits past
+    // start (a chunk spans < kSampBits bits: at most one per chunk)
+    uint32_t* smp = a.samp + i * a.nsamp;
+    uint32_t next_k = 1;
+    uint64_t next_bit = (a.nsamp && live) ? start + kSampBits : ~0ull;
+    uint64_t sp1 = ~0ull;  // the first sample (position, spec-local index)
+    uint32_t si1 = 0;
+    for (;;) {
+        uint32_t L[kChunkSteps];
+        c.chunk<SLOW>(L, stab, K, a.lut, Kg);
+        // the first boundary at or past `end` inside this chunk?
+        uint64_t p = cur, ex = ~0ull;
+        uint32_t ec = 0;
+#pragma unroll
+        for (int k = 0; k < kChunkSteps; ++k) {
+            p += L[k];
+            const bool hit = ex == ~0ull && p >= end;
+            ex = hit ? p : ex;
+            ec = hit ? static_cast<uint32_t>(k + 1) : ec;
         }
-        const uint32_t len = (single_code(r, a.lut, Ks) >> 8) & 0xFFu;
-        if (r.pos + len > B) {  // an incomplete final code is dropped (comp.rs:493-516)
-            r.pos = B;
+        if (ex != ~0ull) {
+            cnt += ec;
+            if (ex > B) {  // an incomplete final code is dropped (comp.rs:493-516)
+                ex = B;
+                --cnt;
+            }
+            cur = ex;
             break;
         }
-        r.consume(len);
-        ++cnt;
+        cur = p;
+        cnt += kChunkSteps;
+        if (cur >= next_bit) {
+            smp[next_k - 1] = (static_cast<uint32_t>(cnt) << 16) | static_cast<uint32_t>(cur - start);
+            if (next_k == 1) {  // kept for the fix-up below
+                sp1 = cur;
+                si1 = static_cast<uint32_t>(cnt);
+            }
+            next_bit = ++next_k <= a.nsamp ? next_bit + kSampBits : ~0ull;
+        }
     }
-    a.s[i] = start;
-    a.x[i] = r.pos;
+    if (live)
+        for (; next_k <= a.nsamp; ++next_k) smp[next_k - 1] = ~0u;
+
+    // fix-up inside the workgroup, on the staged bits: lane i restarts from
+    // lane i-1's exit (the first lane's predecessor is in another workgroup:
+    // k_fix's rounds) and walks, in branch-free chunks, until it lands on one
+    // of this lane's samples (a boundary of the speculative path: the paths
+    // have merged there; exit unchanged, count and index shift corrected) or
+    // passes the end (a new exit: the successor's check in k_fix catches it).
+    // Walking both paths alternately, one code at a time, cost a third of the
+    // speculative pass in divergent branches.
+    __shared__ uint64_t ex_l[kThreads];
+    ex_l[threadIdx.x] = cur;
+    __syncthreads();
+    uint64_t s_out = start;
+    uint32_t tm_out = 0;
+    int32_t dl_out = 0;
+    const uint64_t ns = threadIdx.x ? ex_l[threadIdx.x - 1] : start;
+    if (ns != start) {
+        Cursor ca_;
+        ca_.init(st, ns);
+        uint64_t pa = ns, na = 0;
+        uint64_t pk = sp1;        // current sample: position, spec-local index
+        uint32_t ik = si1, k = 1;
+        for (;;) {
+            uint32_t L[kChunkSteps];
+            ca_.chunk<SLOW>(L, stab, K, a.lut, Kg);
+            uint64_t p = pa;
+            int hit = -1, ex = -1;
+            uint64_t pex = 0;
+#pragma unroll
+            for (int j = 0; j < kChunkSteps; ++j) {
+                p += L[j];
+                hit = (hit < 0 && ex < 0 && p == pk) ? j : hit;
+                const bool e = ex < 0 && hit < 0 && p >= end;
+                ex = e ? j : ex;
+                pex = e ? p : pex;
+            }
+            if (hit >= 0) {  // merged on the sample: true-local index na + hit + 1
+                const uint64_t t = na + static_cast<uint64_t>(hit) + 1;
+                tm_out = static_cast<uint32_t>(t);
+                dl_out = static_cast<int32_t>(static_cast<int64_t>(t) - static_cast<int64_t>(ik));
+                cnt = static_cast<uint64_t>(static_cast<int64_t>(cnt) + dl_out);
+                break;
+            }
+            if (ex >= 0) {  // a new exit
+                cnt = na + static_cast<uint64_t>(ex) + 1;
+                if (pex > B) {  // an incomplete final code is dropped
+                    pex = B;
+                    --cnt;
+                }
+                cur = pex;
+                tm_out = kNoMerge;
+                break;
+            }
+            pa = p;
+            na += kChunkSteps;
+            while (pa > pk) {  // passed the sample without landing on it: the next one
+                const uint32_t sv = k < a.nsamp ? smp[k] : ~0u;
+                ++k;
+                pk = sv == ~0u ? ~0ull : start + (sv & 0xFFFFu);
+                ik = sv >> 16;
+            }
+        }
+        s_out = ns;
+    }
+    if (!live) return;
+    a.s[i] = s_out;
+    a.x[i] = cur;
     a.c[i] = cnt;
+    a.tm[i] = tm_out;
+    a.dl[i] = dl_out;
 }
 
-// sub_abs[g] = start bit of symbol g << shift, from the settled segments
+// the position `n` codes past the boundary `pos` of the staged range
+template <bool SLOW>
+__device__ __forceinline__ uint64_t walk(const Staged& st, uint64_t pos, uint32_t n, const uint16_t* stab, uint32_t K,
+                                         const uint32_t* glut, uint32_t Kg) {
+    Cursor c;
+    c.init(st, pos);
+    while (n) {
+        uint32_t L[kChunkSteps];
+        c.chunk<SLOW>(L, stab, K, glut, Kg);
+#pragma unroll
+        for (int k = 0; k < kChunkSteps; ++k) pos += static_cast<uint32_t>(k) < n ? L[k] : 0u;
+        n = n > kChunkSteps ? n - kChunkSteps : 0u;
+    }
+    return pos;
+}
+
+// sub_abs[g] = start bit of symbol g << shift, from the settled segments:
+// mark m of segment i (true-local index t) is reached by decoding forward from
+// the true start when t precedes the merge with the speculative path (or the
+// paths never merged), else from the last speculative sample at or before
+// spec-local index t - dl[i]
+template <bool SLOW>
 __global__ __launch_bounds__(kThreads) void k_mark_lds(IndexlessArgs a, const uint64_t* __restrict__ off,
                                                        uint64_t* __restrict__ sub_abs, uint32_t shift) {
-    const uint64_t mask = (1ull << shift) - 1;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    const uint32_t K = a.mlut_bits, Ks = a.lut_bits;
-    uint32_t* mlut = lds;
-    for (uint32_t i = threadIdx.x; i < (1u << K); i += blockDim.x) mlut[i] = a.mlut[i];
-    const Staged st = stage_block(a, mlut + (((1u << K) + 3) & ~3u));
+    const uint16_t* stab = load_stab(a, lds);
+    const Staged st = stage_block(a, lds + stab_words(a));
     __syncthreads();
     const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
     if (i >= a.nseg) return;
-    uint64_t j = off[i];
-    const uint64_t jend = j + a.c[i];
-    if (j == jend) return;
-    LaneBits r;
-    r.init(st, a.s[i]);
-    while (j < jend) {
-        if ((j & mask) == 0) sub_abs[j >> shift] = r.pos;
-        r.refill();
-        const uint32_t e = mlut[static_cast<uint32_t>(r.buf >> (64 - K))];
-        const uint32_t cn = e >> 29;
-        if (!(e & kMsSlow) && (j & mask) + cn <= mask + 1 && j + cn <= jend) {  // no mark inside the entry
-            r.consume((e >> 24) & 31u);
-            j += cn;
-            continue;
+    const uint32_t K = a.stab_bits, Kg = a.lut_bits;
+    const uint64_t j0 = off[i];
+    const uint64_t cnt = a.c[i];
+    const uint64_t step = 1ull << shift;
+    uint64_t m = (j0 + step - 1) & ~(step - 1);
+    if (m >= j0 + cnt) return;
+    const uint64_t s_true = a.s[i];
+    const uint64_t s_spec = i * a.seg_bits;
+    const uint32_t tm = a.tm[i];
+    const int64_t dl = a.dl[i];
+    // the lane's samples, loaded at once (a dependent load per sample tried
+    // cost a memory latency each)
+    uint32_t sv[kSampMax];
+#pragma unroll
+    for (uint32_t k = 0; k < kSampMax; ++k) sv[k] = k < a.nsamp ? a.samp[i * a.nsamp + k] : ~0u;
+    for (; m < j0 + cnt; m += step) {
+        const uint64_t t = m - j0;
+        uint64_t pos;
+        if (tm == kNoMerge || t < tm) {
+            pos = walk<SLOW>(st, s_true, static_cast<uint32_t>(t), stab, K, a.lut, Kg);
+        } else {
+            const uint32_t u = static_cast<uint32_t>(static_cast<int64_t>(t) - dl);
+            uint32_t idx = 0, rel = 0;
+#pragma unroll
+            for (uint32_t k = 0; k < kSampMax; ++k) {  // samples ascend; ~0u never qualifies
+                const bool ok = (sv[k] >> 16) <= u;
+                idx = ok ? sv[k] >> 16 : idx;
+                rel = ok ? sv[k] & 0xFFFFu : rel;
+            }
+            pos = walk<SLOW>(st, s_spec + rel, u - idx, stab, K, a.lut, Kg);
         }
-        r.consume((single_code(r, a.lut, Ks) >> 8) & 0xFFu);
-        ++j;
+        sub_abs[m >> shift] = pos;
     }
 }
 
 }  // namespace
 
 static size_t lds_staged_bytes(const IndexlessArgs& a) {
-    return static_cast<size_t>(((1u << a.mlut_bits) + 3) & ~3u) * 4 + ((kThreads * a.seg_bits + 7) / 8 + 96 + 15) / 16 * 16;
+    return static_cast<size_t>(((((1u << a.stab_bits) + 1) / 2) + 3) & ~3u) * 4 +
+           ((kThreads * a.seg_bits + 7) / 8 + 128 + 15) / 16 * 16;
 }
 
-static bool use_staged(const IndexlessArgs& a) { return a.mlut && a.max_len <= 32 && lds_staged_bytes(a) <= 160 * 1024; }
+static bool use_staged(const IndexlessArgs& a) {
+    return a.stab && a.stab_bits && a.max_len <= 32 && lds_staged_bytes(a) <= 160 * 1024;
+}
 
 hipError_t launch_indexless_mark(const IndexlessArgs& a, const uint64_t* off, uint64_t* sub_abs, uint32_t shift,
                                  hipStream_t st) {
     if (a.nseg == 0) return hipSuccess;
-    if (!use_staged(a)) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_mark_lds, dim3((a.nseg + kThreads - 1) / kThreads), dim3(kThreads), lds_staged_bytes(a), st,
-                       a, off, sub_abs, shift);
+    if (!use_staged(a) || !a.samp) return hipErrorInvalidValue;
+    const bool slow = a.max_len > a.stab_bits;
+    hipLaunchKernelGGL(slow ? k_mark_lds<true> : k_mark_lds<false>, dim3((a.nseg + kThreads - 1) / kThreads),
+                       dim3(kThreads), lds_staged_bytes(a), st, a, off, sub_abs, shift);
     return hipGetLastError();
 }
 
@@ -353,8 +574,10 @@ bool indexless_staged(const IndexlessArgs& a) { return use_staged(a); }
 hipError_t launch_indexless_spec(const IndexlessArgs& a, hipStream_t st) {
     if (a.nseg == 0) return hipSuccess;
     if (use_staged(a)) {
-        hipLaunchKernelGGL(k_spec_lds, dim3((a.nseg + kThreads - 1) / kThreads), dim3(kThreads), lds_staged_bytes(a),
-                           st, a);
+        if (!a.samp) return hipErrorInvalidValue;
+        const bool slow = a.max_len > a.stab_bits;
+        hipLaunchKernelGGL(slow ? k_spec_lds<true> : k_spec_lds<false>, dim3((a.nseg + kThreads - 1) / kThreads),
+                           dim3(kThreads), lds_staged_bytes(a), st, a);
         return hipGetLastError();
     }
     const Seg g = make_seg(a);
@@ -364,21 +587,15 @@ hipError_t launch_indexless_spec(const IndexlessArgs& a, hipStream_t st) {
     return hipGetLastError();
 }
 
-hipError_t launch_indexless_fix(const IndexlessArgs& a, const uint64_t* xin, uint64_t* xout, unsigned int* changed,
-                                hipStream_t st) {
+hipError_t launch_indexless_settle_all(const IndexlessArgs& a, hipStream_t st) {
     if (a.nseg == 0) return hipSuccess;
     const Seg g = make_seg(a);
     const size_t lds = (1u << a.lut_bits) * 4;
-    hipLaunchKernelGGL(k_fix, dim3((a.nseg + kThreads - 1) / kThreads), dim3(kThreads), lds, st, g, a.s, xin, xout,
-                       a.c, changed);
-    return hipGetLastError();
-}
-
-hipError_t launch_indexless_settle(const IndexlessArgs& a, uint64_t* x, hipStream_t st) {
-    if (a.nseg == 0) return hipSuccess;
-    const Seg g = make_seg(a);
-    const size_t lds = (1u << a.lut_bits) * 4;
-    hipLaunchKernelGGL(k_settle, dim3(1), dim3(64), lds, st, g, a.s, x, a.c);
+    // grid-stride rounds: a few resident workgroups per CU cover the segments
+    const uint32_t grid = static_cast<uint32_t>(std::min<uint64_t>((a.nseg + kThreads - 1) / kThreads, 2048));
+    for (int r = 0; r < kFixRounds; ++r)
+        hipLaunchKernelGGL(k_fix, dim3(grid), dim3(kThreads), lds, st, g, a.s, a.x, a.c, a.tm, a.dl, a.flags, r);
+    hipLaunchKernelGGL(k_settle, dim3(1), dim3(64), lds, st, g, a.s, a.x, a.c, a.tm, a.flags);
     return hipGetLastError();
 }
 

@@ -120,7 +120,24 @@ struct IndexlessArgs {
     const uint32_t* mlut;         // multi-symbol table (codes <= 32 bits: the LDS-staged kernels)
     uint32_t mlut_bits;
     uint32_t max_len;
+    // spec samples (LDS-staged path): segment i's slot k-1 (k = 1..nsamp) =
+    // (spec-local symbol index << 16) | (bit offset from i*S) of the first
+    // boundary of its speculative path at or after k*kSampBits; ~0u: none
+    uint32_t* samp;
+    uint32_t nsamp;
+    // how the settled path relates to the speculative one: past true-local
+    // symbol tm[i] they coincide, true-local = spec-local + dl[i]
+    // (tm = kNoMerge: never within the segment)
+    uint32_t* tm;
+    int32_t* dl;
+    unsigned int* flags;          // [kFixRounds]: round r found a changed exit
+    const uint16_t* stab;         // single-symbol table (k_decode_fixed's): the LDS-staged kernels
+    uint32_t stab_bits;
 };
+constexpr uint32_t kSampBits = 128;
+constexpr uint32_t kSampMax = 8;  // samples kept per segment (nsamp <= kSampMax)
+constexpr uint32_t kNoMerge = 0xFFFFFFFFu;
+constexpr int kFixRounds = 4;     // device-side fix-up rounds before the sequential fallback
 
 // dst[i] = map[src[i]] (+ arithmetic restart index)
 struct BytemapArgs {
@@ -224,9 +241,10 @@ hipError_t launch_decode_wave(const DecodeArgs& a, hipStream_t s);
 hipError_t launch_decode_fixed(const DecodeArgs& a, hipStream_t s);
 size_t decode_wave_lds_bytes(uint32_t mlut_bits);
 hipError_t launch_indexless_spec(const IndexlessArgs& a, hipStream_t s);
-hipError_t launch_indexless_fix(const IndexlessArgs& a, const uint64_t* xin, uint64_t* xout, unsigned int* changed,
-                                hipStream_t s);
-hipError_t launch_indexless_settle(const IndexlessArgs& a, uint64_t* x, hipStream_t s);
+// kFixRounds fix-up rounds (each a no-op once the previous one changed
+// nothing), then the sequential sweep only if the last round still changed an
+// exit: no host round trip
+hipError_t launch_indexless_settle_all(const IndexlessArgs& a, hipStream_t s);
 hipError_t launch_indexless_emit(const IndexlessArgs& a, const uint64_t* off, uint8_t* out, hipStream_t s);
 // restart index for the ring decoder: sub_abs[g] = start bit of symbol 256 g
 // sub_abs[g] = start bit of symbol g << shift (shift 8: the ring/wide

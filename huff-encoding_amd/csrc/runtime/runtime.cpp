@@ -818,15 +818,24 @@ Status indexless_sync(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_bytes,
     // codes <= 32 bits take the LDS-staged kernels: 1024-bit segments keep a
     // workgroup's staging at 32 KiB (3 workgroups per CU); longer codes 2048
     const uint64_t seg_target = dt->maxdepth <= 32 ? 1024 : 2048;
-    const uint64_t S = static_cast<uint64_t>(g) * ((seg_target + g - 1) / g);
+    uint64_t S = static_cast<uint64_t>(g) * ((seg_target + g - 1) / g);
+    // the LDS-staged kernels read lane i's bits from dword ~S/32 * i: with an
+    // even dword stride every lane starts on the same few banks (1024 bits: all
+    // 32 lanes of a half-wave on one bank); prefer an odd stride (S = 32 mod 64)
+    for (uint64_t k = (seg_target + g - 1) / g, tries = 0; tries < 128; ++k, ++tries)
+        if ((static_cast<uint64_t>(g) * k) % 64 == 32) {
+            S = static_cast<uint64_t>(g) * k;
+            break;
+        }
     const uint64_t nseg = (valid_bits + S - 1) / S;
     if (nseg > 0xFFFFFFFFull) return Status::err(HUFF_E_INVALID_ARG, "stream too long for one decode");
     HUFF_TRY(st.s.ensure(nseg * 8));
     HUFF_TRY(st.x0.ensure(nseg * 8));
-    HUFF_TRY(st.x1.ensure(nseg * 8));
     HUFF_TRY(st.c.ensure(nseg * 8));
     HUFF_TRY(st.off.ensure((nseg + 1) * 8));
-    HUFF_TRY(st.flag.ensure(4));
+    HUFF_TRY(st.tm.ensure(nseg * 4));
+    HUFF_TRY(st.dl.ensure(nseg * 4));
+    HUFF_TRY(st.flag.ensure(dev::kFixRounds * 4));
     dev::IndexlessArgs& a = st.a;
     a = dev::IndexlessArgs{};
     a.comp = d_comp;
@@ -842,21 +851,25 @@ Status indexless_sync(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_bytes,
     a.mlut = static_cast<const uint32_t*>(ctx->d_lut.p) + dt->moff;
     a.mlut_bits = dt->mbits;
     a.max_len = dt->maxdepth;
+    a.stab = reinterpret_cast<const uint16_t*>(static_cast<const uint32_t*>(ctx->d_lut.p) + dt->soff);
+    a.stab_bits = dt->sbits;
+    a.tm = static_cast<uint32_t*>(st.tm.p);
+    a.dl = static_cast<int32_t*>(st.dl.p);
+    a.flags = static_cast<unsigned int*>(st.flag.p);
     hipStream_t strm = ctx->stream;
-    HIP_TRY(dev::launch_indexless_spec(a, strm));
-    uint64_t* xa = static_cast<uint64_t*>(st.x0.p);
-    uint64_t* xb = static_cast<uint64_t*>(st.x1.p);
-    bool settled = false;
-    for (int it = 0; it < 32 && !settled; ++it) {
-        HIP_TRY(hipMemsetAsync(st.flag.p, 0, 4, strm));
-        HIP_TRY(dev::launch_indexless_fix(a, xa, xb, static_cast<unsigned int*>(st.flag.p), strm));
-        unsigned int changed = 0;
-        HIP_TRY(hipMemcpyAsync(&changed, st.flag.p, 4, hipMemcpyDeviceToHost, strm));
-        HUFF_TRY(ctx->sync());
-        std::swap(xa, xb);
-        settled = changed == 0;
+    if (dev::indexless_staged(a)) {  // speculative samples for the marking pass
+        a.nsamp = std::min<uint32_t>(dev::kSampMax, static_cast<uint32_t>((S - 1) / dev::kSampBits));
+        HUFF_TRY(st.samp.ensure(nseg * a.nsamp * 4 + 4));
+        a.samp = static_cast<uint32_t*>(st.samp.p);
+    } else {  // k_spec leaves the merge record to the fix-up rounds
+        HIP_TRY(hipMemsetAsync(st.tm.p, 0, nseg * 4, strm));
+        HIP_TRY(hipMemsetAsync(st.dl.p, 0, nseg * 4, strm));
     }
-    if (!settled) HIP_TRY(dev::launch_indexless_settle(a, xa, strm));
+    HIP_TRY(hipMemsetAsync(st.flag.p, 0, dev::kFixRounds * 4, strm));
+    HIP_TRY(dev::launch_indexless_spec(a, strm));
+    // fix-up rounds and the sequential fallback decide on the device whether
+    // they have work (no host wait between rounds)
+    HIP_TRY(dev::launch_indexless_settle_all(a, strm));
     HUFF_TRY(st.tsum.ensure((nseg / 1024 + 2) * 8));
     HIP_TRY(dev::launch_scan(static_cast<const uint64_t*>(st.c.p), static_cast<uint32_t>(nseg), 0,
                              static_cast<uint64_t*>(st.off.p), static_cast<uint64_t*>(st.tsum.p), strm));
