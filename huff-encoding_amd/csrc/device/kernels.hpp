@@ -202,6 +202,24 @@ hipError_t launch_wide_decode(const WideDecArgs& a, hipStream_t s);
 hipError_t wide_weights(uint32_t width, const void* d_in, uint64_t n, void* d_sorted, void* d_uniq,
                         uint64_t* d_counts, uint64_t* d_nruns, void* d_tmp, size_t* tmp_bytes, hipStream_t s);
 
+// codes longer than kLongMaxLen (deep.hip): up to 255 bits, kDeepWords
+// left-aligned words per letter
+constexpr uint32_t kDeepWords = 8;
+struct DeepPackArgs;
+struct DeepSerialArgs {
+    const uint8_t* comp;
+    uint64_t comp_bytes;
+    uint64_t valid_bits;
+    const uint32_t* lut;          // multi-level table (primary lut_bits, 8-bit secondaries)
+    uint32_t lut_bits;
+    uint8_t* out;
+    uint64_t cap;
+    unsigned long long* count;
+};
+hipError_t launch_pack_deep(const DeepPackArgs& a, hipStream_t s);
+hipError_t launch_decode_deep(const DecodeArgs& a, hipStream_t s);  // lut, lut_bits, restart index, n, out
+hipError_t launch_decode_deep_serial(const DeepSerialArgs& a, hipStream_t s);
+
 size_t pack_lds_bytes(bool long_codes, uint32_t stage_words);
 uint32_t pack_waves_per_group(bool long_codes);
 size_t decode_lds_bytes(uint32_t lut_bits, uint32_t rep_log2);
@@ -227,6 +245,16 @@ hipError_t launch_hist_row(const unsigned long long* gw, const uint8_t* in, uint
                            hipStream_t s);
 struct alignas(8) CodeLens {
     uint8_t len[256];
+};
+struct DeepPackArgs {
+    CodeLens len;
+    const uint32_t* words;        // [256][kDeepWords] left-aligned codes
+    const uint8_t* in;
+    uint64_t n;
+    const uint64_t* chunk_start;  // [nchunks + 1], bits relative to out bit 0
+    uint32_t nchunks;
+    uint8_t* out;                 // zeroed beforehand (codes are ORed in)
+    uint32_t* sub_bit;            // may be null
 };
 hipError_t launch_chunk_bits(const uint32_t* chunk_hist, uint32_t nchunks, const CodeLens& len, uint64_t* bits,
                              hipStream_t s);

@@ -117,8 +117,8 @@ bool HuffTree::read_codes_u64(uint64_t code[256], uint8_t len[256], uint32_t* ma
             const uint8_t l = nd.letter;
             seen[l] = true;
             true_len[l] = fr.depth;
-            code[l] = fr.depth <= 64 ? fr.code : 0;
-            len[l] = fr.depth <= 64 ? static_cast<uint8_t>(fr.depth) : 0;
+            code[l] = fr.depth <= 64 ? fr.code : 0;  // longer codes: read_codes (bit vectors)
+            len[l] = static_cast<uint8_t>(fr.depth);  // <= 255 (a 256-leaf tree's depth)
             continue;
         }
         st[sp++] = {nd.right, fr.depth + 1, (fr.code << 1) | 1};

@@ -26,6 +26,14 @@ const huff::EncTables& huff_tree::enc_tables() const {
     if (!enc) {
         auto e = std::make_unique<huff::EncTables>();
         e->fits64 = t.read_codes_u64(e->code, e->len, &e->maxlen);
+        if (e->maxlen > huff::dev::kLongMaxLen) {  // deep codes: left-aligned words (deep.hip)
+            std::array<std::vector<uint8_t>, 256> bits;
+            t.read_codes(bits);
+            e->deep.assign(256 * huff::dev::kDeepWords, 0);
+            for (int b = 0; b < 256; ++b)
+                for (size_t k = 0; k < bits[b].size(); ++k)
+                    if (bits[b][k]) e->deep[b * huff::dev::kDeepWords + k / 32] |= 0x80000000u >> (k % 32);
+        }
         enc = std::move(e);
     }
     return *enc;
@@ -151,9 +159,7 @@ Status build_dec_tables(const HuffTree& t, DecTables& out) {
         build_single_table(t, 1, out);
         return Status::ok();
     }
-    const uint32_t maxd = t.max_depth();
-    if (maxd > dev::kLongMaxLen)
-        return Status::err(HUFF_E_CODE_TOO_LONG, "code longer than 57 bits: outside the GPU decoder's range");
+    const uint32_t maxd = t.max_depth();  // > dev::kLongMaxLen: the deep kernels (deep.hip)
     out.maxdepth = maxd;
     {
         uint32_t mind = 255;
@@ -416,7 +422,7 @@ huff::Status huff_enc::bits(const huff_tree* t, uint64_t* total) {
     const huff::EncTables& et = t->enc_tables();
     uint64_t b = 0;
     for (int i = 0; i < 256; ++i) {
-        if (w[i] && et.len[i] == 0 && et.fits64) {
+        if (w[i] && et.len[i] == 0) {
             // compress_with_tree reports the FIRST missing letter in input order
             uint8_t m[256];
             for (int k = 0; k < 256; ++k) m[k] = (w[k] && et.len[k] == 0) ? 1 : 0;
@@ -437,8 +443,6 @@ huff::Status huff_enc::bits(const huff_tree* t, uint64_t* total) {
         }
         b += w[i] * et.len[i];
     }
-    if (!et.fits64 || et.maxlen > huff::dev::kLongMaxLen)
-        return huff::Status::err(HUFF_E_CODE_TOO_LONG, "code longer than 57 bits: outside the GPU encoder's range");
     *total = b;
     return huff::Status::ok();
 }
@@ -486,6 +490,46 @@ huff::Status huff_enc::pack(const huff_tree* t, uint64_t base, const uint8_t* pr
         return huff::dev::launch_scan(static_cast<const uint64_t*>(chunk_bits.p), nchunks, base & 7,
                                       static_cast<uint64_t*>(chunk_start.p), static_cast<uint64_t*>(tsum.p), s);
     }));
+    if (et.maxlen > huff::dev::kLongMaxLen) {  // deep codes (deep.hip): ORed into a zeroed output
+        const uint64_t nb = ((base & 7) + tb + 7) / 8;
+        HIP_TRY(hipMemsetAsync(d_out, 0, nb, s));
+        if ((base & 7) && prev_tail_len) {
+            // the first byte's leading bits end the previous letters' codes
+            // (what k_pack's lane 0 recomputes from prev_tail)
+            uint32_t byte0 = 0;
+            int64_t pos = static_cast<int64_t>(base & 7);
+            for (size_t j = prev_tail_len; j-- > 0 && pos > 0;) {
+                const uint8_t b = prev_tail[j];
+                const int64_t L = et.len[b];
+                if (L == 0) break;
+                for (int64_t q = std::max<int64_t>(pos - L, 0); q < pos; ++q) {
+                    const int64_t k = q - (pos - L);  // code bit index
+                    if ((et.deep[b * huff::dev::kDeepWords + k / 32] >> (31 - k % 32)) & 1u) byte0 |= 0x80u >> q;
+                }
+                pos -= L;
+            }
+            HIP_TRY(hipMemsetAsync(d_out, static_cast<int>(byte0), 1, s));
+        }
+        HUFF_TRY(deep_words.ensure(256 * huff::dev::kDeepWords * 4));
+        HIP_TRY(hipMemcpyAsync(deep_words.p, et.deep.data(), 256 * huff::dev::kDeepWords * 4, hipMemcpyHostToDevice, s));
+        huff::dev::DeepPackArgs d{};
+        d.len = lens;
+        d.words = static_cast<const uint32_t*>(deep_words.p);
+        d.in = d_in;
+        d.n = n;
+        d.chunk_start = static_cast<const uint64_t*>(chunk_start.p);
+        d.nchunks = nchunks;
+        d.out = d_out;
+        d.sub_bit = static_cast<uint32_t*>(sub_bit.p);
+        HUFF_TRY(ctx->timed("pack", [&] { return huff::dev::launch_pack_deep(d, s); }));
+        packed = true;
+        index_pending = false;
+        packed_tree_id = t->id;
+        remember_tree(t);
+        bit_base = base;
+        total_bits = tb;
+        return huff::Status::ok();
+    }
     huff::dev::PackArgs a{};
     if (long_codes)
         for (int b = 0; b < 256; ++b) a.table.l[b] = (et.code[b] << 6) | et.len[b];
@@ -547,6 +591,20 @@ huff::Status huff_enc::decode(const huff_tree* t, const uint8_t* d_comp, uint64_
     }
     HUFF_TRY(ensure_index());
     huff::dev::DecodeArgs a{};
+    if (dt->maxdepth > huff::dev::kLongMaxLen) {  // deep codes (deep.hip)
+        a.comp = d_comp;
+        a.comp_bytes = comp_bytes;
+        a.lut = static_cast<const uint32_t*>(ctx->d_lut.p);
+        a.lut_bits = dt->bits;
+        a.chunk_start = static_cast<const uint64_t*>(chunk_start.p);
+        a.sub_bit = static_cast<const uint32_t*>(sub_bit.p);
+        a.nchunks = nchunks;
+        a.n = n;
+        a.out = d_out;
+        HUFF_TRY(ctx->timed("decode", [&] { return huff::dev::launch_decode_deep(a, ctx->stream); }));
+        HIP_TRY(hipEventRecord(ctx->lut_free, ctx->stream));
+        return huff::Status::ok();
+    }
     a.comp = d_comp;
     a.comp_bytes = comp_bytes;
     a.lut = static_cast<const uint32_t*>(ctx->d_lut.p);
@@ -630,6 +688,7 @@ void huff_enc::remember_tree(const huff_tree* t) {
     const huff::EncTables& et = t->enc_tables();
     std::memcpy(packed_len, et.len, sizeof packed_len);
     std::memcpy(packed_code, et.code, sizeof packed_code);
+    packed_deep = et.deep;
     packed_any_tree = false;
 }
 
@@ -637,7 +696,7 @@ bool huff_enc::codes_match(const huff_tree* t) const {
     if (packed_any_tree) return true;
     const huff::EncTables& et = t->enc_tables();
     return std::memcmp(packed_len, et.len, sizeof packed_len) == 0 &&
-           std::memcmp(packed_code, et.code, sizeof packed_code) == 0;
+           std::memcmp(packed_code, et.code, sizeof packed_code) == 0 && packed_deep == et.deep;
 }
 
 // ---------------------------------------------------------------------------
@@ -914,6 +973,32 @@ Status decode_indexless_dev(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_
         m.n = n;
         for (int b = 0; b < 256; ++b) m.map[b] = static_cast<uint8_t>(dt->lut[b]);
         HIP_TRY(dev::launch_bytemap(m, ctx->stream));
+        return Status::ok();
+    }
+    if (dt->maxdepth > dev::kLongMaxLen) {  // deep codes: one lane walks the stream (deep.hip)
+        DevBuf& cnt = ctx->idx_sub_abs;
+        HUFF_TRY(cnt.ensure(8));
+        dev::DeepSerialArgs d{};
+        d.comp = d_comp;
+        d.comp_bytes = comp_bytes;
+        d.valid_bits = valid_bits;
+        d.lut = static_cast<const uint32_t*>(ctx->d_lut.p);
+        d.lut_bits = dt->bits;
+        d.out = d_user;
+        d.cap = d_user ? user_cap : 0;
+        d.count = static_cast<unsigned long long*>(cnt.p);
+        HIP_TRY(dev::launch_decode_deep_serial(d, ctx->stream));  // counts (and writes, when d_user is given)
+        uint64_t total = 0;
+        HIP_TRY(hipMemcpyAsync(&total, cnt.p, 8, hipMemcpyDeviceToHost, ctx->stream));
+        HUFF_TRY(ctx->sync());
+        *nsym = total;
+        HUFF_TRY(out_ptr(total));
+        if (!d_user) {  // into `out`, now that its size is known
+            d.out = static_cast<uint8_t*>(out.p);
+            d.cap = total;
+            HIP_TRY(dev::launch_decode_deep_serial(d, ctx->stream));
+        }
+        HIP_TRY(hipEventRecord(ctx->lut_free, ctx->stream));
         return Status::ok();
     }
     IndexlessSync& st = ctx->indexless_ws();

@@ -30,10 +30,13 @@ inline Status hip_status(hipError_t e, const char* what) {
 
 // Encode/decode tables derived from a tree (built once per tree, cached).
 struct EncTables {
-    uint64_t code[256];
-    uint8_t len[256];
+    uint64_t code[256];           // codes <= 64 bits (right-aligned); 0 for longer ones
+    uint8_t len[256];             // every code's length (0: letter absent)
     uint32_t maxlen = 0;
     bool fits64 = true;
+    // maxlen > dev::kLongMaxLen: every code left-aligned in dev::kDeepWords
+    // words per letter (deep.hip)
+    std::vector<uint32_t> deep;
 };
 
 struct DecTables {
@@ -154,6 +157,7 @@ struct huff_enc {
     uint64_t n = 0;
     uint32_t nchunks = 0;
     DevBuf chunk_hist, gw, chunk_bits, chunk_start, tsum, sub_bit, mask, pos;
+    DevBuf deep_words;  // codes longer than 57 bits (deep.hip)
     uint64_t w[256] = {};
     bool have_hist = false;
     // state of the last pack (for decode)
@@ -163,6 +167,7 @@ struct huff_enc {
     // index was uploaded): decode refuses a tree with other codes
     uint8_t packed_len[256] = {};
     uint64_t packed_code[256] = {};
+    std::vector<uint32_t> packed_deep;  // deep codes' words (EncTables::deep)
     bool packed_any_tree = false;  // an index uploaded without a tree
     void remember_tree(const huff_tree* t);
     bool codes_match(const huff_tree* t) const;

@@ -42,7 +42,9 @@ enum huff_status {
     HUFF_E_FROM_BIN = 4,        /* FromBinError tree_inner.rs:530-590                     */
     HUFF_E_FROM_BYTES = 5,      /* CompressedDataFromBytesError comp.rs:128-184           */
     HUFF_E_BUFFER_TOO_SMALL = 6,/* caller buffer too small; *_len outputs hold the need   */
-    HUFF_E_CODE_TOO_LONG = 7,   /* a code longer than the GPU path's 57-bit limit         */
+    HUFF_E_CODE_TOO_LONG = 7,   /* a code too long for the requested view (u64 code table, */
+                                /* wide letters' kernels); byte-path compress/decompress  */
+                                /* take any length (deep.hip)                             */
     HUFF_E_HIP = 8,             /* HIP runtime error (message has the HIP error string)   */
     HUFF_E_IO = 9,              /* ErrorKind::Io huff/src/error.rs                         */
     HUFF_E_UNRECOGNIZED = 10,   /* ErrorKind::UnrecognizedFormat                           */

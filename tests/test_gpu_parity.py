@@ -135,6 +135,62 @@ def test_long_codes(H, O, ctx):
     assert H.decompress(H.CompressData.try_from_bytes(cd.to_bytes()), ctx) == data
 
 
+def _fib_tree(H, O, nletters, seed):
+    f = [1, 1]
+    while len(f) < nletters:
+        f.append(f[-1] + f[-2])
+    rng = np.random.default_rng(seed)
+    w = np.zeros(256, np.uint64)
+    # letter 0 left out: its iterator quirk double-counts a
+    # weight and the tree is no longer a chain
+    letters = rng.choice(np.arange(1, 256), nletters, replace=False)
+    w[letters] = np.array(f, dtype=np.uint64)
+    return (H.HuffTree.from_weights(H.ByteWeights.from_array(w)), O.Tree.from_weights(O.weights_from_array(w)),
+            letters, rng)
+
+
+@pytest.mark.parametrize("nletters", [62, 75])
+def test_deep_codes(H, O, ctx, nletters):
+    """codes longer than 57 bits (deep.hip): 62 Fibonacci-weighted letters
+    give 61-bit codes, 75 give 74-bit codes (past u64; the weights stay
+    below 2^53, exact in every representation); the reference encodes
+    any depth (tree_inner.rs:422-440, comp.rs:419-451). Byte-exact against the
+    bit-serial oracle through the host API, the index-free decoder of a
+    to_bytes container, and the device job (restart index decode)"""
+    import torch
+
+    t, ot, letters, rng = _fib_tree(H, O, nletters, 40 + nletters)
+    maxlen = max(len(v) for v in ot.codes().values())
+    assert maxlen > 57
+    # mostly the deep letters, so every round of the packer meets long codes
+    deep_letters = [k for k, v in ot.codes().items() if len(v) > 40]
+    data = np.where(rng.random(200_003) < 0.5, rng.choice(deep_letters, 200_003),
+                    rng.choice(letters, 200_003)).astype(np.uint8).tobytes()
+    cd = H.compress_with_tree(data, t, ctx)
+    comp, pad = O.compress_with_tree(data, ot)
+    assert cd.comp_bytes() == comp and cd.padding_bits() == pad
+    assert H.decompress(cd, ctx) == data
+    assert H.decompress(H.CompressData.try_from_bytes(cd.to_bytes()), ctx) == data
+    assert cd.to_bytes() == O.to_bytes(comp, pad, ot)
+    # the device job at a non-zero bit base with the previous letters' tail
+    n = len(data)
+    x = torch.from_numpy(np.frombuffer(data, np.uint8).copy()).cuda()
+    seg = torch.empty(n - 1000 + 64, dtype=torch.uint8, device="cuda")
+    seg[: n - 1000] = x[1000:]
+    job = H.EncodeJob(ctx, seg.data_ptr(), n - 1000)
+    job.hist()
+    base = int(sum(len(ot.codes()[b]) for b in data[:1000]))
+    bits = job.bits(t)
+    out = torch.zeros((base % 8 + bits + 7) // 8 + 64, dtype=torch.uint8, device="cuda")
+    job.pack(t, out.data_ptr(), out.numel(), bit_base=base, prev_tail=data[992:1000])
+    dec = torch.empty(n - 1000 + 64, dtype=torch.uint8, device="cuda")
+    job.decode(t, out.data_ptr(), dec.data_ptr())
+    torch.cuda.synchronize()
+    assert dec[: n - 1000].cpu().numpy().tobytes() == data[1000:]
+    got = out[: (base % 8 + bits + 7) // 8].cpu().numpy().tobytes()
+    assert got == comp[base // 8:]
+
+
 def test_missing_letter(H, ctx):
     t = H.HuffTree.from_weights(H.ByteWeights.from_bytes(b"abb", ctx))
     with pytest.raises(H.CompressError) as e:
