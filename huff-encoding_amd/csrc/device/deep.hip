@@ -17,6 +17,9 @@
 //                  every level, so any depth resolves;
 //  k_decode_deep_serial : streams without an index (reference-written bytes,
 //                  .hff files): one lane walks the whole stream.
+// Two small helpers of the file path's windowed decode live here too, as they
+// walk codes of any length: k_walk_end (the end of a window's last complete
+// code) and k_shift_bits (realign a window that starts inside a byte).
 #include "bitreader.hpp"
 
 namespace huff::dev {
@@ -135,9 +138,48 @@ __global__ void k_decode_deep_serial(DeepSerialArgs a) {
         pos += len;
     }
     *a.count = n;
+    if (a.end) *a.end = pos;
+}
+
+// the bit after `count` codes from the boundary *start (or start_v when
+// start is null): the end of a window's last complete code, for the file
+// path's windowed decode
+__global__ void k_walk_end(WalkEndArgs a) {
+    extern __shared__ uint32_t prim[];
+    for (uint32_t i = threadIdx.x; i < (1u << a.lut_bits); i += blockDim.x) prim[i] = a.lut[i];
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    const BitSrc src{reinterpret_cast<const uint32_t*>(a.comp), a.comp, a.comp_bytes};
+    uint64_t pos = a.start ? *a.start : a.start_v;
+    const uint64_t cnt = a.count ? *a.count : a.count_v;
+    for (uint64_t j = 0; j < cnt; ++j) pos += (deep_lookup(src, prim, a.lut_bits, a.lut, pos) >> 8) & 0xFFu;
+    *a.end = pos;
+}
+
+// dst[i] = the 8 stream bits starting at bit r of src[i] (a window that
+// starts inside a byte, realigned to bit 0)
+__global__ void k_shift_bits(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, uint64_t n, uint32_t r) {
+    for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
+         i += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
+        const uint32_t hi = src[i], lo = i + 1 < n ? src[i + 1] : 0u;
+        dst[i] = static_cast<uint8_t>((hi << r) | (lo >> (8 - r)));
+    }
 }
 
 }  // namespace
+
+hipError_t launch_walk_end(const WalkEndArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(k_walk_end, dim3(1), dim3(64), (1u << a.lut_bits) * 4, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_shift_bits(const uint8_t* src, uint8_t* dst, uint64_t n, uint32_t r, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const uint64_t want = (n + 255) / 256;
+    hipLaunchKernelGGL(k_shift_bits, dim3(static_cast<uint32_t>(want < 8192 ? want : 8192)), dim3(256), 0, s, src,
+                       dst, n, r);
+    return hipGetLastError();
+}
 
 hipError_t launch_pack_deep(const DeepPackArgs& a, hipStream_t s) {
     if (a.nchunks == 0) return hipSuccess;

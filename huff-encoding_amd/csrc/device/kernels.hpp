@@ -215,7 +215,21 @@ struct DeepSerialArgs {
     uint8_t* out;
     uint64_t cap;
     unsigned long long* count;
+    unsigned long long* end;      // may be null: the bit after the last complete code
 };
+struct WalkEndArgs {
+    const uint8_t* comp;
+    uint64_t comp_bytes;
+    const uint32_t* lut;
+    uint32_t lut_bits;
+    const uint64_t* start;        // device value, or start_v when null
+    uint64_t start_v;
+    const uint64_t* count;        // device value, or count_v when null
+    uint64_t count_v;
+    unsigned long long* end;
+};
+hipError_t launch_walk_end(const WalkEndArgs& a, hipStream_t s);
+hipError_t launch_shift_bits(const uint8_t* src, uint8_t* dst, uint64_t n, uint32_t r, hipStream_t s);
 hipError_t launch_pack_deep(const DeepPackArgs& a, hipStream_t s);
 hipError_t launch_decode_deep(const DecodeArgs& a, hipStream_t s);  // lut, lut_bits, restart index, n, out
 hipError_t launch_decode_deep_serial(const DeepSerialArgs& a, hipStream_t s);

@@ -400,6 +400,18 @@ huff::Status huff_enc::hist() {
     return huff::Status::ok();
 }
 
+huff::Status huff_enc::hist_known(const uint64_t counts[256]) {
+    HUFF_TRY(ctx->activate());
+    std::memcpy(w, counts, sizeof w);
+    have_hist = true;
+    packed = false;
+    if (nchunks == 0) return huff::Status::ok();
+    return ctx->timed("hist", [&] {
+        return huff::dev::launch_hist(d_in, 0, n, nchunks, static_cast<uint32_t*>(chunk_hist.p),
+                                      static_cast<unsigned long long*>(gw.p), ctx->stream);
+    });
+}
+
 huff::Status huff_enc::hist_row(long long* d_row) {
     HUFF_TRY(ctx->activate());
     hipStream_t s = ctx->stream;
@@ -945,7 +957,8 @@ Status indexless_mark(huff_ctx* ctx, IndexlessSync& st, DevBuf& sub_abs, uint32_
 }
 
 Status decode_indexless_dev(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_bytes, uint64_t valid_bits,
-                            const huff_tree* t, DevBuf& out, uint64_t* nsym, uint8_t* d_user, size_t user_cap) {
+                            const huff_tree* t, DevBuf& out, uint64_t* nsym, uint8_t* d_user, size_t user_cap,
+                            unsigned long long* d_end) {
     *nsym = 0;
     // the output goes to d_user when given (capacity checked once the count
     // is known), else into `out`
@@ -963,9 +976,26 @@ Status decode_indexless_dev(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_
     HUFF_TRY(ctx->activate());
     const DecTables* dt = nullptr;
     HUFF_TRY(ctx->upload_dec_tables(t, &dt));
+    // the window end (d_end): `count` codes walked from a known boundary
+    auto walk_end = [&](const uint64_t* start, uint64_t start_v, const uint64_t* count, uint64_t count_v) -> Status {
+        if (!d_end) return Status::ok();
+        dev::WalkEndArgs w{};
+        w.comp = d_comp;
+        w.comp_bytes = comp_bytes;
+        w.lut = static_cast<const uint32_t*>(ctx->d_lut.p);
+        w.lut_bits = dt->bits;
+        w.start = start;
+        w.start_v = start_v;
+        w.count = count;
+        w.count_v = count_v;
+        w.end = d_end;
+        HIP_TRY(dev::launch_walk_end(w, ctx->stream));
+        return Status::ok();
+    };
     if (dt->all8 && !fixed8_disabled()) {  // every code 8 bits: one symbol per whole byte
         const uint64_t n = valid_bits / 8;
         *nsym = n;
+        HUFF_TRY(walk_end(nullptr, 8 * n, nullptr, 0));
         HUFF_TRY(out_ptr(n));
         dev::BytemapArgs m{};
         m.src = d_comp;
@@ -987,6 +1017,7 @@ Status decode_indexless_dev(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_
         d.out = d_user;
         d.cap = d_user ? user_cap : 0;
         d.count = static_cast<unsigned long long*>(cnt.p);
+        d.end = d_end;
         HIP_TRY(dev::launch_decode_deep_serial(d, ctx->stream));  // counts (and writes, when d_user is given)
         uint64_t total = 0;
         HIP_TRY(hipMemcpyAsync(&total, cnt.p, 8, hipMemcpyDeviceToHost, ctx->stream));
@@ -1006,6 +1037,7 @@ Status decode_indexless_dev(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_
     HUFF_TRY(indexless_sync(ctx, d_comp, comp_bytes, valid_bits, t, st));
     const uint64_t total = st.total;
     *nsym = total;
+    if (total == 0) HUFF_TRY(walk_end(nullptr, 0, nullptr, 0));
     HUFF_TRY(out_ptr(total));
     hipStream_t strm = ctx->stream;
     const bool aligned16 = !(reinterpret_cast<uintptr_t>(d_comp) & 15) && !(reinterpret_cast<uintptr_t>(out_at()) & 15);
@@ -1013,6 +1045,8 @@ Status decode_indexless_dev(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_
         // a restart point every 64 symbols, then the fixed-count decoder
         DevBuf& sub_abs = ctx->idx_sub_abs;
         HUFF_TRY(indexless_mark(ctx, st, sub_abs, 6));
+        const uint64_t m = ((total - 1) >> 6) << 6;  // the last mark: symbol m
+        HUFF_TRY(walk_end(static_cast<const uint64_t*>(sub_abs.p) + (m >> 6), 0, nullptr, total - m));
         dev::DecodeArgs d{};
         d.comp = d_comp;
         d.comp_bytes = comp_bytes;
@@ -1035,6 +1069,8 @@ Status decode_indexless_dev(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_
         return Status::ok();
     }
     HIP_TRY(dev::launch_indexless_emit(st.a, static_cast<const uint64_t*>(st.off.p), out_at(), strm));
+    if (total)  // the last segment's codes from its settled start
+        HUFF_TRY(walk_end(st.a.s + st.a.nseg - 1, 0, st.a.c + st.a.nseg - 1, 0));
     HIP_TRY(hipEventRecord(ctx->lut_free, strm));
     return Status::ok();
 }

@@ -179,6 +179,9 @@ struct huff_enc {
 
     huff::Status init(huff_ctx* c, const uint8_t* d, uint64_t nbytes);
     huff::Status hist();
+    // pass 1 when the counts are already known (the file path's second pass):
+    // the per-chunk rows only, no host wait
+    huff::Status hist_known(const uint64_t counts[256]);
     // pass 1 without a host wait: weights + tail bytes as a device row (see
     // huff_enc_hist_row); the weights reach the host with the exchanged rows
     huff::Status hist_row(long long* d_row);
@@ -205,7 +208,9 @@ Status run_checked_decode(huff_ctx* ctx, dev::DecodeArgs& a, const std::function
 // symbols land in `out` (grown as needed), their count in *nsym
 Status decode_indexless_dev(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_bytes, uint64_t valid_bits,
                             const huff_tree* t, DevBuf& out, uint64_t* nsym, uint8_t* d_user = nullptr,
-                            size_t user_cap = 0);
+                            size_t user_cap = 0, unsigned long long* d_end = nullptr);
+// (d_end, device: the bit after the last complete code, for a window of a
+// longer stream)
 // the self-synchronising part of the index-free decode (spec, fix, scan):
 // symbol offsets per segment in `off`, the symbol count in `total`
 struct IndexlessSync {

@@ -577,6 +577,31 @@ def test_file_path_matches_cli(H, O, ctx, golden):
             H.read_compress_write(empty, empty + ".hff", 100, ctx)
 
 
+@pytest.mark.parametrize("window", [256, 1000, 4099, 65536])
+def test_file_path_windows(H, O, ctx, window, monkeypatch):
+    """the windowed .hff decompress (filepath.cpp): HUFF_FILE_WINDOW shrinks
+    the payload window so a file crosses many windows, each ending inside a
+    code (carried to the next window, realigned when it starts inside a
+    byte). Multi-block files (the bug-compatible stitching) and a tree deeper
+    than 57 bits (the serial deep walk) included; outputs equal the oracle's
+    CLI decompress (huff/src/comp.rs:205-283)"""
+    monkeypatch.setenv("HUFF_FILE_WINDOW", str(window))
+    _, _, letters, rng = _fib_tree(H, O, 70, 7)
+    deep = rng.choice(letters, 40_000).astype(np.uint8)
+    with tempfile.TemporaryDirectory() as d:
+        cases = [(O.gen_text(21, 200_000), 200_000 + 5), (O.gen_zipf(22, 150_000), 150_000),
+                 (O.gen_text(23, 90_000), 7_000), (deep, 40_000)]
+        for k, (src, bs) in enumerate(cases):
+            src = bytes(src)
+            p = os.path.join(d, f"w{k}")
+            open(p, "wb").write(src)
+            H.read_compress_write(p, p + ".hff", bs, ctx)
+            blob = open(p + ".hff", "rb").read()
+            assert blob == O.cli_compress(src, bs), k
+            H.read_decompress_write(p + ".hff", p + ".out", bs, ctx)
+            assert open(p + ".out", "rb").read() == O.cli_decompress(blob, bs), (k, window)
+
+
 def test_hist_row_and_device_exchange(H, O, ctx):
     """the sharded pass 1 without a host round trip: huff_enc_hist_row's
     device row (weights | tail bytes | count) equals the oracle, and the
