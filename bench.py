@@ -304,6 +304,20 @@ def run_workload(s: Setup, kind: str, n: int, with_cpu: bool):
     torch.cuda.synchronize()
     t_dec = s.max_over_ranks(time.perf_counter() - t0)
 
+    # index-free decode (huff_dev_decompress, comp.rs:487-519): the same
+    # stream as the reference holds it, without the restart index
+    comp_bytes = (bits + 7) // 8
+    pad = (8 - bits % 8) % 8
+    got = D.decompress_dev(ctx, tree, state["out"].data_ptr(), comp_bytes, pad, dec.data_ptr(), n + 64)
+    torch.cuda.synchronize()
+    assert got == n and (args.no_verify or torch.equal(dec[:n], x[:n])), "index-free decode != x"
+    s.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        D.decompress_dev(ctx, tree, state["out"].data_ptr(), comp_bytes, pad, dec.data_ptr(), n + 64)
+    torch.cuda.synchronize()
+    t_idx = s.max_over_ranks(time.perf_counter() - t0)
+
     _, ln = tree.code_table()  # letters present in the input are exactly those with a code
     present = np.asarray(ln) > 0
     fixed8 = bool((ln[present] == 8).all()) and os.environ.get("HUFF_DISABLE_FIXED8", "0") in ("", "0")
@@ -311,7 +325,6 @@ def run_workload(s: Setup, kind: str, n: int, with_cpu: bool):
     dec_kernel = "k_decode" if maxlen > 32 else "k_decode_fixed"
     ms_per_step = elapsed * 1e3 / args.steps
     value = world * n / (elapsed / args.steps) / 1e9
-    comp_bytes = (bits + 7) // 8
     nchunks = (n + 65535) // 65536
     algo = {  # algorithmic bytes per launch
         "hist": n,
@@ -369,7 +382,11 @@ def run_workload(s: Setup, kind: str, n: int, with_cpu: bool):
         "e2e": {"encode_GBps": round(world * n / (t_enc / args.steps) / 1e9, 1),
                 "decode_GBps": round(world * n / (t_dec / args.steps) / 1e9, 1),
                 "encode_ms": round(t_enc * 1e3 / args.steps, 4), "decode_ms": round(t_dec * 1e3 / args.steps, 4),
-                "note": "encode = pass 1 + host tree + pass 2 (+ the collective at N>1); decode = restart-index decode"},
+                "indexfree_decode_GBps": round(world * n / (t_idx / args.steps) / 1e9, 1),
+                "indexfree_decode_ms": round(t_idx * 1e3 / args.steps, 4),
+                "note": "encode = pass 1 + host tree + pass 2 (+ the collective at N>1); decode = restart-index "
+                        "decode; indexfree = huff_dev_decompress of the bare stream (spec/fix/scan/mark/decode, "
+                        "one host read of the symbol count)"},
         "kernel_enc_GBps": round(n / (enc_ms * 1e-3) / 1e9, 1),
         "host_gap_ms": round(ms_per_step - sum(k["avg_ms"] for k in kernels.values()), 4),
         "kernel_dec_GBps": kernels.get("decode", {}).get("GBps"),
@@ -381,6 +398,67 @@ def run_workload(s: Setup, kind: str, n: int, with_cpu: bool):
     del x, dec, state, job
     torch.cuda.empty_cache()
     return r
+
+
+def file_path_bench(s: Setup, kind: str, n: int, steps: int):
+    """the .hff file path (huff_file_compress /
+    huff_file_decompress = read_compress_write / read_decompress_write,
+    huff/src/comp.rs:32-280) on an n-byte file in the page cache: wall time
+    of each call, file reads, PCIe copies and file writes included. The CLI's
+    default -b 2G (one block) round-trips; -b 256Mi exercises the pipelined
+    multi-block compress, whose output is the reference's bug-compatible
+    stitching (decodable only when every block's padding is 0 or 4, SURVEY
+    App. C.3), so its round trip is reported, not asserted."""
+    import shutil
+    import tempfile
+
+    x, _ = make_input(s, kind, n)
+    host = x[:n].cpu().numpy()
+    del x
+    torch.cuda.empty_cache()
+    d = tempfile.mkdtemp(prefix="huffbench")
+    try:
+        p = os.path.join(d, "in")
+        host.tofile(p)
+        res = {"file_bytes": n, "workload": f"{human(n)} {kind} file", "steps": steps,
+               "how": "wall time of one library call, file in the page cache, best of the timed steps"}
+        # the host's own page-cache rates on the same file (numpy, one thread)
+        t0 = time.perf_counter()
+        np.fromfile(p, np.uint8)
+        t1 = time.perf_counter()
+        host.tofile(p + ".copy")
+        t2 = time.perf_counter()
+        os.remove(p + ".copy")
+        res["host_io"] = {"read_GBps": round(n / (t1 - t0) / 1e9, 3), "write_GBps": round(n / (t2 - t1) / 1e9, 3),
+                          "how": "np.fromfile / ndarray.tofile of the same 1 GiB, one thread"}
+        for bs, name in ((2_000_000_000, "b2G"), (256 << 20, "b256Mi")):
+            tc, td = [], []
+            for i in range(steps + 1):
+                for f in (p + ".hff", p + ".out"):  # new files, as the CLI writes (not a truncation)
+                    if os.path.exists(f):
+                        os.remove(f)
+                t0 = time.perf_counter()
+                H.read_compress_write(p, p + ".hff", bs, s.ctx)
+                t1 = time.perf_counter()
+                try:
+                    H.read_decompress_write(p + ".hff", p + ".out", bs, s.ctx)
+                except H.HuffError as e:  # the stitched multi-block stream may not decode (as in the reference)
+                    if name == "b2G":
+                        raise
+                    res[name + "_decompress_error"] = str(e)
+                t2 = time.perf_counter()
+                if i:
+                    tc.append(t1 - t0)
+                    td.append(t2 - t1)
+            same = os.path.getsize(p + ".out") == n and np.array_equal(np.fromfile(p + ".out", np.uint8), host)
+            if name == "b2G":
+                assert same, "file round trip != input"
+            res[name] = {"compress_GBps": round(n / min(tc) / 1e9, 3), "decompress_GBps": round(n / min(td) / 1e9, 3),
+                         "compress_ms": round(min(tc) * 1e3, 2), "decompress_ms": round(min(td) * 1e3, 2),
+                         "hff_bytes": os.path.getsize(p + ".hff"), "roundtrip_equal": bool(same)}
+        return res
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
 
 
 def main():
@@ -395,6 +473,8 @@ def main():
     ap.add_argument("--side", default="zipf", choices=["zipf", "text", "none"],
                     help="N=1: a second workload reported under 'side' (configs[2] by default)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--file-path", default="zipf", choices=["zipf", "text", "uniform", "none"],
+                    help="N=1: time the .hff file path on a 1 GiB file of this workload")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
@@ -419,6 +499,8 @@ def main():
     result = run_workload(s, args.workload, n, with_cpu)
     if world == 1 and args.side != "none" and args.side != args.workload:
         result["side"] = {args.side: run_workload(s, args.side, n, with_cpu)}
+    if world == 1 and args.file_path != "none":
+        result["file_path"] = file_path_bench(s, args.file_path, n, 2)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if s.comm is not None:

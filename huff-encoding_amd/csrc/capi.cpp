@@ -84,6 +84,7 @@ int huff_ctx_destroy(huff_ctx* ctx) {
     if (!ctx) return HUFF_OK;
     hipSetDevice(ctx->device);
     hipStreamSynchronize(ctx->stream);
+    ctx->file_ws.reset();
     for (auto& p : ctx->pending) {
         hipEventDestroy(p.a);
         hipEventDestroy(p.b);

@@ -111,6 +111,7 @@ struct DevBuf {
 
 namespace huff {
 struct IndexlessSync;
+struct FileWs;
 }
 
 struct huff_ctx {
@@ -132,6 +133,9 @@ struct huff_ctx {
     std::shared_ptr<huff::IndexlessSync> idx_ws;
     DevBuf idx_sub_abs;
     huff::IndexlessSync& indexless_ws();
+    // the .hff file path's pinned pieces and device buffers (filepath.cpp),
+    // kept across calls: pinning ~0.5 GB per call costs more than the copies
+    std::shared_ptr<huff::FileWs> file_ws;
     uint64_t lut_tree_id = 0;
 
     // kernel timing

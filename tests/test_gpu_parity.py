@@ -577,15 +577,19 @@ def test_file_path_matches_cli(H, O, ctx, golden):
             H.read_compress_write(empty, empty + ".hff", 100, ctx)
 
 
-@pytest.mark.parametrize("window", [256, 1000, 4099, 65536])
-def test_file_path_windows(H, O, ctx, window, monkeypatch):
-    """the windowed .hff decompress (filepath.cpp): HUFF_FILE_WINDOW shrinks
-    the payload window so a file crosses many windows, each ending inside a
-    code (carried to the next window, realigned when it starts inside a
-    byte). Multi-block files (the bug-compatible stitching) and a tree deeper
-    than 57 bits (the serial deep walk) included; outputs equal the oracle's
-    CLI decompress (huff/src/comp.rs:205-283)"""
+@pytest.mark.parametrize("window,piece", [(256, 4096), (1000, 5000), (4099, 65536), (65536, 1 << 20)])
+def test_file_path_windows(H, O, ctx, window, piece, monkeypatch):
+    """the streamed .hff path (filepath.cpp): HUFF_FILE_PIECE shrinks the
+    compress pieces (a block split into pieces that pack at their bit offset
+    with the previous piece's tail; pass-1 rows per ration share) and
+    HUFF_FILE_WINDOW the decompress windows, so a file crosses many windows,
+    each ending inside a code (carried to the next window, realigned when it
+    starts inside a byte). Multi-block files (the bug-compatible stitching)
+    and a tree deeper than 57 bits (deep pack, serial deep walk) included;
+    outputs equal the oracle's CLI compress / decompress
+    (huff/src/comp.rs:32-283)"""
     monkeypatch.setenv("HUFF_FILE_WINDOW", str(window))
+    monkeypatch.setenv("HUFF_FILE_PIECE", str(piece))
     _, _, letters, rng = _fib_tree(H, O, 70, 7)
     deep = rng.choice(letters, 40_000).astype(np.uint8)
     with tempfile.TemporaryDirectory() as d:
@@ -600,6 +604,25 @@ def test_file_path_windows(H, O, ctx, window, monkeypatch):
             assert blob == O.cli_compress(src, bs), k
             H.read_decompress_write(p + ".hff", p + ".out", bs, ctx)
             assert open(p + ".out", "rb").read() == O.cli_decompress(blob, bs), (k, window)
+
+
+def test_file_path_large(H, O, ctx):
+    """a 40 MiB file: pieces and windows of the default 64 MiB, reads and
+    writes split over the I/O threads (>= 16 MiB), -b 2G (one block) and
+    -b 10Mi (four stitched blocks, several pieces); byte-equal to the
+    oracle's CLI compress and decompress"""
+    src = O.gen_zipf(5, 40 << 20)
+    with tempfile.TemporaryDirectory() as d:
+        p = os.path.join(d, "big")
+        src.tofile(p)
+        src = src.tobytes()
+        for bs in (2_000_000_000, 10 << 20):
+            H.read_compress_write(p, p + ".hff", bs, ctx)
+            blob = open(p + ".hff", "rb").read()
+            assert blob == O.cli_compress(src, bs), bs
+            H.read_decompress_write(p + ".hff", p + ".out", bs, ctx)
+            got = open(p + ".out", "rb").read()
+            assert got == (src if bs > len(src) else O.cli_decompress(blob, bs)), bs
 
 
 def test_hist_row_and_device_exchange(H, O, ctx):
