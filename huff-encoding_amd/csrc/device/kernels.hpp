@@ -21,7 +21,7 @@ constexpr uint32_t kChunk = 65536;      // input bytes (= symbols) per chunk / w
 constexpr uint32_t kRound = 4096;       // bytes per workgroup round (256 lanes x 16 B)
 constexpr uint32_t kSub = 256;          // symbols per lane of the chunk decoders (decode.hip, decode_ring.hip)
 constexpr uint32_t kIdx = 64;           // restart index stride of the byte path (sub_bit): symbols
-constexpr uint32_t kShortMaxLen = 27;   // u32 table entries: code << 5 | len
+constexpr uint32_t kShortMaxLen = 27;   // u32 table entries: code << (32 - len) | len
 constexpr uint32_t kLongMaxLen = 57;    // u64 table entries: code << 6 | len
 constexpr uint32_t kHistCopies = 8;     // XCD-group copies of the global weights
 constexpr uint32_t kLutMaxBits = 12;    // primary decode table index bits
@@ -41,8 +41,8 @@ constexpr uint32_t kSsSlow = 0x80u;
 
 
 // The code table travels in the kernel arguments (no upload copy on the
-// critical path between pass 1 and pass 2): u32 code << 5 | len for codes
-// <= 27 bits, u64 code << 6 | len up to 57 bits.
+// critical path between pass 1 and pass 2): u32 code << (32 - len) | len
+// (left-aligned) for codes <= 27 bits, u64 code << 6 | len up to 57 bits.
 union alignas(8) CodeTable {
     uint32_t s[256];
     uint64_t l[256];
@@ -162,6 +162,7 @@ struct WideArgs {
     uint64_t n;
     uint32_t width;               // 1, 2, 4, 8, 16
     uint32_t log2_slots;          // cuckoo table: 2^log2_slots slots in buckets of 2
+    uint64_t fold;                // 16-byte keys: hash of lo ^ hi * fold (host/wide.hpp wide_buckets)
     const uint8_t* keys;          // [slots * max(4, width)]
     const void* vals;             // [slots] (code << 8) | len, 0 = empty; u32 if val32 else u64
     uint32_t val32;               // every code <= 24 bits
@@ -234,7 +235,7 @@ hipError_t launch_pack_deep(const DeepPackArgs& a, hipStream_t s);
 hipError_t launch_decode_deep(const DecodeArgs& a, hipStream_t s);  // lut, lut_bits, restart index, n, out
 hipError_t launch_decode_deep_serial(const DeepSerialArgs& a, hipStream_t s);
 
-size_t pack_lds_bytes(bool long_codes, uint32_t stage_words);
+size_t pack_lds_bytes(bool long_codes, uint32_t max_len, uint32_t stage_words);
 uint32_t pack_waves_per_group(bool long_codes);
 size_t decode_lds_bytes(uint32_t lut_bits, uint32_t rep_log2);
 constexpr uint32_t kDecodeSingle = 1;  // decode.hip k_decode_short

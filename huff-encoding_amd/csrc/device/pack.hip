@@ -50,22 +50,35 @@ struct LaneIn {
     uint4 v[kPieces];
 };
 
+// Table entries. Short codes (<= 27 bits): u32, the code LEFT-aligned (its
+// first bit at bit 31) and the length in bits [0, 5): groups join with one
+// shift and one and-or per code, and a group lands at bit s of its two stage
+// words as (J >> s, alignbit(J, 0, s)) with no 64-bit shift. Long codes: u64
+// code << 6 | len, right-aligned. 32 lane copies of each letter's entry
+// ([letter][copy], lane l reads copy l % 32: conflict-free on any data).
+// (64 copies, so that letter b's address is one v_perm ((b << 8) | 4 lane)
+// instead of bfe + lshl_or, measured slower: the 64 KiB table leaves 4 waves
+// per SIMD instead of 6 — Zipf 0.481 vs 0.446 ms, text 0.440 vs 0.417)
 template <bool LONG>
 struct Entry;
 template <>
 struct Entry<false> {
     using T = uint32_t;
-    static constexpr uint32_t kShift = 5;
     static constexpr uint32_t kMask = 31;
-    static constexpr uint32_t kTableWords = 256 * 32;
+    __device__ static uint64_t code(T e) {
+        const uint32_t len = e & 31u;
+        return len ? e >> (32 - len) : 0u;
+    }
 };
 template <>
 struct Entry<true> {
     using T = uint64_t;
-    static constexpr uint32_t kShift = 6;
     static constexpr uint32_t kMask = 63;
-    static constexpr uint32_t kTableWords = 256 * 32 * 2;
+    __device__ static uint64_t code(T e) { return e >> 6; }
 };
+constexpr int kCopies = 32;
+template <bool LONG>
+constexpr uint32_t table_words() { return 256u * kCopies * (LONG ? 2u : 1u); }
 
 template <bool LONG>
 __device__ __forceinline__ void emit_codes(uint32_t* __restrict__ stage, uint64_t p,
@@ -91,7 +104,7 @@ __device__ __forceinline__ void emit_codes(uint32_t* __restrict__ stage, uint64_
 #pragma unroll
     for (int k = 0; k < static_cast<int>(kBPL); ++k) {
         const uint32_t len = static_cast<uint32_t>(ent[k] & E::kMask);
-        const uint64_t code = static_cast<uint64_t>(ent[k] >> E::kShift);
+        const uint64_t code = E::code(ent[k]);
         if (LONG && len > 32) {
             const uint32_t hl = len - 32;
             acc = (acc << hl) | (code >> 32);
@@ -113,41 +126,64 @@ __device__ __forceinline__ void emit_codes(uint32_t* __restrict__ stage, uint64_
 }
 
 // short codes: groups of G consecutive codes (G * max_len <= 32) are joined
-// in a register and ORed into their (at most) two stage words at the group's
-// bit offset: no serial 64-bit accumulator, no per-code branch. An empty
-// entry past the chunk end has len 0 and code 0 and ORs zero. (Re-reading the
-// entries from the table here instead of keeping them live measured 30 %
+// left-aligned in a register (J = e0 & ~31 | (e1 & ~31) >> l0, the shift
+// taking l0 from e0's low bits) and ORed into their (at most) two stage
+// words at the group's bit offset s: J >> s and alignbit(J, 0, s) = the bits
+// shifted past the first word (0 for s = 0). No 64-bit shift, no per-code
+// branch; an empty entry past the chunk end is 0 and ORs zero. (Re-reading
+// the entries from the table here instead of keeping them live measured 30 %
 // slower.)
+__device__ __forceinline__ uint32_t join2(uint32_t e0, uint32_t e1) {
+    // (e1 & ~31) >> (e0 & 31): v_lshrrev uses the low 5 bits of its shift
+    return (e0 & ~31u) | ((e1 & ~31u) >> (e0 & 31u));
+}
+
 template <int G>
 __device__ __forceinline__ void emit_codes_or(uint32_t* __restrict__ stage, uint32_t p, const uint32_t (&ent)[kBPL]) {
+    const uint32_t stage_addr = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(
+        (__attribute__((address_space(3))) uint32_t*)(stage)));
     uint32_t o = p;
 #pragma unroll
     for (int k = 0; k < static_cast<int>(kBPL); k += G) {
-        uint32_t code = 0, len = 0;
-#pragma unroll
-        for (int g = 0; g < G; ++g) {
-            const uint32_t l = ent[k + g] & 31u;
-            code = (code << l) | (ent[k + g] >> 5);
-            len += l;
+        uint32_t J, len;
+        if constexpr (G == 1) {
+            J = ent[k] & ~31u;
+            len = ent[k] & 31u;
+        } else if constexpr (G == 2) {
+            J = join2(ent[k], ent[k + 1]);
+            len = (ent[k] & 31u) + (ent[k + 1] & 31u);
+        } else {
+            static_assert(G == 4, "groups of 1, 2 or 4 codes");
+            const uint32_t l01 = (ent[k] & 31u) + (ent[k + 1] & 31u);
+            const uint32_t J23 = join2(ent[k + 2], ent[k + 3]);
+            J = join2(ent[k], ent[k + 1]) | (J23 >> l01);
+            len = l01 + (ent[k + 2] & 31u) + (ent[k + 3] & 31u);
         }
         const uint32_t s = o & 31u;
-        // the group left-aligned at bit s of a 64-bit window starting at word o/32
-        const uint64_t v = static_cast<uint64_t>(code) << ((64u - s - len) & 63u);
-        uint32_t* w = stage + (o >> 5);
-        __hip_atomic_fetch_or(w, static_cast<uint32_t>(v >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        __hip_atomic_fetch_or(w + 1, static_cast<uint32_t>(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        // the word's LDS address, lshr + lshl_add (opaque: the compiler's
+        // canonical (o >> 3 & ~3) + base costs one more op per group)
+        uint32_t wa;
+        asm volatile("v_lshl_add_u32 %0, %1, 2, %2" : "=v"(wa) : "v"(o >> 5), "v"(stage_addr));
+        auto* w = (__attribute__((address_space(3))) uint32_t*)(static_cast<uintptr_t>(wa));
+        __hip_atomic_fetch_or(w, J >> s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_fetch_or(w + 1, __builtin_amdgcn_alignbit(J, 0u, s), __ATOMIC_RELAXED,
+                              __HIP_MEMORY_SCOPE_WORKGROUP);
         o += len;
     }
 }
 
+// segment s of the stage (global bytes [gbyte, gbyte + 16)); segments
+// [full_lo, full_hi) lie inside the wave's bytes [own_lo, own_hi) (wave-uniform
+// 32-bit bounds), the others are stored byte by byte where owned
 __device__ __forceinline__ void store_segment(const uint32_t* __restrict__ stage, uint32_t s, uint64_t gbyte,
-                                              uint64_t own_lo, uint64_t own_hi, uint8_t* __restrict__ out) {
+                                              uint32_t full_lo, uint32_t full_hi, uint64_t own_lo, uint64_t own_hi,
+                                              uint8_t* __restrict__ out) {
     uint4 v = reinterpret_cast<const uint4*>(stage)[s];  // one ds_read_b128
     v.x = __builtin_bswap32(v.x);
     v.y = __builtin_bswap32(v.y);
     v.z = __builtin_bswap32(v.z);
     v.w = __builtin_bswap32(v.w);
-    if (gbyte >= own_lo && gbyte + 16 <= own_hi) {
+    if (s >= full_lo && s < full_hi) {
         *reinterpret_cast<uint4*>(out + gbyte) = v;
         return;
     }
@@ -163,20 +199,22 @@ template <bool LONG, int G = 1>
 __global__ __launch_bounds__(pack_waves<LONG>() * 64) void k_pack(PackArgs a) {
     constexpr int kWaves = pack_waves<LONG>();
     constexpr int kThreads = kWaves * 64;
+    constexpr int C = kCopies;
+    constexpr int LOGC = 5;
     using E = Entry<LONG>;
     using T = typename E::T;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     T* tab = reinterpret_cast<T*>(lds);
     // wave_index(): the chunk, its buffer resource and the round bounds are scalar
-    const uint32_t t = threadIdx.x, lane = t & 63, copy = t & 31, wave = wave_index();
-    uint32_t* stage = lds + E::kTableWords + wave * a.stage_words;
+    const uint32_t t = threadIdx.x, lane = t & 63, copy = t & (C - 1), wave = wave_index();
+    uint32_t* stage = lds + table_words<LONG>() + wave * a.stage_words;
 
-    // replicate the table: thread t writes copy t%32 of letters t/32 + 8i
+    // replicate the table: thread t writes copy t % C of letters t / C + (kThreads / C) i
     const T* tg = reinterpret_cast<const T*>(LONG ? static_cast<const void*>(a.table.l) : static_cast<const void*>(a.table.s));
 #pragma unroll 4
-    for (int i = 0; i < 256 / (kThreads / 32); ++i) {
-        const uint32_t e = (t >> 5) + (kThreads / 32) * i;
-        tab[(e << 5) | copy] = tg[e];
+    for (int i = 0; i < 256 / (kThreads / C); ++i) {
+        const uint32_t e = (t >> LOGC) + (kThreads / C) * i;
+        tab[(e << LOGC) | copy] = tg[e];
     }
     for (uint32_t i = lane; i < a.stage_words; i += 64) stage[i] = 0;
     __syncthreads();
@@ -218,9 +256,9 @@ __global__ __launch_bounds__(pack_waves<LONG>() * 64) void k_pack(PackArgs a) {
                     if (j > a.prev_tail_len) break;
                     b = a.prev_tail[8 - j];
                 }
-                const T ent = tab[static_cast<uint32_t>(b) << 5];
+                const T ent = tab[static_cast<uint32_t>(b) << LOGC];
                 const int64_t len = static_cast<int64_t>(ent & E::kMask);
-                const uint64_t code = static_cast<uint64_t>(ent >> E::kShift);
+                const uint64_t code = E::code(ent);
                 if (len == 0) break;
                 const int64_t start = pos - len;  // may precede bit 0 of out (a shard's first byte)
                 for (int64_t q = (start > floor8 ? start : floor8); q < pos; ++q) {
@@ -239,9 +277,11 @@ __global__ __launch_bounds__(pack_waves<LONG>() * 64) void k_pack(PackArgs a) {
             const LaneIn v = v0;
             v0 = v1;
             v1 = load_round(r + 2);
-            const uint64_t s_in_chunk = static_cast<uint64_t>(r) * kPackWaveRound + lane * kBPL;
-            const int nvalid = s_in_chunk >= nsym ? 0 : (nsym - s_in_chunk >= kBPL ? static_cast<int>(kBPL)
-                                                                                     : static_cast<int>(nsym - s_in_chunk));
+            // 32-bit: a chunk holds at most 65536 symbols
+            const uint32_t s_in_chunk = r * kPackWaveRound + lane * kBPL;
+            const uint32_t nsym32 = static_cast<uint32_t>(nsym);
+            const int nvalid = s_in_chunk >= nsym32 ? 0
+                                                    : static_cast<int>(nsym32 - s_in_chunk < kBPL ? nsym32 - s_in_chunk : kBPL);
 
             uint32_t bits = 0;
             uint32_t wv[4 * kPieces];
@@ -253,16 +293,13 @@ __global__ __launch_bounds__(pack_waves<LONG>() * 64) void k_pack(PackArgs a) {
                 wv[4 * q + 3] = v.v[q].w;
             }
             T ent[kBPL];
+            auto lookup = [&](int k) -> T { return tab[(((wv[k >> 2] >> (8 * (k & 3))) & 0xFFu) << LOGC) | copy]; };
             if ((r + 1ull) * kPackWaveRound <= nsym) {  // whole round (wave-uniform): no per-letter masks
 #pragma unroll
-                for (int k = 0; k < static_cast<int>(kBPL); ++k)
-                    ent[k] = tab[(((wv[k >> 2] >> (8 * (k & 3))) & 0xFFu) << 5) | copy];
+                for (int k = 0; k < static_cast<int>(kBPL); ++k) ent[k] = lookup(k);
             } else {
 #pragma unroll
-                for (int k = 0; k < static_cast<int>(kBPL); ++k) {
-                    const uint32_t b = (wv[k >> 2] >> (8 * (k & 3))) & 0xFFu;
-                    ent[k] = (k < nvalid) ? tab[(b << 5) | copy] : T(0);
-                }
+                for (int k = 0; k < static_cast<int>(kBPL); ++k) ent[k] = (k < nvalid) ? lookup(k) : T(0);
             }
 #pragma unroll
             for (int k = 0; k < static_cast<int>(kBPL); ++k) bits += static_cast<uint32_t>(ent[k] & E::kMask);
@@ -285,8 +322,12 @@ __global__ __launch_bounds__(pack_waves<LONG>() * 64) void k_pack(PackArgs a) {
             const bool last = (r + 1 == nrounds);
             const uint32_t nseg_done = static_cast<uint32_t>((end_bit - stage_bit0) >> 7);
             const uint32_t nseg_store = last ? static_cast<uint32_t>((end_bit - stage_bit0 + 127) >> 7) : nseg_done;
+            const uint64_t sb0 = stage_bit0 >> 3;  // global byte of stage segment 0
+            const uint32_t full_lo = own_lo > sb0 ? static_cast<uint32_t>((own_lo - sb0 + 15) >> 4) : 0u;
+            const uint64_t hi_rel = own_hi > sb0 ? (own_hi - sb0) >> 4 : 0;
+            const uint32_t full_hi = static_cast<uint32_t>(hi_rel < 0x7FFFFFFFull ? hi_rel : 0x7FFFFFFFull);
             for (uint32_t s = lane; s < nseg_store; s += 64)
-                store_segment(stage, s, (stage_bit0 >> 3) + 16ull * s, own_lo, own_hi, a.out);
+                store_segment(stage, s, sb0 + 16ull * s, full_lo, full_hi, own_lo, own_hi, a.out);
             const uint32_t used_words = static_cast<uint32_t>((end_bit - stage_bit0 + 31) >> 5);
             uint32_t keep = 0;
             if (!last && lane < 4) keep = stage[nseg_done * 4 + lane];
@@ -307,8 +348,9 @@ __global__ __launch_bounds__(pack_waves<LONG>() * 64) void k_pack(PackArgs a) {
 
 }  // namespace
 
-size_t pack_lds_bytes(bool long_codes, uint32_t stage_words) {
-    const uint32_t table = long_codes ? Entry<true>::kTableWords : Entry<false>::kTableWords;
+size_t pack_lds_bytes(bool long_codes, uint32_t max_len, uint32_t stage_words) {
+    (void)max_len;
+    const uint32_t table = long_codes ? table_words<true>() : table_words<false>();
     const uint32_t waves = long_codes ? pack_waves<true>() : pack_waves<false>();
     return static_cast<size_t>(table + waves * stage_words) * 4;
 }
@@ -317,7 +359,7 @@ uint32_t pack_waves_per_group(bool long_codes) { return long_codes ? pack_waves<
 
 hipError_t launch_pack(bool long_codes, const PackArgs& a, hipStream_t s) {
     if (a.nchunks == 0) return hipSuccess;
-    const size_t lds = pack_lds_bytes(long_codes, a.stage_words);
+    const size_t lds = pack_lds_bytes(long_codes, a.max_len, a.stage_words);
     if (long_codes) {
         hipLaunchKernelGGL(k_pack<true>, dim3(a.grid), dim3(pack_waves<true>() * 64), lds, s, a);
     } else if (a.max_len <= 8) {  // 4 codes per OR pair

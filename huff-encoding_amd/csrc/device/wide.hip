@@ -74,14 +74,14 @@ __device__ __forceinline__ KeyStore<T> to_store(T v) {
 
 // host/wide.hpp wide_buckets
 template <typename T>
-__device__ __forceinline__ void buckets_of(T key, uint32_t lgb, uint32_t& b1, uint32_t& b2) {
+__device__ __forceinline__ void buckets_of(T key, uint32_t lgb, uint64_t fold, uint32_t& b1, uint32_t& b2) {
     using K = KeyOps<T>;
     if constexpr (sizeof(T) <= 4) {
         const uint32_t x = static_cast<uint32_t>(K::lo(key));
         b1 = (x * 0x9E3779B1u) >> (32 - lgb);
         b2 = (x * 0x85EBCA77u + 0x165667B1u) >> (32 - lgb);
     } else {
-        const uint64_t k = K::lo(key) ^ (K::hi(key) * 0xC2B2AE3D27D4EB4Full);
+        const uint64_t k = K::lo(key) ^ (K::hi(key) * fold);
         b1 = static_cast<uint32_t>((k * 0x9E3779B97F4A7C15ull) >> (64 - lgb));
         b2 = static_cast<uint32_t>((k * 0xD6E8FEB86659FD93ull + 0x165667B19E3779F9ull) >> (64 - lgb));
     }
@@ -90,10 +90,10 @@ __device__ __forceinline__ void buckets_of(T key, uint32_t lgb, uint32_t& b1, ui
 // value of a key: the four slots of its two buckets, no loop, no branch (a
 // key is stored once; empty slots hold value 0)
 template <typename T, typename V>
-__device__ __forceinline__ V lookup(const KeyStore<T>* keys, const V* vals, uint32_t lgs, T key) {
+__device__ __forceinline__ V lookup(const KeyStore<T>* keys, const V* vals, uint32_t lgs, uint64_t fold, T key) {
     using K = KeyOps<KeyStore<T>>;
     uint32_t b1, b2;
-    buckets_of<T>(key, lgs - 1, b1, b2);
+    buckets_of<T>(key, lgs - 1, fold, b1, b2);
     const KeyStore<T> k = to_store<T>(key);
     const uint32_t s1 = 2 * b1, s2 = 2 * b2;
     const KeyStore<T> k10 = keys[s1], k11 = keys[s1 + 1], k20 = keys[s2], k21 = keys[s2 + 1];
@@ -104,10 +104,10 @@ __device__ __forceinline__ V lookup(const KeyStore<T>* keys, const V* vals, uint
 
 // the values of the letters of a 16-byte vector (0 = no code)
 template <typename T, typename V, uint32_t L>
-__device__ __forceinline__ void probe_vec(const KeyStore<T>* keys, const V* vals, uint32_t lgs, const uint4& in,
-                                          V (&e)[L]) {
+__device__ __forceinline__ void probe_vec(const KeyStore<T>* keys, const V* vals, uint32_t lgs, uint64_t fold,
+                                          const uint4& in, V (&e)[L]) {
 #pragma unroll
-    for (uint32_t j = 0; j < L; ++j) e[j] = lookup<T, V>(keys, vals, lgs, KeyOps<T>::get(in, j));
+    for (uint32_t j = 0; j < L; ++j) e[j] = lookup<T, V>(keys, vals, lgs, fold, KeyOps<T>::get(in, j));
 }
 
 // the last partial 16 bytes of a buffer (zero past the end); out of line:
@@ -189,7 +189,7 @@ __device__ __forceinline__ void wbits_chunk(const WideArgs& a, const KeyStore<T>
             const uint32_t gg = g + q * L;
             const uint4 v = in.take(q, gg);
             V e[L];
-            probe_vec<T, V, L>(keys, vals, a.log2_slots, v, e);
+            probe_vec<T, V, L>(keys, vals, a.log2_slots, a.fold, v, e);
 #pragma unroll
             for (uint32_t j = 0; j < L; ++j) {
                 const bool ok = gg + j < cnt;
@@ -281,7 +281,7 @@ __device__ __forceinline__ void wpack_chunk(const WideArgs& a, const KeyStore<T>
             const uint4 v = in.take(q, gg);
             if (gg < cnt) {
                 V e[L];
-                probe_vec<T, V, L>(keys, vals, a.log2_slots, v, e);
+                probe_vec<T, V, L>(keys, vals, a.log2_slots, a.fold, v, e);
 #pragma unroll
                 for (uint32_t j = 0; j < L; ++j) put(gg + j < cnt ? static_cast<uint64_t>(e[j]) : 0ull, false);
             }
@@ -292,7 +292,7 @@ __device__ __forceinline__ void wpack_chunk(const WideArgs& a, const KeyStore<T>
     // first bits), or pad it with zeros at the end of the stream
     const T* letters = reinterpret_cast<const T*>(a.in);
     for (uint64_t i = i0 + cnt; i < a.n; ++i)
-        if (put(lookup<T, V>(keys, vals, a.log2_slots, letters[i]), true)) return;
+        if (put(lookup<T, V>(keys, vals, a.log2_slots, a.fold, letters[i]), true)) return;
     out[w] = __builtin_bswap32(static_cast<uint32_t>(acc << (32 - nacc)));
 }
 

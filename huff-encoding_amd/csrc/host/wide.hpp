@@ -92,10 +92,14 @@ constexpr uint32_t kWideLutPtr = 0x80000000u;  // = dev::kLutPtr
 constexpr uint32_t kWideLutMaxBits = 12;        // = dev::kLutMaxBits
 constexpr uint32_t kWideMaxDecodeLen = 57;      // = dev::kLongMaxLen
 constexpr uint32_t kWideMaxEncodeLen = 56;      // (code << 8) | len in a u64
+constexpr uint64_t kWideFold0 = 0xC2B2AE3D27D4EB4Full;
 
 struct WideEncTables {
     uint32_t width = 1;
     uint32_t log2_slots = 0;     // slots = 2 * buckets
+    // 16-byte keys fold to lo ^ hi * fold before hashing; distinct keys that
+    // fold alike under one multiplier separate under another (re-seeded)
+    uint64_t fold = kWideFold0;
     std::vector<uint8_t> keys;   // slots * wide_key_bytes(width)
     std::vector<uint64_t> vals;  // slots
     std::vector<uint32_t> vals32;  // the same when every code has <= 24 bits (else empty)
@@ -113,14 +117,15 @@ struct WideDecTables {
 // fixed loads and no loop. Keys of <= 4 bytes are stored as u32. Same hashes
 // on host and device (device/wide.hip buckets_of).
 inline uint32_t wide_key_bytes(uint32_t width) { return width < 4 ? 4 : width; }
-inline void wide_buckets(uint64_t lo, uint64_t hi, uint32_t lgb, uint32_t width, uint32_t* b1, uint32_t* b2) {
+inline void wide_buckets(uint64_t lo, uint64_t hi, uint32_t lgb, uint32_t width, uint64_t fold, uint32_t* b1,
+                         uint32_t* b2) {
     if (width <= 4) {
         const uint32_t x = static_cast<uint32_t>(lo);
         *b1 = static_cast<uint32_t>((static_cast<uint64_t>(x * 0x9E3779B1u)) >> (32 - lgb));
         *b2 = static_cast<uint32_t>((static_cast<uint64_t>(x * 0x85EBCA77u + 0x165667B1u)) >> (32 - lgb));
         return;
     }
-    const uint64_t k = lo ^ (hi * 0xC2B2AE3D27D4EB4Full);
+    const uint64_t k = lo ^ (hi * fold);
     *b1 = static_cast<uint32_t>((k * 0x9E3779B97F4A7C15ull) >> (64 - lgb));
     *b2 = static_cast<uint32_t>((k * 0xD6E8FEB86659FD93ull + 0x165667B19E3779F9ull) >> (64 - lgb));
 }

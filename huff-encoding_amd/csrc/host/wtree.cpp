@@ -203,9 +203,12 @@ Status build_wide_enc_tables(const WideTree& t, WideEncTables& out) {
     out.width = W;
     out.maxlen = maxlen;
     out.distinct = codes.size();
-    // buckets of 2 slots, load <= 1/2; grow until every key is placed
-    uint32_t lgb = 5;
-    while ((2ull << lgb) < 2 * codes.size()) ++lgb;
+    // buckets of 2 slots, load <= 1/2; grow (at most 16x) until every key is
+    // placed. Keys of <= 8 bytes hash injectively, so they separate within
+    // that; 16-byte keys fold to 64 bits first, and letters whose folds
+    // collide never separate by growing: then re-seed the fold multiplier
+    uint32_t lgb0 = 5;
+    while ((2ull << lgb0) < 2 * codes.size()) ++lgb0;
     struct Ent {
         u128 key;
         uint64_t val;
@@ -213,7 +216,19 @@ Status build_wide_enc_tables(const WideTree& t, WideEncTables& out) {
     };
     std::vector<Ent> slot;
     uint64_t rng = 0x9E3779B97F4A7C15ull;
+    uint64_t fold = kWideFold0, seed = 0;
+    const uint32_t lg_cap = std::min<uint32_t>(lgb0 + 4, 31);
+    uint32_t lgb = lgb0;
     for (;; ++lgb) {
+        if (lgb > lg_cap) {
+            if (W <= 8 || ++seed > 64)
+                return Status::err(HUFF_E_INVALID_ARG, "letters do not separate in the encoder's hash table");
+            uint64_t z = (seed * 0x9E3779B97F4A7C15ull) ^ kWideFold0;  // splitmix64 of the seed
+            z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+            z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+            fold = (z ^ (z >> 31)) | 1u;
+            lgb = lgb0;
+        }
         slot.assign(size_t(2) << lgb, Ent{0, 0, false});
         bool ok = true;
         for (const WideLeaf& c : codes) {
@@ -221,7 +236,8 @@ Status build_wide_enc_tables(const WideTree& t, WideEncTables& out) {
             bool placed = false;
             for (int kick = 0; kick < 1000 && !placed; ++kick) {
                 uint32_t b[2];
-                wide_buckets(static_cast<uint64_t>(cur.key), static_cast<uint64_t>(cur.key >> 64), lgb, W, &b[0], &b[1]);
+                wide_buckets(static_cast<uint64_t>(cur.key), static_cast<uint64_t>(cur.key >> 64), lgb, W, fold, &b[0],
+                             &b[1]);
                 for (int q = 0; q < 4 && !placed; ++q) {
                     Ent& e = slot[2 * b[q >> 1] + (q & 1)];
                     if (!e.used) {
@@ -243,6 +259,7 @@ Status build_wide_enc_tables(const WideTree& t, WideEncTables& out) {
         if (ok) break;
     }
     out.log2_slots = lgb + 1;
+    out.fold = fold;
     out.keys.assign(slot.size() * KB, 0);
     out.vals.assign(slot.size(), 0);
     for (size_t i = 0; i < slot.size(); ++i) {

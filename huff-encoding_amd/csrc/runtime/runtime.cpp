@@ -546,7 +546,8 @@ huff::Status huff_enc::pack(const huff_tree* t, uint64_t base, const uint8_t* pr
     if (long_codes)
         for (int b = 0; b < 256; ++b) a.table.l[b] = (et.code[b] << 6) | et.len[b];
     else
-        for (int b = 0; b < 256; ++b) a.table.s[b] = static_cast<uint32_t>(et.code[b] << 5) | et.len[b];
+        for (int b = 0; b < 256; ++b)  // left-aligned (pack.hip Entry<false>)
+            a.table.s[b] = et.len[b] ? static_cast<uint32_t>(et.code[b] << (32 - et.len[b])) | et.len[b] : 0u;
     if (prev_tail_len) std::memcpy(a.prev_tail + 8 - prev_tail_len, prev_tail, prev_tail_len);
     a.in = d_in;
     a.n = n;
@@ -559,7 +560,7 @@ huff::Status huff_enc::pack(const huff_tree* t, uint64_t base, const uint8_t* pr
     // 128-bit window past the last unit, which the OR emit may touch with zero)
     a.stage_words = (huff::dev::kPackWaveRound / 32 * std::max<uint32_t>(et.maxlen, 1) + 12 + 3) & ~3u;
     a.max_len = et.maxlen;
-    const size_t lds = huff::dev::pack_lds_bytes(long_codes, a.stage_words);
+    const size_t lds = huff::dev::pack_lds_bytes(long_codes, et.maxlen, a.stage_words);
     const uint32_t per_cu = std::max<uint32_t>(1, std::min<uint32_t>(8, static_cast<uint32_t>((160 * 1024) / lds)));
     const uint32_t wpg = huff::dev::pack_waves_per_group(long_codes);
     a.grid = std::max<uint32_t>(1, std::min<uint32_t>((nchunks + wpg - 1) / wpg, ctx->cu_count * per_cu));
@@ -645,10 +646,17 @@ huff::Status huff_enc::decode(const huff_tree* t, const uint8_t* d_comp, uint64_
             v == static_cast<int>(huff::dev::kDecodeWave) || v == static_cast<int>(huff::dev::kDecodeFixed))
             a.variant = static_cast<uint32_t>(v);
     }
-    // the wave decoder stores 16-B pieces: the output must be 16-B aligned
-    if ((a.variant == huff::dev::kDecodeWave || a.variant == huff::dev::kDecodeFixed) &&
-        (reinterpret_cast<uintptr_t>(d_out) & 15))
-        a.variant = (total_bits < 7 * n) ? huff::dev::kDecodeRing : huff::dev::kDecodeSingle;
+    // the wave decoders store 16-B pieces: a misaligned output (e.g. a tensor
+    // view at an odd offset) is decoded into an aligned buffer of the context
+    // and copied on the stream (one extra n-byte copy, against 1.5-2x for the
+    // older unaligned-capable decoders)
+    uint8_t* dst = d_out;
+    const bool bounce = (a.variant == huff::dev::kDecodeWave || a.variant == huff::dev::kDecodeFixed) &&
+                        (reinterpret_cast<uintptr_t>(d_out) & 15);
+    if (bounce) {
+        HUFF_TRY(ctx->d_align.ensure(n + 64));
+        dst = static_cast<uint8_t*>(ctx->d_align.p);
+    }
     a.cu_count = static_cast<uint32_t>(ctx->cu_count);
     a.pad_stage = huff::dev::fixed_decode_pad(total_bits, n);
     a.mlut = static_cast<const uint32_t*>(ctx->d_lut.p) + dt->moff;
@@ -656,13 +664,14 @@ huff::Status huff_enc::decode(const huff_tree* t, const uint8_t* d_comp, uint64_
     a.stab = reinterpret_cast<const uint16_t*>(static_cast<const uint32_t*>(ctx->d_lut.p) + dt->soff);
     a.stab_bits = dt->sbits;
     a.n = n;
-    a.out = d_out;
+    a.out = dst;
     if (a.check_mode) {
         HUFF_TRY(huff::run_checked_decode(ctx, a, [&] { return huff::dev::launch_decode(a, ctx->stream); }));
     } else {
         HUFF_TRY(ctx->timed("decode", [&] { return huff::dev::launch_decode(a, ctx->stream); }));
     }
     HIP_TRY(hipEventRecord(ctx->lut_free, ctx->stream));
+    if (bounce && n) HIP_TRY(hipMemcpyAsync(d_out, dst, n, hipMemcpyDeviceToDevice, ctx->stream));
     return huff::Status::ok();
 }
 
@@ -1040,8 +1049,10 @@ Status decode_indexless_dev(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_
     if (total == 0) HUFF_TRY(walk_end(nullptr, 0, nullptr, 0));
     HUFF_TRY(out_ptr(total));
     hipStream_t strm = ctx->stream;
-    const bool aligned16 = !(reinterpret_cast<uintptr_t>(d_comp) & 15) && !(reinterpret_cast<uintptr_t>(out_at()) & 15);
-    if (dev::indexless_staged(st.a) && total && aligned16) {
+    if (dev::indexless_staged(st.a) && total && !(reinterpret_cast<uintptr_t>(d_comp) & 15)) {
+        // a misaligned output: decoded into an aligned buffer, then copied (as huff_enc::decode)
+        const bool bounce = reinterpret_cast<uintptr_t>(out_at()) & 15;
+        if (bounce) HUFF_TRY(ctx->d_align.ensure(total + 64));
         // a restart point every 64 symbols, then the fixed-count decoder
         DevBuf& sub_abs = ctx->idx_sub_abs;
         HUFF_TRY(indexless_mark(ctx, st, sub_abs, 6));
@@ -1062,10 +1073,11 @@ Status decode_indexless_dev(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_
         d.cu_count = static_cast<uint32_t>(ctx->cu_count);
         d.pad_stage = dev::fixed_decode_pad(valid_bits, total);
         d.n = total;
-        d.out = out_at();
+        d.out = bounce ? static_cast<uint8_t*>(ctx->d_align.p) : out_at();
         d.check_mode = decode_check_mode();
         HUFF_TRY(run_checked_decode(ctx, d, [&] { return dev::launch_decode_fixed(d, strm); }));
         HIP_TRY(hipEventRecord(ctx->lut_free, strm));
+        if (bounce) HIP_TRY(hipMemcpyAsync(out_at(), ctx->d_align.p, total, hipMemcpyDeviceToDevice, strm));
         return Status::ok();
     }
     HIP_TRY(dev::launch_indexless_emit(st.a, static_cast<const uint64_t*>(st.off.p), out_at(), strm));

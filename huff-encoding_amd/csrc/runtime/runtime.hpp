@@ -127,6 +127,7 @@ struct huff_ctx {
     PinnedBuf pin_lut;   // decode table upload
     DevBuf d_in, d_out;  // staging of the host-pointer API
     DevBuf d_lut;
+    DevBuf d_align;      // aligned decode target for a misaligned output pointer
     DevBuf d_err;        // k_decode_fixed self-check record (check builds)
     // index-free decode workspace, kept across calls (per-call allocations
     // of its ~100 MB per GiB of stream cost more than the kernels)

@@ -86,6 +86,7 @@ Status huff_wenc::bits(const huff_wtree* t, uint64_t* total, huff::u128* missing
     a.n = n;
     a.width = width;
     a.log2_slots = et->log2_slots;
+    a.fold = et->fold;
     a.keys = static_cast<const uint8_t*>(keys.p);
     a.vals = vals.p;
     a.val32 = !et->vals32.empty();
@@ -128,6 +129,7 @@ Status huff_wenc::pack(const huff_wtree* t, uint8_t* d_out, size_t out_cap, uint
     a.n = n;
     a.width = width;
     a.log2_slots = et->log2_slots;
+    a.fold = et->fold;
     a.keys = static_cast<const uint8_t*>(keys.p);
     a.vals = vals.p;
     a.val32 = !et->vals32.empty();

@@ -287,7 +287,8 @@ def test_device_job_medium(H, O, ctx, kind, seed, dec, monkeypatch):
     runtime picks and through each decode kernel forced (HUFF_DEC_VARIANT)"""
     import torch
 
-    if dec != "auto":
+    forced = dec != "auto"
+    if forced:
         monkeypatch.setenv("HUFF_DEC_VARIANT", dec)
         monkeypatch.setenv("HUFF_DISABLE_FIXED8", "1")
 
@@ -314,6 +315,37 @@ def test_device_job_medium(H, O, ctx, kind, seed, dec, monkeypatch):
     job.decode(tree, out.data_ptr(), dec.data_ptr())
     torch.cuda.synchronize()
     assert torch.equal(dec[:n], x[:n])
+    if not forced:
+        # a misaligned output (a tensor view at an odd offset): decoded into the
+        # context's aligned buffer and copied; the bytes around it untouched
+        dec.fill_(0xA5)
+        job.decode(tree, out.data_ptr(), dec.data_ptr() + 3)
+        torch.cuda.synchronize()
+        assert torch.equal(dec[3:3 + n], x[:n])
+        assert (dec[:3] == 0xA5).all() and (dec[3 + n:] == 0xA5).all()
+
+
+def test_indexfree_misaligned_output(H, O, ctx):
+    """huff_dev_decompress into an output pointer that is not 16-B aligned:
+    the fixed-count decoder runs into an aligned buffer, then one copy"""
+    import torch
+    from huff_coding import device as D
+
+    n = (1 << 22) + 77
+    x = _device_gen(H, ctx, "zipf", 61, n)
+    host = x[:n].cpu().numpy()
+    w = O.fast_hist(host, 8)
+    ot = O.Tree.from_weights(O.weights_from_array(w))
+    tree = H.HuffTree.from_weights(H.ByteWeights.from_array(w))
+    code, ln = ot.code_table()
+    comp, bits = O.fast_encode(host, code, ln, threads=8)
+    dc = torch.from_numpy(np.concatenate([comp, np.zeros(64, np.uint8)])).cuda()
+    out = torch.full((n + 128,), 0x5A, dtype=torch.uint8, device="cuda")
+    got = D.decompress_dev(ctx, tree, dc.data_ptr(), len(comp), (8 - bits % 8) % 8, out.data_ptr() + 5, n + 64)
+    torch.cuda.synchronize()
+    assert got == n
+    assert torch.equal(out[5:5 + n], x[:n])
+    assert (out[:5] == 0x5A).all() and (out[5 + n:] == 0x5A).all()
 
 
 @pytest.mark.parametrize("dec", ["auto", "1", "7", "9", "10"], ids=["dec-auto", "dec-single", "dec-ring", "dec-wave", "dec-fixed"])

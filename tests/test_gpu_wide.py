@@ -103,6 +103,27 @@ def test_u128_letters(W, O, ctx):
         assert back2.tobytes() == letters.tobytes()
 
 
+def test_u128_letters_with_colliding_folds(W, O, ctx):
+    """16-byte letters fold to lo ^ hi * C before hashing; eight letters
+    with (hi, lo) = (i, i * C mod 2^64) all fold to 0, so no table size
+    separates them: the table build re-seeds the fold (wtree.cpp) instead
+    of growing without bound, and the codes stay those of the reference"""
+    C = 0xC2B2AE3D27D4EB4F
+    vals = [(i << 64) | ((i * C) & ((1 << 64) - 1)) for i in range(8)] + [12345, 1 << 100]
+    rng = np.random.default_rng(8)
+    idx = rng.integers(0, len(vals), 50_001)
+    letters = W.letters_u128([vals[i] for i in idx])
+    wmap = W.build_weights_map(letters, ctx)
+    items = list(wmap.items())
+    t = W.WideTree.from_weights(items, W.U128)
+    cd = W.compress_with_tree(letters, t, ctx)
+    rank = {v: r for r, v in enumerate(vals)}
+    ot = O.Tree.from_leaves([rank[k] for k, _ in items], [w for _, w in items])
+    ocomp, opad = O.wcompress_with_tree(np.asarray([rank[vals[i]] for i in idx], np.uint64), ot)
+    assert cd.comp_bytes() == ocomp and cd.padding_bits() == opad
+    assert W.decompress(cd, ctx).tobytes() == letters.tobytes()
+
+
 def test_missing_letter_first_in_input_order(W, ctx):
     """comp.rs:426-432: CompressError for the first letter without a code"""
     import huff_coding as H
