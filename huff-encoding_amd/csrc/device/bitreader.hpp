@@ -19,6 +19,15 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_wave_barrier();
 }
 
+// orders a wave's LDS accesses across lanes without waiting for them: the LDS
+// executes one wave's DS instructions in issue order, so a later read sees an
+// earlier write (or ds_or) of any lane; only the compiler must not move
+// memory operations across (register results still get their own waits)
+__device__ __forceinline__ void wave_order() {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+}
+
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 
 // 16-byte streaming load that does not pollute the caches

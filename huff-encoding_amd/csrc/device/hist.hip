@@ -260,15 +260,50 @@ __global__ __launch_bounds__(1024) void k_scan_tiles(const uint64_t* __restrict_
     if (t == 0) tsum[blockIdx.x] = tot;
 }
 
-// k_scan_fix: add base + the totals of the tiles before; the last tile also
-// writes start[nchunks]
-__global__ __launch_bounds__(1024) void k_scan_fix(uint32_t nchunks, uint64_t base, const uint64_t* __restrict__ tsum,
-                                                   uint64_t* __restrict__ start) {
+// k_scan_tsum: one workgroup turns the tile totals into exclusive prefixes in
+// place (tsum[tiles] = the grand total): each thread scans a run of tiles
+// (the index-free decode has ~5,400 tiles per GiB: the per-tile sum over all
+// earlier tiles this replaces read 15 M words)
+__global__ __launch_bounds__(1024) void k_scan_tsum(uint32_t tiles, uint64_t* __restrict__ tsum) {
+    __shared__ uint64_t wsum[16];
+    const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const uint32_t per = (tiles + 1023) / 1024;
+    const uint32_t lo = t * per < tiles ? t * per : tiles, hi = lo + per < tiles ? lo + per : tiles;
+    uint64_t mine = 0;
+    for (uint32_t q = lo; q < hi; ++q) mine += tsum[q];
+    uint64_t incl = mine;  // wave inclusive scan (64-bit shuffles)
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t v = __shfl_up(incl, d, 64);
+        if (lane >= static_cast<uint32_t>(d)) incl += v;
+    }
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    uint64_t pre = 0, tot = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < 16; ++w) {
+        pre += (w < wave) ? wsum[w] : 0u;
+        tot += wsum[w];
+    }
+    uint64_t run = pre + incl - mine;
+    for (uint32_t q = lo; q < hi; ++q) {
+        const uint64_t v = tsum[q];
+        tsum[q] = run;
+        run += v;
+    }
+    if (t == 0) tsum[tiles] = tot;
+}
+
+// k_scan_fix_small (<= 64 tiles, the encoder's case: one launch less): add
+// base + the totals of the tiles before, summed by one wave per tile; the
+// last tile also writes start[nchunks]
+__global__ __launch_bounds__(1024) void k_scan_fix_small(uint32_t nchunks, uint64_t base,
+                                                         const uint64_t* __restrict__ tsum,
+                                                         uint64_t* __restrict__ start) {
     __shared__ uint64_t off;
     const uint32_t t = threadIdx.x;
-    if (t < 64) {  // one wave sums the tsum[q], q < blockIdx.x
-        uint64_t sum = 0;
-        for (uint32_t q = t; q < blockIdx.x; q += 64) sum += tsum[q];
+    if (t < 64) {
+        uint64_t sum = t < blockIdx.x ? tsum[t] : 0;
 #pragma unroll
         for (int d = 32; d >= 1; d >>= 1) sum += __shfl_down(sum, d, 64);
         if (t == 0) off = base + sum;
@@ -277,6 +312,17 @@ __global__ __launch_bounds__(1024) void k_scan_fix(uint32_t nchunks, uint64_t ba
     const uint32_t i = blockIdx.x * 1024 + t;
     if (i < nchunks) start[i] += off;
     if (blockIdx.x == gridDim.x - 1 && t == 0) start[nchunks] = off + tsum[blockIdx.x];
+}
+
+// k_scan_fix: add base + the exclusive prefix of the tile totals; the last
+// tile also writes start[nchunks]
+__global__ __launch_bounds__(1024) void k_scan_fix(uint32_t nchunks, uint64_t base, const uint64_t* __restrict__ tsum,
+                                                   uint64_t* __restrict__ start) {
+    const uint32_t t = threadIdx.x;
+    const uint64_t off = base + tsum[blockIdx.x];
+    const uint32_t i = blockIdx.x * 1024 + t;
+    if (i < nchunks) start[i] += off;
+    if (blockIdx.x == gridDim.x - 1 && t == 0) start[nchunks] = base + tsum[gridDim.x];
 }
 
 // lowest index i with missing_mask[in[i]] != 0 (error path of compress_with_tree)
@@ -333,7 +379,12 @@ hipError_t launch_scan(const uint64_t* bits, uint32_t nchunks, uint64_t base, ui
                        hipStream_t s) {
     const uint32_t tiles = nchunks ? (nchunks + 1023) / 1024 : 1;
     hipLaunchKernelGGL(k_scan_tiles, dim3(tiles), dim3(1024), 0, s, bits, nchunks, start, tsum);
-    hipLaunchKernelGGL(k_scan_fix, dim3(tiles), dim3(1024), 0, s, nchunks, base, tsum, start);
+    if (tiles <= 64) {
+        hipLaunchKernelGGL(k_scan_fix_small, dim3(tiles), dim3(1024), 0, s, nchunks, base, tsum, start);
+    } else {
+        hipLaunchKernelGGL(k_scan_tsum, dim3(1), dim3(1024), 0, s, tiles, tsum);
+        hipLaunchKernelGGL(k_scan_fix, dim3(tiles), dim3(1024), 0, s, nchunks, base, tsum, start);
+    }
     return hipGetLastError();
 }
 

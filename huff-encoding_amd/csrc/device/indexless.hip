@@ -341,23 +341,54 @@ struct Cursor {
             L[k] = step<SLOW>(stab, K, glut, Kg);
         }
     }
+    // kChunkSteps windows, each consuming ALL its complete codes (walk table:
+    // bits used, count): U bits and N codes in total, ~2 codes per lookup on
+    // Zipf bytes. A window whose first code is longer than K takes that code.
+    template <bool SLOW>
+    __device__ __forceinline__ void multi_chunk(uint32_t& U, uint32_t& N, const uint16_t* wtab, const uint16_t* stab,
+                                                uint32_t K, const uint32_t* glut, uint32_t Kg) {
+        U = 0;
+        N = 0;
+#pragma unroll
+        for (int k = 0; k < kChunkSteps; ++k) {
+            if ((k & 1) == 0) refill();
+            const uint32_t e = wtab[static_cast<uint32_t>(buf >> 32) >> (32 - K)];
+            if (SLOW && (e & kWtSlow)) {
+                U += step<SLOW>(stab, K, glut, Kg);
+                N += 1;
+            } else {
+                const uint32_t u = e & 15u;
+                buf <<= u;
+                X -= u;
+                U += u;
+                N += (e >> 4) & 15u;
+            }
+        }
+    }
 };
 
-// LDS: [single-symbol table][staged input]
+// LDS: [single-symbol table][walk table (if any)][staged input]
+__device__ __forceinline__ uint32_t stab_words(const IndexlessArgs& a) {
+    return ((((1u << a.stab_bits) + 1) / 2) + 3) & ~3u;
+}
+__device__ __forceinline__ uint32_t tables_words(const IndexlessArgs& a) {
+    return stab_words(a) * (a.wtab ? 2u : 1u);
+}
 __device__ __forceinline__ const uint16_t* load_stab(const IndexlessArgs& a, uint32_t* lds) {
     const uint32_t words = ((1u << a.stab_bits) + 1) / 2;
     for (uint32_t i = threadIdx.x; i < words; i += blockDim.x) lds[i] = reinterpret_cast<const uint32_t*>(a.stab)[i];
+    if (a.wtab)
+        for (uint32_t i = threadIdx.x; i < words; i += blockDim.x)
+            lds[stab_words(a) + i] = reinterpret_cast<const uint32_t*>(a.wtab)[i];
     return reinterpret_cast<const uint16_t*>(lds);
-}
-__device__ __forceinline__ uint32_t stab_words(const IndexlessArgs& a) {
-    return ((((1u << a.stab_bits) + 1) / 2) + 3) & ~3u;
 }
 
 template <bool SLOW>
 __global__ __launch_bounds__(kThreads) void k_spec_lds(IndexlessArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const uint16_t* stab = load_stab(a, lds);
-    const Staged st = stage_block(a, lds + stab_words(a));
+    const uint16_t* wtab = a.wtab ? stab + 2 * stab_words(a) : nullptr;
+    const Staged st = stage_block(a, lds + tables_words(a));
     __syncthreads();
     const uint64_t i0 = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
     const bool live = i0 < a.nseg;  // no early return: the fix-up below has a barrier
@@ -376,6 +407,28 @@ __global__ __launch_bounds__(kThreads) void k_spec_lds(IndexlessArgs a) {
     uint64_t next_bit = (a.nsamp && live) ? start + kSampBits : ~0ull;
     uint64_t sp1 = ~0ull;  // the first sample (position, spec-local index)
     uint32_t si1 = 0;
+    auto note_sample = [&]() {
+        if (cur >= next_bit) {
+            smp[next_k - 1] = (static_cast<uint32_t>(cnt) << 16) | static_cast<uint32_t>(cur - start);
+            if (next_k == 1) {  // kept for the fix-up below
+                sp1 = cur;
+                si1 = static_cast<uint32_t>(cnt);
+            }
+            next_bit = ++next_k <= a.nsamp ? next_bit + kSampBits : ~0ull;
+        }
+    };
+    if (wtab) {
+        // multi-code chunks while the chunk's last boundary stays below `end`
+        // (so no boundary inside it can be the exit); single codes after
+        const uint64_t span = static_cast<uint64_t>(kChunkSteps) * (a.max_len > K ? a.max_len : K);
+        while (cur + span < end) {
+            uint32_t U, N;
+            c.multi_chunk<SLOW>(U, N, wtab, stab, K, a.lut, Kg);
+            cur += U;
+            cnt += N;
+            note_sample();
+        }
+    }
     for (;;) {
         uint32_t L[kChunkSteps];
         c.chunk<SLOW>(L, stab, K, a.lut, Kg);
@@ -400,14 +453,7 @@ __global__ __launch_bounds__(kThreads) void k_spec_lds(IndexlessArgs a) {
         }
         cur = p;
         cnt += kChunkSteps;
-        if (cur >= next_bit) {
-            smp[next_k - 1] = (static_cast<uint32_t>(cnt) << 16) | static_cast<uint32_t>(cur - start);
-            if (next_k == 1) {  // kept for the fix-up below
-                sp1 = cur;
-                si1 = static_cast<uint32_t>(cnt);
-            }
-            next_bit = ++next_k <= a.nsamp ? next_bit + kSampBits : ~0ull;
-        }
+        note_sample();
     }
     if (live)
         for (; next_k <= a.nsamp; ++next_k) smp[next_k - 1] = ~0u;
@@ -509,7 +555,7 @@ __global__ __launch_bounds__(kThreads) void k_mark_lds(IndexlessArgs a, const ui
                                                        uint64_t* __restrict__ sub_abs, uint32_t shift) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const uint16_t* stab = load_stab(a, lds);
-    const Staged st = stage_block(a, lds + stab_words(a));
+    const Staged st = stage_block(a, lds + tables_words(a));
     __syncthreads();
     const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
     if (i >= a.nseg) return;
@@ -551,7 +597,7 @@ __global__ __launch_bounds__(kThreads) void k_mark_lds(IndexlessArgs a, const ui
 }  // namespace
 
 static size_t lds_staged_bytes(const IndexlessArgs& a) {
-    return static_cast<size_t>(((((1u << a.stab_bits) + 1) / 2) + 3) & ~3u) * 4 +
+    return static_cast<size_t>(((((1u << a.stab_bits) + 1) / 2) + 3) & ~3u) * 4 * (a.wtab ? 2 : 1) +
            ((kThreads * a.seg_bits + 7) / 8 + 128 + 15) / 16 * 16;
 }
 
@@ -564,8 +610,10 @@ hipError_t launch_indexless_mark(const IndexlessArgs& a, const uint64_t* off, ui
     if (a.nseg == 0) return hipSuccess;
     if (!use_staged(a) || !a.samp) return hipErrorInvalidValue;
     const bool slow = a.max_len > a.stab_bits;
-    hipLaunchKernelGGL(slow ? k_mark_lds<true> : k_mark_lds<false>, dim3((a.nseg + kThreads - 1) / kThreads),
-                       dim3(kThreads), lds_staged_bytes(a), st, a, off, sub_abs, shift);
+    IndexlessArgs m = a;
+    m.wtab = nullptr;  // single steps: the walks stop at exact counts
+    hipLaunchKernelGGL(slow ? k_mark_lds<true> : k_mark_lds<false>, dim3((m.nseg + kThreads - 1) / kThreads),
+                       dim3(kThreads), lds_staged_bytes(m), st, m, off, sub_abs, shift);
     return hipGetLastError();
 }
 

@@ -27,7 +27,10 @@ constexpr uint32_t kHistCopies = 8;     // XCD-group copies of the global weight
 constexpr uint32_t kLutMaxBits = 12;    // primary decode table index bits
 constexpr uint32_t kLutPtr = 0x80000000u;
 constexpr uint32_t kPackWaveRound = 1024;  // bytes per wave round in pack (64 lanes x 16 B: ~80 VGPRs, 6 waves per SIMD)
-constexpr uint32_t kPackWaves = 8;         // waves per pack workgroup (short codes; long codes: 4)
+#ifndef HUFF_PACK_WAVES
+#define HUFF_PACK_WAVES 8
+#endif
+constexpr uint32_t kPackWaves = HUFF_PACK_WAVES;  // waves per pack workgroup (short codes; long codes: 4)
 // multi-symbol decode entry: up to 3 letters in bits [0, 24), bits used in
 // [24, 29), letter count in [29, 31); kMsSlow: the first code is longer than
 // the table's index bits (decode it with the single-symbol tables)
@@ -133,7 +136,12 @@ struct IndexlessArgs {
     unsigned int* flags;          // [kFixRounds]: round r found a changed exit
     const uint16_t* stab;         // single-symbol table (k_decode_fixed's): the LDS-staged kernels
     uint32_t stab_bits;
+    // multi-code walk table over the same stab_bits-bit windows: bits [0, 4)
+    // = bits of the window's complete codes, [4, 8) = their count; kWtSlow:
+    // the first code is longer than the window (null: single steps only)
+    const uint16_t* wtab;
 };
+constexpr uint32_t kWtSlow = 0x8000u;
 constexpr uint32_t kSampBits = 128;
 constexpr uint32_t kSampMax = 8;  // samples kept per segment (nsamp <= kSampMax)
 constexpr uint32_t kNoMerge = 0xFFFFFFFFu;

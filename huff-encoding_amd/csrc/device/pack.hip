@@ -242,6 +242,9 @@ __global__ __launch_bounds__(pack_waves<LONG>() * 64) void k_pack(PackArgs a) {
         };
         LaneIn v0 = load_round(0);
         LaneIn v1 = load_round(1);
+#if HUFF_PACK_AHEAD3
+        LaneIn v2 = load_round(2);
+#endif
 
         // bits of the shared first byte that belong to the symbols before this chunk
         if (lane == 0 && (cs & 7)) {
@@ -276,7 +279,12 @@ __global__ __launch_bounds__(pack_waves<LONG>() * 64) void k_pack(PackArgs a) {
         for (uint32_t r = 0; r < nrounds; ++r) {
             const LaneIn v = v0;
             v0 = v1;
+#if HUFF_PACK_AHEAD3
+            v1 = v2;
+            v2 = load_round(r + 3);
+#else
             v1 = load_round(r + 2);
+#endif
             // 32-bit: a chunk holds at most 65536 symbols
             const uint32_t s_in_chunk = r * kPackWaveRound + lane * kBPL;
             const uint32_t nsym32 = static_cast<uint32_t>(nsym);
@@ -316,7 +324,7 @@ __global__ __launch_bounds__(pack_waves<LONG>() * 64) void k_pack(PackArgs a) {
             } else {
                 emit_codes_or<G>(stage, static_cast<uint32_t>(round_bit - stage_bit0 + excl), ent);
             }
-            wave_sync();
+            wave_order();
 
             const uint64_t end_bit = round_bit + tot;
             const bool last = (r + 1 == nrounds);
@@ -331,15 +339,15 @@ __global__ __launch_bounds__(pack_waves<LONG>() * 64) void k_pack(PackArgs a) {
             const uint32_t used_words = static_cast<uint32_t>((end_bit - stage_bit0 + 31) >> 5);
             uint32_t keep = 0;
             if (!last && lane < 4) keep = stage[nseg_done * 4 + lane];
-            wave_sync();
+            wave_order();
             // clear what this round wrote (16-B stores); carry the partial segment to the front
             for (uint32_t i = lane; i < (used_words + 3) / 4; i += 64)
                 reinterpret_cast<uint4*>(stage)[i] = make_uint4(0, 0, 0, 0);
-            wave_sync();
+            wave_order();
             if (!last) {
                 if (lane < 4) stage[lane] = keep;
                 stage_bit0 += static_cast<uint64_t>(nseg_done) << 7;
-                wave_sync();
+                wave_order();
             }
             round_bit = end_bit;
         }

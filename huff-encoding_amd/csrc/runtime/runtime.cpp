@@ -147,6 +147,30 @@ static void build_single_table(const HuffTree& t, uint32_t sbits, DecTables& out
     }
 }
 
+// entry i of the walk table: every complete code of the sbits-bit window i
+// (bits used, count), for walking a stream without its letters
+static void build_walk_table(const HuffTree& t, uint32_t sbits, DecTables& out) {
+    const auto& nodes = t.nodes();
+    const uint32_t n = 1u << sbits;
+    out.woff = static_cast<uint32_t>(out.lut.size());
+    out.lut.resize(out.lut.size() + (n + 1) / 2, 0);
+    uint16_t* w = reinterpret_cast<uint16_t*>(out.lut.data() + out.woff);
+    const bool root_leaf = t.root_is_leaf();
+    for (uint32_t i = 0; i < n; ++i) {
+        uint32_t used = 0, count = 0;
+        int32_t x = t.root();
+        for (uint32_t p = 0; p < sbits; ++p) {
+            if (!root_leaf) x = ((i >> (sbits - 1 - p)) & 1u) ? nodes[x].right : nodes[x].left;
+            if (nodes[x].is_leaf) {
+                ++count;
+                used = p + 1;
+                x = t.root();
+            }
+        }
+        w[i] = count ? static_cast<uint16_t>(used | (count << 4)) : static_cast<uint16_t>(dev::kWtSlow);
+    }
+}
+
 Status build_dec_tables(const HuffTree& t, DecTables& out) {
     const auto& nodes = t.nodes();
     out.lut.clear();
@@ -157,6 +181,7 @@ Status build_dec_tables(const HuffTree& t, DecTables& out) {
         out.lut = {e, e};
         build_multi_table(t, ms_bits(), out);
         build_single_table(t, 1, out);
+        build_walk_table(t, 1, out);
         return Status::ok();
     }
     const uint32_t maxd = t.max_depth();  // > dev::kLongMaxLen: the deep kernels (deep.hip)
@@ -206,6 +231,7 @@ Status build_dec_tables(const HuffTree& t, DecTables& out) {
     }
     build_multi_table(t, ms_bits(), out);
     build_single_table(t, std::min<uint32_t>(maxd, dev::kSsMaxBits), out);
+    build_walk_table(t, out.sbits, out);
     return Status::ok();
 }
 
@@ -933,6 +959,7 @@ Status indexless_sync(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_bytes,
     a.max_len = dt->maxdepth;
     a.stab = reinterpret_cast<const uint16_t*>(static_cast<const uint32_t*>(ctx->d_lut.p) + dt->soff);
     a.stab_bits = dt->sbits;
+    a.wtab = reinterpret_cast<const uint16_t*>(static_cast<const uint32_t*>(ctx->d_lut.p) + dt->woff);
     a.tm = static_cast<uint32_t*>(st.tm.p);
     a.dl = static_cast<int32_t*>(st.dl.p);
     a.flags = static_cast<unsigned int*>(st.flag.p);

@@ -51,6 +51,9 @@ struct DecTables {
     // entries per word at word `soff`: [1 << sbits] entries, used | letter << 8,
     // kSsSlow for windows whose first code is longer than sbits
     uint32_t sbits = 0, soff = 0;
+    // multi-code walk table (indexless.hip's speculative pass): [1 << sbits]
+    // u16 entries at word `woff`, dev::kWtSlow / used | count << 4
+    uint32_t woff = 0;
 };
 
 // append the multi-symbol table (decode.hip k_decode_ms) to out.lut
