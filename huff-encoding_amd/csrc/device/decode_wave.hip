@@ -55,17 +55,25 @@ struct Task {
     uint32_t cnt;       // this lane's symbols
     uint64_t b0;        // first staged byte (16-B aligned)
     uint32_t len;       // staged bytes
-    uint64_t end;       // the task's end bit (= the next task's first bit)
+    uint64_t end;       // the task's end bit (= the next task's first bit; SKIP: a bound)
+    uint32_t skip;      // SKIP: codes to decode and drop before this lane's letters
 };
 
+// SKIP: the index-free path's k_mark_lite entries (boundary | skip << 48)
+template <bool SKIP = false>
 __device__ __forceinline__ Task task_info(const DecodeArgs& a, uint64_t t, uint32_t lane) {
     Task k;
     k.sym0 = t * kTaskSym;
     k.nsym = static_cast<uint32_t>(a.n - k.sym0 < kTaskSym ? a.n - k.sym0 : kTaskSym);
     const uint32_t ls = lane * kLaneSym;
     k.cnt = ls >= k.nsym ? 0u : (k.nsym - ls < kLaneSym ? k.nsym - ls : kLaneSym);
+    k.skip = 0;
     if (a.sub_abs64) {  // index-free streams: absolute start bit of every 64th symbol (k_mark_lds)
         k.lane_bit = k.cnt ? a.sub_abs64[k.sym0 / kIdx + lane] : 0;
+        if constexpr (SKIP) {
+            k.skip = static_cast<uint32_t>(k.lane_bit >> 48);
+            k.lane_bit &= kSkipPosMask;
+        }
     } else {
         const uint32_t c = static_cast<uint32_t>(k.sym0 / kChunk);
         k.lane_bit = k.cnt ? a.chunk_start[c] + a.sub_bit[k.sym0 / kIdx + lane] : 0;
@@ -78,6 +86,8 @@ __device__ __forceinline__ Task task_info(const DecodeArgs& a, uint64_t t, uint3
     uint64_t end;
     if (a.sub_abs64) {
         end = next < a.n ? a.sub_abs64[next / kIdx] : a.end_bit;
+        if constexpr (SKIP)  // the next task's first bit lies within its skipped codes
+            if (next < a.n) end = (end & kSkipPosMask) + (end >> 48) * a.max_len;
     } else if (next < a.n) {
         end = a.chunk_start[next / kChunk] + a.sub_bit[next / kIdx];
     } else {
@@ -308,10 +318,11 @@ __global__ __launch_bounds__(kThreads) void k_decode_wave(DecodeArgs a) {
 // don't-care (X -= entry borrows only from them)
 // Invariant: the window's valid bits end at stream bit 32 rp, so the lane's
 // position after its 64 letters is 32 rp - nb (*end_rel, for the self-check).
-template <bool SLOW, class Words>
+template <bool SLOW, bool SKIP, class Words>
 __device__ __forceinline__ void decode_fixed64(const Words& src, uint32_t rel, uint32_t (&o)[16],
                                                const uint16_t* __restrict__ stab, uint32_t K,
-                                               const uint32_t* __restrict__ glut, uint32_t Ks, uint32_t* end_rel) {
+                                               const uint32_t* __restrict__ glut, uint32_t Ks, uint32_t* end_rel,
+                                               uint32_t skip) {
     uint32_t rp = rel >> 5;
     const uint32_t sh = rel & 31;
     uint64_t buf = static_cast<uint64_t>(src(rp) << sh) << 32;
@@ -352,7 +363,40 @@ __device__ __forceinline__ void decode_fixed64(const Words& src, uint32_t rel, u
                                                  ((i) & 3) == 1 ? 0x0C0C0500u                 \
                                                  : ((i) & 3) == 2 ? 0x0C050100u : 0x05020100u); \
     } while (0)
+// one code consumed, its letter dropped (the SKIP build's leading codes)
+#define FX_STEP()                                                                             \
+    do {                                                                                      \
+        uint32_t e = stab[static_cast<uint32_t>(buf >> 32) >> (32 - K)];                      \
+        if (SLOW && (e & kSsSlow)) {                                                          \
+            FX_REFILL();                                                                      \
+            uint32_t e1 = glut[static_cast<uint32_t>(buf >> (64 - Ks))];                      \
+            uint32_t d1 = Ks;                                                                 \
+            while (e1 & kLutPtr) {                                                            \
+                const uint32_t idx = static_cast<uint32_t>((buf >> (56 - d1)) & 0xFFu);       \
+                e1 = glut[(e1 & ~kLutPtr) + idx];                                             \
+                d1 += 8;                                                                      \
+            }                                                                                 \
+            const uint32_t l1 = (e1 >> 8) & 0xFFu;                                            \
+            buf <<= l1;                                                                       \
+            X -= l1;                                                                          \
+            FX_REFILL();                                                                      \
+            e = 0;                                                                            \
+        }                                                                                     \
+        buf <<= (e & 63u);                                                                    \
+        X -= e;                                                                               \
+    } while (0)
 
+    if constexpr (SKIP) {  // codes before this lane's first letter: decoded, not kept
+        for (uint32_t j = skip; j >= 2; j -= 2) {
+            FX_REFILL();
+            FX_STEP();
+            FX_STEP();
+        }
+        if (skip & 1u) {
+            FX_REFILL();
+            FX_STEP();
+        }
+    }
 #pragma unroll
     for (int i = 0; i < 64; i += 2) {
         FX_REFILL();
@@ -360,32 +404,34 @@ __device__ __forceinline__ void decode_fixed64(const Words& src, uint32_t rel, u
         FX_LOOKUP(i + 1);
     }
     *end_rel = 32 * rp - (X & 63u);
+#undef FX_STEP
 #undef FX_LOOKUP
 #undef FX_REFILL
 }
 
-template <bool SLOW, bool PAD>
+template <bool SLOW, bool PAD, bool SKIP = false>
 __device__ __forceinline__ void decode_fixed64_stage(const uint32_t* stage, uint32_t rel, uint32_t (&o)[16],
                                                      const uint16_t* __restrict__ stab, uint32_t K,
                                                      const uint32_t* __restrict__ glut, uint32_t Ks,
-                                                     uint32_t* end_rel) {
+                                                     uint32_t* end_rel, uint32_t skip = 0) {
     if constexpr (PAD)
-        decode_fixed64<SLOW>(PaddedLdsWords{stage}, rel, o, stab, K, glut, Ks, end_rel);
+        decode_fixed64<SLOW, SKIP>(PaddedLdsWords{stage}, rel, o, stab, K, glut, Ks, end_rel, skip);
     else
-        decode_fixed64<SLOW>(LdsWords{stage}, rel, o, stab, K, glut, Ks, end_rel);
+        decode_fixed64<SLOW, SKIP>(LdsWords{stage}, rel, o, stab, K, glut, Ks, end_rel, skip);
 }
 
 // fallback for a task whose compressed range exceeds the stage: a compact
 // loop straight from global memory, one letter per lookup stored as a byte
 template <class Words>
 __device__ __forceinline__ uint32_t decode_fixed_global(const Words& src, uint32_t rel, uint32_t cnt, uint8_t* dst,
-                                                     const uint32_t* __restrict__ glut, uint32_t Ks) {
+                                                     const uint32_t* __restrict__ glut, uint32_t Ks,
+                                                     uint32_t skip = 0) {
     uint32_t rp = rel >> 5;
     const uint32_t sh = rel & 31;
     uint64_t buf = ((static_cast<uint64_t>(src(rp)) << 32) | src(rp + 1)) << sh;
     uint32_t nb = 64 - sh;
     rp += 2;
-    for (uint32_t j = 0; j < cnt; ++j) {
+    for (uint32_t j = 0; j < skip + cnt; ++j) {  // the first `skip` letters are dropped
         if (nb < 32) {
             buf |= static_cast<uint64_t>(src(rp)) << (32 - nb);
             nb += 32;
@@ -401,7 +447,7 @@ __device__ __forceinline__ uint32_t decode_fixed_global(const Words& src, uint32
         const uint32_t l1 = (e1 >> 8) & 0xFFu;
         buf <<= l1;
         nb -= l1;
-        dst[j] = static_cast<uint8_t>(e1);
+        if (j >= skip) dst[j - skip] = static_cast<uint8_t>(e1);
     }
     return 32 * rp - nb;  // end position (valid bits end at 32 rp)
 }
@@ -445,8 +491,9 @@ __device__ __forceinline__ void fx_check(const DecodeArgs& a, const Task& k, uin
     }
 }
 
-template <bool SLOW, bool PAD, bool CHECK>
+template <bool SLOW, bool PAD, bool CHECK, bool SKIP = false>
 __device__ __forceinline__ void decode_fixed_body(const DecodeArgs& a) {
+    static_assert(!(CHECK && SKIP), "the self-check needs exact lane starts");
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const uint32_t K = a.stab_bits;
     const uint32_t nent = 1u << K;
@@ -465,7 +512,7 @@ __device__ __forceinline__ void decode_fixed_body(const DecodeArgs& a) {
     uint64_t task = static_cast<uint64_t>(blockIdx.x) * kWaves + wave;
     if (task >= ntasks) return;
 
-    Task cur = task_info(a, task, lane);
+    Task cur = task_info<SKIP>(a, task, lane);
 
     // no software prefetch of the next task: its 20 registers would cost a
     // wave per SIMD; the other resident waves hide the load latency instead.
@@ -496,12 +543,12 @@ __device__ __forceinline__ void decode_fixed_body(const DecodeArgs& a) {
         if (cur.len > kInCap) {
             uint32_t e = 0;
             if (cur.cnt) e = decode_fixed_global(GlobalWords{a.comp, a.comp_bytes, cur.b0 / 4}, rel, cur.cnt, dst,
-                                                 a.lut, a.lut_bits);
+                                                 a.lut, a.lut_bits, SKIP ? cur.skip : 0u);
             fx_check<CHECK>(a, cur, task, lane, cur.b0 * 8 + e, cur.cnt != 0);
         } else if (cur.nsym == kTaskSym) {  // wave-uniform: every lane has 64 letters
             uint32_t o[16];
             uint32_t e = 0;
-            decode_fixed64_stage<SLOW, PAD>(stage, rel, o, stab, K, a.lut, a.lut_bits, &e);
+            decode_fixed64_stage<SLOW, PAD, SKIP>(stage, rel, o, stab, K, a.lut, a.lut_bits, &e, cur.skip);
             fx_check<CHECK>(a, cur, task, lane, cur.b0 * 8 + e, true);
             // transpose through the stage so every store instruction writes
             // 1 KiB contiguous (16 B per lane): lane-strided 16-B pieces cost
@@ -519,7 +566,7 @@ __device__ __forceinline__ void decode_fixed_body(const DecodeArgs& a) {
         } else if (cur.cnt) {
             uint32_t o[16];
             uint32_t e = 0;
-            decode_fixed64_stage<SLOW, PAD>(stage, rel, o, stab, K, a.lut, a.lut_bits, &e);
+            decode_fixed64_stage<SLOW, PAD, SKIP>(stage, rel, o, stab, K, a.lut, a.lut_bits, &e, cur.skip);
             // a lane with fewer than 64 letters decodes past its end: only full lanes are checked
             fx_check<CHECK>(a, cur, task, lane, cur.b0 * 8 + e, cur.cnt == kLaneSym);
             if (cur.cnt == kLaneSym) {
@@ -537,7 +584,7 @@ __device__ __forceinline__ void decode_fixed_body(const DecodeArgs& a) {
         if (!more) break;
         wave_sync();  // the input stage is reused by the next task
         task = nxt_task;
-        cur = task_info(a, task, lane);
+        cur = task_info<SKIP>(a, task, lane);
     }
 }
 
@@ -564,6 +611,12 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(5, 8))
 template <bool SLOW, bool PAD>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_decode_fixed_chk_spill(DecodeArgs a) {
     decode_fixed_body<SLOW, PAD, true>(a);
+}
+// index-free streams with k_mark_lite's entries: each lane first decodes and
+// drops its skip codes
+template <bool SLOW, bool PAD>
+__global__ __launch_bounds__(kThreads) void k_decode_fixed_skip(DecodeArgs a) {
+    decode_fixed_body<SLOW, PAD, false, true>(a);
 }
 // diagnostics: the production body (no check) forced to >= 5 waves per SIMD
 template <bool SLOW, bool PAD>
@@ -619,8 +672,11 @@ hipError_t launch_decode_fixed(const DecodeArgs& a, hipStream_t s) {
         {{k_decode_fixed_w5<false, false>, k_decode_fixed_w5<false, true>},
          {k_decode_fixed_w5<true, false>, k_decode_fixed_w5<true, true>}},
     };
+    static const K skip_table[2][2] = {{k_decode_fixed_skip<false, false>, k_decode_fixed_skip<false, true>},
+                                       {k_decode_fixed_skip<true, false>, k_decode_fixed_skip<true, true>}};
     if (a.check_mode > 4 || (a.check_mode && !a.err)) return hipErrorInvalidValue;
-    K kern = table[a.check_mode][slow][pad];
+    if (a.skip_packed && (a.check_mode || !a.sub_abs64)) return hipErrorInvalidValue;
+    K kern = a.skip_packed ? skip_table[slow][pad] : table[a.check_mode][slow][pad];
     // persistent grid = resident workgroups (registers and LDS both limit)
     int per_cu = 0;
     hipError_t err = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kThreads, lds);

@@ -151,7 +151,11 @@ __global__ void k_walk_end(WalkEndArgs a) {
     if (threadIdx.x != 0) return;
     const BitSrc src{reinterpret_cast<const uint32_t*>(a.comp), a.comp, a.comp_bytes};
     uint64_t pos = a.start ? *a.start : a.start_v;
-    const uint64_t cnt = a.count ? *a.count : a.count_v;
+    uint64_t cnt = a.count ? *a.count : a.count_v;
+    if (a.start_packed) {  // a k_mark_lite entry: boundary | codes to skip << 48
+        cnt += pos >> 48;
+        pos &= kSkipPosMask;
+    }
     for (uint64_t j = 0; j < cnt; ++j) pos += (deep_lookup(src, prim, a.lut_bits, a.lut, pos) >> 8) & 0xFFu;
     *a.end = pos;
 }

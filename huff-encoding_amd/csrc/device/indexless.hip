@@ -594,7 +594,57 @@ __global__ __launch_bounds__(kThreads) void k_mark_lds(IndexlessArgs a, const ui
     }
 }
 
+// the same marks as k_mark_lds without walking: each is written as the
+// boundary it would walk from and the number of codes to walk, and the
+// fixed-count decoder (skip build) decodes those codes without storing them.
+// No staging and no table: only the segment records and its samples.
+__global__ __launch_bounds__(kThreads) void k_mark_lite(IndexlessArgs a, const uint64_t* __restrict__ off,
+                                                        uint64_t* __restrict__ sub_abs) {
+    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= a.nseg) return;
+    const uint64_t j0 = off[i];
+    const uint64_t cnt = a.c[i];
+    uint64_t m = (j0 + kIdx - 1) & ~static_cast<uint64_t>(kIdx - 1);
+    if (m >= j0 + cnt) return;
+    const uint64_t s_true = a.s[i];
+    const uint64_t s_spec = i * a.seg_bits;
+    const uint32_t tm = a.tm[i];
+    const int64_t dl = a.dl[i];
+    uint32_t sv[kSampMax];
+#pragma unroll
+    for (uint32_t k = 0; k < kSampMax; ++k) sv[k] = k < a.nsamp ? a.samp[i * a.nsamp + k] : ~0u;
+    for (; m < j0 + cnt; m += kIdx) {
+        const uint32_t t = static_cast<uint32_t>(m - j0);
+        uint64_t pos;
+        uint32_t skip;
+        if (tm == kNoMerge || t < tm) {
+            pos = s_true;
+            skip = t;
+        } else {
+            const uint32_t u = static_cast<uint32_t>(static_cast<int64_t>(t) - dl);
+            uint32_t idx = 0, rel = 0;
+#pragma unroll
+            for (uint32_t k = 0; k < kSampMax; ++k) {  // samples ascend; ~0u never qualifies
+                const bool ok = (sv[k] >> 16) <= u;
+                idx = ok ? sv[k] >> 16 : idx;
+                rel = ok ? sv[k] & 0xFFFFu : rel;
+            }
+            pos = s_spec + rel;
+            skip = u - idx;
+        }
+        sub_abs[m / kIdx] = pos | (static_cast<uint64_t>(skip) << 48);
+    }
+}
+
 }  // namespace
+
+hipError_t launch_indexless_mark_lite(const IndexlessArgs& a, const uint64_t* off, uint64_t* sub_abs,
+                                      hipStream_t st) {
+    if (a.nseg == 0) return hipSuccess;
+    if (!a.samp) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_mark_lite, dim3((a.nseg + kThreads - 1) / kThreads), dim3(kThreads), 0, st, a, off, sub_abs);
+    return hipGetLastError();
+}
 
 static size_t lds_staged_bytes(const IndexlessArgs& a) {
     return static_cast<size_t>(((((1u << a.stab_bits) + 1) / 2) + 3) & ~3u) * 4 * (a.wtab ? 2 : 1) +

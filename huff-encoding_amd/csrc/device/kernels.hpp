@@ -91,6 +91,9 @@ struct DecodeArgs {
     // kIdx-th symbol (instead of chunk_start + sub_bit) and the stream's end
     const uint64_t* sub_abs64;
     uint64_t end_bit;
+    // sub_abs64 entries as k_mark_lite writes them: a boundary at or before
+    // the symbol in bits [0, 48) and the codes to skip from it in [48, 64)
+    uint32_t skip_packed;
     // k_decode_fixed: pad the input stage (one 16-B piece per 8) — for mean
     // code lengths near 4, 8 or 12 bits the lanes' streams start a multiple of
     // 8 dwords apart and every refill would hit the same few LDS banks
@@ -233,6 +236,7 @@ struct WalkEndArgs {
     uint32_t lut_bits;
     const uint64_t* start;        // device value, or start_v when null
     uint64_t start_v;
+    uint32_t start_packed;        // *start is a k_mark_lite entry (position | skip << 48)
     const uint64_t* count;        // device value, or count_v when null
     uint64_t count_v;
     unsigned long long* end;
@@ -300,6 +304,10 @@ hipError_t launch_indexless_emit(const IndexlessArgs& a, const uint64_t* off, ui
 // restart index for the ring decoder: sub_abs[g] = start bit of symbol 256 g
 // sub_abs[g] = start bit of symbol g << shift (shift 8: the ring/wide
 // decoders' 256-symbol runs; 6: k_decode_fixed's kIdx = 64)
+// sub_abs[g] = (a boundary at or before symbol 64 g) | (codes from it to the
+// symbol) << 48, without walking: the decoder skips the codes (k_mark_lite)
+hipError_t launch_indexless_mark_lite(const IndexlessArgs& a, const uint64_t* off, uint64_t* sub_abs, hipStream_t st);
+constexpr uint64_t kSkipPosMask = (1ull << 48) - 1;
 hipError_t launch_indexless_mark(const IndexlessArgs& a, const uint64_t* off, uint64_t* sub_abs, uint32_t shift,
                                  hipStream_t s);
 bool indexless_staged(const IndexlessArgs& a);  // k_spec/k_mark LDS variants apply

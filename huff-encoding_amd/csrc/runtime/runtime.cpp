@@ -1013,9 +1013,11 @@ Status decode_indexless_dev(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_
     const DecTables* dt = nullptr;
     HUFF_TRY(ctx->upload_dec_tables(t, &dt));
     // the window end (d_end): `count` codes walked from a known boundary
-    auto walk_end = [&](const uint64_t* start, uint64_t start_v, const uint64_t* count, uint64_t count_v) -> Status {
+    auto walk_end = [&](const uint64_t* start, uint64_t start_v, const uint64_t* count, uint64_t count_v,
+                        bool packed = false) -> Status {
         if (!d_end) return Status::ok();
         dev::WalkEndArgs w{};
+        w.start_packed = packed ? 1u : 0u;
         w.comp = d_comp;
         w.comp_bytes = comp_bytes;
         w.lut = static_cast<const uint32_t*>(ctx->d_lut.p);
@@ -1081,10 +1083,20 @@ Status decode_indexless_dev(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_
         const bool bounce = reinterpret_cast<uintptr_t>(out_at()) & 15;
         if (bounce) HUFF_TRY(ctx->d_align.ensure(total + 64));
         // a restart point every 64 symbols, then the fixed-count decoder
+        // (k_mark_lite: a boundary and the codes to skip from it, the
+        // decoder's lanes walk those codes themselves; the self-check builds,
+        // HUFF_DEC_VARIANT 11-13, need exact lane starts: k_mark_lds walks)
         DevBuf& sub_abs = ctx->idx_sub_abs;
-        HUFF_TRY(indexless_mark(ctx, st, sub_abs, 6));
+        const uint32_t check = decode_check_mode();
+        if (check) {
+            HUFF_TRY(indexless_mark(ctx, st, sub_abs, 6));
+        } else {
+            HUFF_TRY(sub_abs.ensure(((total + 63) >> 6) * 8 + 8));
+            HIP_TRY(dev::launch_indexless_mark_lite(st.a, static_cast<const uint64_t*>(st.off.p),
+                                                    static_cast<uint64_t*>(sub_abs.p), strm));
+        }
         const uint64_t m = ((total - 1) >> 6) << 6;  // the last mark: symbol m
-        HUFF_TRY(walk_end(static_cast<const uint64_t*>(sub_abs.p) + (m >> 6), 0, nullptr, total - m));
+        HUFF_TRY(walk_end(static_cast<const uint64_t*>(sub_abs.p) + (m >> 6), 0, nullptr, total - m, !check));
         dev::DecodeArgs d{};
         d.comp = d_comp;
         d.comp_bytes = comp_bytes;
@@ -1092,6 +1104,7 @@ Status decode_indexless_dev(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_
         d.lut_bits = dt->bits;
         d.lut_words = static_cast<uint32_t>(dt->lut.size());
         d.sub_abs64 = static_cast<const uint64_t*>(sub_abs.p);
+        d.skip_packed = check ? 0u : 1u;
         d.end_bit = valid_bits;
         d.nchunks = static_cast<uint32_t>((total + dev::kChunk - 1) / dev::kChunk);
         d.max_len = dt->maxdepth;
@@ -1101,7 +1114,7 @@ Status decode_indexless_dev(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_
         d.pad_stage = dev::fixed_decode_pad(valid_bits, total);
         d.n = total;
         d.out = bounce ? static_cast<uint8_t*>(ctx->d_align.p) : out_at();
-        d.check_mode = decode_check_mode();
+        d.check_mode = check;
         HUFF_TRY(run_checked_decode(ctx, d, [&] { return dev::launch_decode_fixed(d, strm); }));
         HIP_TRY(hipEventRecord(ctx->lut_free, strm));
         if (bounce) HIP_TRY(hipMemcpyAsync(out_at(), ctx->d_align.p, total, hipMemcpyDeviceToDevice, strm));
