@@ -154,6 +154,25 @@ __global__ __launch_bounds__(kThreads) void k_fix(Seg g, uint64_t* __restrict__ 
         if (i) fix_one(g, s, x, c, tm, dl, flags, r, i, plut);
 }
 
+// round 0 after the staged speculative pass: only the segments that can
+// differ from their predecessor's exit — every workgroup's first segment and
+// the listed successors of in-workgroup new exits (each index once, so no two
+// lanes update one segment's merge record)
+__global__ __launch_bounds__(kThreads) void k_fix_list(Seg g, uint64_t* __restrict__ s, uint64_t* __restrict__ x,
+                                                       uint64_t* __restrict__ c, uint32_t* __restrict__ tm,
+                                                       int32_t* __restrict__ dl, unsigned int* __restrict__ flags,
+                                                       const uint32_t* __restrict__ list) {
+    extern __shared__ uint32_t plut[];
+    load_prim(plut, g);
+    const uint64_t firsts = (g.nseg - 1) / kThreads;  // segments 256, 512, ...
+    const uint64_t n = firsts + __builtin_nontemporal_load(flags + kFixRounds);
+    for (uint64_t j = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; j < n;
+         j += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
+        const uint64_t i = j < firsts ? (j + 1) * kThreads : list[j - firsts];
+        fix_one(g, s, x, c, tm, dl, flags, 0, i, plut);
+    }
+}
+
 // sequential fallback: settle every segment in order (one lane), only when
 // the last fix-up round still changed an exit
 __global__ void k_settle(Seg g, uint64_t* __restrict__ s, uint64_t* __restrict__ x, uint64_t* __restrict__ c,
@@ -520,6 +539,11 @@ __global__ __launch_bounds__(kThreads) void k_spec_lds(IndexlessArgs a) {
             }
         }
         s_out = ns;
+        // a new exit: the successor started from the old one (a workgroup's
+        // first segment is checked anyway)
+        if (live && tm_out == kNoMerge && cur != ex_l[threadIdx.x] && i + 1 < a.nseg &&
+            ((i + 1) % kThreads) != 0 && a.fixlist)
+            a.fixlist[atomicAdd(a.flags + kFixRounds, 1u)] = static_cast<uint32_t>(i + 1);
     }
     if (!live) return;
     a.s[i] = s_out;
@@ -691,7 +715,14 @@ hipError_t launch_indexless_settle_all(const IndexlessArgs& a, hipStream_t st) {
     const size_t lds = (1u << a.lut_bits) * 4;
     // grid-stride rounds: a few resident workgroups per CU cover the segments
     const uint32_t grid = static_cast<uint32_t>(std::min<uint64_t>((a.nseg + kThreads - 1) / kThreads, 2048));
-    for (int r = 0; r < kFixRounds; ++r)
+    int r0 = 0;
+    if (a.fixlist && use_staged(a)) {  // the staged pass listed what round 0 must look at
+        const uint32_t lgrid = static_cast<uint32_t>(std::min<uint64_t>(((a.nseg / kThreads) + kThreads) / kThreads, 256));
+        hipLaunchKernelGGL(k_fix_list, dim3(std::max<uint32_t>(lgrid, 1)), dim3(kThreads), lds, st, g, a.s, a.x, a.c,
+                           a.tm, a.dl, a.flags, a.fixlist);
+        r0 = 1;
+    }
+    for (int r = r0; r < kFixRounds; ++r)
         hipLaunchKernelGGL(k_fix, dim3(grid), dim3(kThreads), lds, st, g, a.s, a.x, a.c, a.tm, a.dl, a.flags, r);
     hipLaunchKernelGGL(k_settle, dim3(1), dim3(64), lds, st, g, a.s, a.x, a.c, a.tm, a.flags);
     return hipGetLastError();

@@ -136,7 +136,11 @@ struct IndexlessArgs {
     // (tm = kNoMerge: never within the segment)
     uint32_t* tm;
     int32_t* dl;
-    unsigned int* flags;          // [kFixRounds]: round r found a changed exit
+    unsigned int* flags;          // [kFixRounds + 1]: round r found a changed exit; [kFixRounds]: fixlist count
+    // (LDS-staged path) segments whose start may not be their predecessor's
+    // exit after the speculative pass, besides every workgroup's first one:
+    // the successors of segments the in-workgroup fix-up gave a new exit
+    uint32_t* fixlist;
     const uint16_t* stab;         // single-symbol table (k_decode_fixed's): the LDS-staged kernels
     uint32_t stab_bits;
     // multi-code walk table over the same stab_bits-bit windows: bits [0, 4)

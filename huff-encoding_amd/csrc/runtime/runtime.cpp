@@ -941,7 +941,7 @@ Status indexless_sync(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_bytes,
     HUFF_TRY(st.off.ensure((nseg + 1) * 8));
     HUFF_TRY(st.tm.ensure(nseg * 4));
     HUFF_TRY(st.dl.ensure(nseg * 4));
-    HUFF_TRY(st.flag.ensure(dev::kFixRounds * 4));
+    HUFF_TRY(st.flag.ensure((dev::kFixRounds + 1) * 4));
     dev::IndexlessArgs& a = st.a;
     a = dev::IndexlessArgs{};
     a.comp = d_comp;
@@ -968,11 +968,13 @@ Status indexless_sync(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_bytes,
         a.nsamp = std::min<uint32_t>(dev::kSampMax, static_cast<uint32_t>((S - 1) / dev::kSampBits));
         HUFF_TRY(st.samp.ensure(nseg * a.nsamp * 4 + 4));
         a.samp = static_cast<uint32_t*>(st.samp.p);
+        HUFF_TRY(st.fixlist.ensure(nseg * 4 + 4));
+        a.fixlist = static_cast<uint32_t*>(st.fixlist.p);
     } else {  // k_spec leaves the merge record to the fix-up rounds
         HIP_TRY(hipMemsetAsync(st.tm.p, 0, nseg * 4, strm));
         HIP_TRY(hipMemsetAsync(st.dl.p, 0, nseg * 4, strm));
     }
-    HIP_TRY(hipMemsetAsync(st.flag.p, 0, dev::kFixRounds * 4, strm));
+    HIP_TRY(hipMemsetAsync(st.flag.p, 0, (dev::kFixRounds + 1) * 4, strm));
     HIP_TRY(dev::launch_indexless_spec(a, strm));
     // fix-up rounds and the sequential fallback decide on the device whether
     // they have work (no host wait between rounds)
