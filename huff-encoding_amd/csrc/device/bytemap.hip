@@ -90,6 +90,26 @@ __global__ __launch_bounds__(256) void k_arith_index(uint64_t n, uint32_t nchunk
 
 }  // namespace
 
+// sub_bit[g] = task_base[g / 64] + sub16[g] - chunk_start[g / 1024]
+__global__ __launch_bounds__(256) void k_index_expand(uint64_t nsub, const uint64_t* __restrict__ task_base,
+                                                      const uint16_t* __restrict__ sub16,
+                                                      const uint64_t* __restrict__ chunk_start,
+                                                      uint32_t* __restrict__ sub_bit) {
+    const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+    for (uint64_t g = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; g < nsub; g += stride)
+        sub_bit[g] = static_cast<uint32_t>(task_base[g * kIdx / kTaskSym] + sub16[g] - chunk_start[g * kIdx / kChunk]);
+}
+
+hipError_t launch_index_expand(uint64_t n, const uint64_t* task_base, const uint16_t* sub16,
+                               const uint64_t* chunk_start, uint32_t* sub_bit, hipStream_t s) {
+    const uint64_t nsub = (n + kIdx - 1) / kIdx;
+    if (nsub == 0) return hipSuccess;
+    const uint64_t want = (nsub + 255) / 256;
+    hipLaunchKernelGGL(k_index_expand, dim3(static_cast<uint32_t>(want < 4096 ? want : 4096)), dim3(256), 0, s, nsub,
+                       task_base, sub16, chunk_start, sub_bit);
+    return hipGetLastError();
+}
+
 hipError_t launch_arith_index(uint64_t n, uint32_t nchunks, uint64_t base_bits, uint64_t* chunk_start,
                               uint32_t* sub_bit, hipStream_t s) {
     hipLaunchKernelGGL(k_arith_index, dim3(1024), dim3(256), 0, s, n, nchunks, base_bits, chunk_start, sub_bit);

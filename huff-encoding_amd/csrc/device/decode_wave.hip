@@ -33,7 +33,7 @@ namespace {
 constexpr int kThreads = 256;
 constexpr int kWaves = kThreads / 64;
 constexpr uint32_t kLaneSym = kIdx;              // symbols per lane per task
-constexpr uint32_t kTaskSym = 64 * kLaneSym;     // 4,096 symbols per wave task
+static_assert(kTaskSym == 64 * kLaneSym, "4,096 symbols per wave task");
 constexpr uint32_t kOutWords = kLaneSym / 4 + 2; // output dwords per lane (64 letters + overshoot)
 constexpr uint32_t kInCap = 4608;                // input stage bytes per wave (9 bits per symbol)
 // k_decode_fixed's per-wave stage: the task's input, then (after the decode)
@@ -74,6 +74,8 @@ __device__ __forceinline__ Task task_info(const DecodeArgs& a, uint64_t t, uint3
             k.skip = static_cast<uint32_t>(k.lane_bit >> 48);
             k.lane_bit &= kSkipPosMask;
         }
+    } else if (a.sub16) {  // compact index: task base + u16 offset
+        k.lane_bit = k.cnt ? a.task_base[t] + a.sub16[k.sym0 / kIdx + lane] : 0;
     } else {
         const uint32_t c = static_cast<uint32_t>(k.sym0 / kChunk);
         k.lane_bit = k.cnt ? a.chunk_start[c] + a.sub_bit[k.sym0 / kIdx + lane] : 0;
@@ -89,7 +91,7 @@ __device__ __forceinline__ Task task_info(const DecodeArgs& a, uint64_t t, uint3
         if constexpr (SKIP)  // the next task's first bit lies within its skipped codes
             if (next < a.n) end = (end & kSkipPosMask) + (end >> 48) * a.max_len;
     } else if (next < a.n) {
-        end = a.chunk_start[next / kChunk] + a.sub_bit[next / kIdx];
+        end = a.sub16 ? a.task_base[t + 1] : a.chunk_start[next / kChunk] + a.sub_bit[next / kIdx];
     } else {
         end = a.chunk_start[a.nchunks];
     }

@@ -60,6 +60,11 @@ struct PackArgs {
     uint32_t nchunks;
     uint8_t* out;
     uint32_t* sub_bit;            // may be null
+    // compact restart index (codes <= 16 bits; instead of sub_bit): the first
+    // bit of every kTaskSym-symbol task (u64) and every 64th symbol's offset
+    // from its task's first bit (u16: 4,096 codes of <= 16 bits fit)
+    uint16_t* sub16;
+    uint64_t* task_base;
     uint32_t prev_tail_len;
     uint32_t stage_words;         // per wave
     uint32_t grid;                // persistent workgroups (4 waves each)
@@ -91,6 +96,10 @@ struct DecodeArgs {
     // kIdx-th symbol (instead of chunk_start + sub_bit) and the stream's end
     const uint64_t* sub_abs64;
     uint64_t end_bit;
+    // the compact restart index (PackArgs::sub16 / task_base), instead of
+    // chunk_start + sub_bit (k_decode_fixed, k_decode_wave)
+    const uint16_t* sub16;
+    const uint64_t* task_base;
     // sub_abs64 entries as k_mark_lite writes them: a boundary at or before
     // the symbol in bits [0, 48) and the codes to skip from it in [48, 64)
     uint32_t skip_packed;
@@ -170,6 +179,10 @@ struct BytemapArgs {
 // sub_bit[g] = 8 (g kIdx mod kChunk)
 hipError_t launch_arith_index(uint64_t n, uint32_t nchunks, uint64_t base_bits, uint64_t* chunk_start,
                               uint32_t* sub_bit, hipStream_t s);
+constexpr uint32_t kTaskSym = 4096;  // symbols per decode task (k_decode_fixed) = per compact index base
+// sub_bit[g] from the compact index (for the decoders that read sub_bit)
+hipError_t launch_index_expand(uint64_t n, const uint64_t* task_base, const uint16_t* sub16,
+                               const uint64_t* chunk_start, uint32_t* sub_bit, hipStream_t s);
 
 // wider letters (wide.hip): W-byte keys, hash-table code lookup
 struct WideArgs {

@@ -275,7 +275,8 @@ __global__ __launch_bounds__(pack_waves<LONG>() * 64) void k_pack(PackArgs a) {
         }
         wave_sync();
 
-        uint64_t round_bit = cs;
+        uint64_t round_bit = cs, task_bit0 = cs;
+        static_assert(kTaskSym == 4 * kPackWaveRound, "a decode task is 4 pack rounds");
         for (uint32_t r = 0; r < nrounds; ++r) {
             const LaneIn v = v0;
             v0 = v1;
@@ -316,8 +317,16 @@ __global__ __launch_bounds__(pack_waves<LONG>() * 64) void k_pack(PackArgs a) {
             const uint32_t tot = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(incl), 63));
             const uint32_t excl = incl - bits;
 
-            if (a.sub_bit && nvalid > 0 && (s_in_chunk & (kIdx - 1)) == 0)
+            if (a.sub16) {  // compact index: a u64 base per task of 4 rounds, u16 offsets
+                if ((r & 3u) == 0) {
+                    task_bit0 = round_bit;
+                    if (lane == 0) a.task_base[(sym0 + r * kPackWaveRound) / kTaskSym] = round_bit;
+                }
+                if (nvalid > 0 && (s_in_chunk & (kIdx - 1)) == 0)
+                    a.sub16[(sym0 + s_in_chunk) / kIdx] = static_cast<uint16_t>(round_bit - task_bit0 + excl);
+            } else if (a.sub_bit && nvalid > 0 && (s_in_chunk & (kIdx - 1)) == 0) {
                 a.sub_bit[(sym0 + s_in_chunk) / kIdx] = static_cast<uint32_t>(round_bit - cs + excl);
+            }
 
             if constexpr (LONG) {
                 if (bits) emit_codes<LONG>(stage, round_bit - stage_bit0 + excl, ent);

@@ -489,6 +489,7 @@ huff::Status huff_enc::pack(const huff_tree* t, uint64_t base, const uint8_t* pr
                             uint8_t* d_out, size_t out_cap, uint64_t* total) {
     uint64_t tb = 0;
     HUFF_TRY(bits(t, &tb));
+    compact_index = false;  // set by the general pack below when it writes the compact index
     const uint64_t need = ((base & 7) + tb + 7) / 8;
     if (total) *total = tb;
     if (need > out_cap) return huff::Status::err(HUFF_E_BUFFER_TOO_SMALL, "output buffer too small");
@@ -581,6 +582,15 @@ huff::Status huff_enc::pack(const huff_tree* t, uint64_t base, const uint8_t* pr
     a.nchunks = nchunks;
     a.out = d_out;
     a.sub_bit = static_cast<uint32_t*>(sub_bit.p);
+    // codes <= 16 bits: the compact restart index (4,096 codes fit a u16 offset)
+    const bool compact = !long_codes && et.maxlen <= 16;
+    if (compact) {
+        HUFF_TRY(sub16.ensure(((n + huff::dev::kIdx - 1) / huff::dev::kIdx + 1) * 2));
+        HUFF_TRY(task_base.ensure(((n + huff::dev::kTaskSym - 1) / huff::dev::kTaskSym + 1) * 8));
+        a.sub16 = static_cast<uint16_t*>(sub16.p);
+        a.task_base = static_cast<uint64_t*>(task_base.p);
+        a.sub_bit = nullptr;
+    }
     a.prev_tail_len = static_cast<uint32_t>(prev_tail_len);
     // one wave round: <= kPackWaveRound*maxlen bits + a < 128-bit carry (+ the
     // 128-bit window past the last unit, which the OR emit may touch with zero)
@@ -593,6 +603,7 @@ huff::Status huff_enc::pack(const huff_tree* t, uint64_t base, const uint8_t* pr
     HUFF_TRY(ctx->timed("pack", [&] { return huff::dev::launch_pack(long_codes, a, s); }));
     packed = true;
     index_pending = false;
+    compact_index = compact;
     packed_tree_id = t->id;
     remember_tree(t);
     bit_base = base;
@@ -606,6 +617,18 @@ huff::Status huff_enc::ensure_index() {
     HIP_TRY(huff::dev::launch_arith_index(n, nchunks, bit_base & 7, static_cast<uint64_t*>(chunk_start.p),
                                           static_cast<uint32_t*>(sub_bit.p), ctx->stream));
     index_pending = false;
+    compact_index = false;
+    return huff::Status::ok();
+}
+
+huff::Status huff_enc::expand_index() {
+    if (!compact_index) return huff::Status::ok();
+    HUFF_TRY(ctx->activate());
+    HIP_TRY(huff::dev::launch_index_expand(n, static_cast<const uint64_t*>(task_base.p),
+                                           static_cast<const uint16_t*>(sub16.p),
+                                           static_cast<const uint64_t*>(chunk_start.p),
+                                           static_cast<uint32_t*>(sub_bit.p), ctx->stream));
+    compact_index = false;
     return huff::Status::ok();
 }
 
@@ -677,6 +700,14 @@ huff::Status huff_enc::decode(const huff_tree* t, const uint8_t* d_comp, uint64_
     // and copied on the stream (one extra n-byte copy, against 1.5-2x for the
     // older unaligned-capable decoders)
     uint8_t* dst = d_out;
+    if (compact_index) {  // the task decoders read it as is; the others get sub_bit
+        if (a.variant == huff::dev::kDecodeWave || a.variant == huff::dev::kDecodeFixed) {
+            a.sub16 = static_cast<const uint16_t*>(sub16.p);
+            a.task_base = static_cast<const uint64_t*>(task_base.p);
+        } else {
+            HUFF_TRY(expand_index());
+        }
+    }
     const bool bounce = (a.variant == huff::dev::kDecodeWave || a.variant == huff::dev::kDecodeFixed) &&
                         (reinterpret_cast<uintptr_t>(d_out) & 15);
     if (bounce) {
@@ -703,6 +734,7 @@ huff::Status huff_enc::decode(const huff_tree* t, const uint8_t* d_comp, uint64_
 
 huff::Status huff_enc::download_index(huff_index_host& idx) {
     HUFF_TRY(ensure_index());
+    HUFF_TRY(expand_index());  // the host index (CompressData) keeps chunk_start + sub_bit
     idx.n = n;
     idx.chunk_start.resize(nchunks + 1);
     idx.sub_bit.resize((n + huff::dev::kIdx - 1) / huff::dev::kIdx);
@@ -728,6 +760,7 @@ huff::Status huff_enc::upload_index(const huff_index_host& idx) {
     packed = true;
     packed_any_tree = true;  // the caller vouches for the tree (huff_enc_upload_index)
     index_pending = false;
+    compact_index = false;
     return huff::Status::ok();
 }
 

@@ -166,6 +166,12 @@ struct huff_enc {
     uint32_t nchunks = 0;
     DevBuf chunk_hist, gw, chunk_bits, chunk_start, tsum, sub_bit, mask, pos;
     DevBuf deep_words;  // codes longer than 57 bits (deep.hip)
+    // compact restart index (codes <= 16 bits, pack.hip): u64 per 4,096
+    // symbols + u16 per 64, half the bytes of chunk_start + sub_bit;
+    // expanded into sub_bit for the consumers that read that
+    DevBuf task_base, sub16;
+    bool compact_index = false;
+    huff::Status expand_index();
     uint64_t w[256] = {};
     bool have_hist = false;
     // state of the last pack (for decode)
