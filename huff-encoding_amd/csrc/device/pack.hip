@@ -138,8 +138,20 @@ __device__ __forceinline__ uint32_t join2(uint32_t e0, uint32_t e1) {
     return (e0 & ~31u) | ((e1 & ~31u) >> (e0 & 31u));
 }
 
+// the code lengths of two entries, summed by one SDWA add of their low bytes
+// (codes of <= 24 bits leave bits 5-7 of an entry zero; G >= 2 means <= 16)
+__device__ __forceinline__ uint32_t len2(uint32_t e0, uint32_t e1) {
+    uint32_t r;
+    asm("v_add_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_0 src1_sel:BYTE_0"
+        : "=v"(r)
+        : "v"(e0), "v"(e1));
+    return r;
+}
+
+// Lp[i] = len2(ent[2i], ent[2i+1]) (G >= 2)
 template <int G>
-__device__ __forceinline__ void emit_codes_or(uint32_t* __restrict__ stage, uint32_t p, const uint32_t (&ent)[kBPL]) {
+__device__ __forceinline__ void emit_codes_or(uint32_t* __restrict__ stage, uint32_t p, const uint32_t (&ent)[kBPL],
+                                              const uint32_t (&Lp)[kBPL / 2]) {
     const uint32_t stage_addr = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(
         (__attribute__((address_space(3))) uint32_t*)(stage)));
     uint32_t o = p;
@@ -151,13 +163,13 @@ __device__ __forceinline__ void emit_codes_or(uint32_t* __restrict__ stage, uint
             len = ent[k] & 31u;
         } else if constexpr (G == 2) {
             J = join2(ent[k], ent[k + 1]);
-            len = (ent[k] & 31u) + (ent[k + 1] & 31u);
+            len = Lp[k / 2];
         } else {
             static_assert(G == 4, "groups of 1, 2 or 4 codes");
-            const uint32_t l01 = (ent[k] & 31u) + (ent[k + 1] & 31u);
+            const uint32_t l01 = Lp[k / 2];
             const uint32_t J23 = join2(ent[k + 2], ent[k + 3]);
             J = join2(ent[k], ent[k + 1]) | (J23 >> l01);
-            len = l01 + (ent[k + 2] & 31u) + (ent[k + 3] & 31u);
+            len = l01 + Lp[k / 2 + 1];
         }
         const uint32_t s = o & 31u;
         // the word's LDS address, lshr + lshl_add (opaque: the compiler's
@@ -310,8 +322,17 @@ __global__ __launch_bounds__(pack_waves<LONG>() * 64) void k_pack(PackArgs a) {
 #pragma unroll
                 for (int k = 0; k < static_cast<int>(kBPL); ++k) ent[k] = (k < nvalid) ? lookup(k) : T(0);
             }
+            uint32_t Lp[kBPL / 2];  // pair lengths (SDWA) for the grouped emit
+            if constexpr (!LONG && G >= 2) {
 #pragma unroll
-            for (int k = 0; k < static_cast<int>(kBPL); ++k) bits += static_cast<uint32_t>(ent[k] & E::kMask);
+                for (int k = 0; k < static_cast<int>(kBPL / 2); ++k) {
+                    Lp[k] = len2(static_cast<uint32_t>(ent[2 * k]), static_cast<uint32_t>(ent[2 * k + 1]));
+                    bits += Lp[k];
+                }
+            } else {
+#pragma unroll
+                for (int k = 0; k < static_cast<int>(kBPL); ++k) bits += static_cast<uint32_t>(ent[k] & E::kMask);
+            }
             // wave exclusive scan of the bit counts
             const uint32_t incl = wave_scan_incl(bits);
             const uint32_t tot = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(incl), 63));
@@ -331,7 +352,7 @@ __global__ __launch_bounds__(pack_waves<LONG>() * 64) void k_pack(PackArgs a) {
             if constexpr (LONG) {
                 if (bits) emit_codes<LONG>(stage, round_bit - stage_bit0 + excl, ent);
             } else {
-                emit_codes_or<G>(stage, static_cast<uint32_t>(round_bit - stage_bit0 + excl), ent);
+                emit_codes_or<G>(stage, static_cast<uint32_t>(round_bit - stage_bit0 + excl), ent, Lp);
             }
             wave_order();
 
