@@ -1042,9 +1042,14 @@ Status decode_indexless_dev(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_
     };
     auto out_at = [&]() { return d_user ? d_user : static_cast<uint8_t*>(out.p); };
     if (valid_bits == 0) return Status::ok();
-    if (reinterpret_cast<uintptr_t>(d_comp) & 3)
-        return Status::err(HUFF_E_INVALID_ARG, "compressed stream must be 4-byte aligned");
     HUFF_TRY(ctx->activate());
+    if (reinterpret_cast<uintptr_t>(d_comp) & 15) {
+        // the staged kernels read the stream in 16-B pieces: a stream at any
+        // other alignment (a tensor view) is copied once to an aligned buffer
+        HUFF_TRY(ctx->d_comp_align.ensure(comp_bytes + 64));
+        HIP_TRY(hipMemcpyAsync(ctx->d_comp_align.p, d_comp, comp_bytes, hipMemcpyDeviceToDevice, ctx->stream));
+        d_comp = static_cast<const uint8_t*>(ctx->d_comp_align.p);
+    }
     const DecTables* dt = nullptr;
     HUFF_TRY(ctx->upload_dec_tables(t, &dt));
     // the window end (d_end): `count` codes walked from a known boundary

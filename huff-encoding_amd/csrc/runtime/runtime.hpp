@@ -131,6 +131,7 @@ struct huff_ctx {
     DevBuf d_in, d_out;  // staging of the host-pointer API
     DevBuf d_lut;
     DevBuf d_align;      // aligned decode target for a misaligned output pointer
+    DevBuf d_comp_align; // aligned copy of a misaligned index-free input stream
     DevBuf d_err;        // k_decode_fixed self-check record (check builds)
     // index-free decode workspace, kept across calls (per-call allocations
     // of its ~100 MB per GiB of stream cost more than the kernels)

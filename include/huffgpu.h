@@ -251,7 +251,8 @@ int huff_mgpu_compress(huff_comm* c, huff_enc* e, uint8_t* d_out, size_t out_cap
 
 /* decompress (comp.rs:487-519) of a device-resident stream that has no
  * restart index (e.g. written by the reference CPU path): comp_bytes bytes at
- * d_comp (4-B aligned), the last holding `padding` pad bits (the walk reads
+ * d_comp (any alignment; a stream not 16-B aligned is first copied to an
+ * aligned buffer of the context), the last holding `padding` pad bits (the walk reads
  * 8 - padding bits of it; an incomplete final code is dropped). Self-
  * synchronising parallel decode; writes the letters to d_out and their count
  * to *n_out (set also on HUFF_E_BUFFER_TOO_SMALL; d_out NULL: count only). */

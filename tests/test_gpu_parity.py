@@ -346,6 +346,13 @@ def test_indexfree_misaligned_output(H, O, ctx):
     assert got == n
     assert torch.equal(out[5:5 + n], x[:n])
     assert (out[:5] == 0x5A).all() and (out[5 + n:] == 0x5A).all()
+    # a stream at an odd address (copied to an aligned buffer first)
+    dc2 = torch.zeros(len(comp) + 64, dtype=torch.uint8, device="cuda")
+    dc2[3:3 + len(comp)] = dc[:len(comp)]
+    out.fill_(0)
+    got = D.decompress_dev(ctx, tree, dc2.data_ptr() + 3, len(comp), (8 - bits % 8) % 8, out.data_ptr(), n + 64)
+    torch.cuda.synchronize()
+    assert got == n and torch.equal(out[:n], x[:n])
 
 
 @pytest.mark.parametrize("dec", ["auto", "1", "7", "9", "10"], ids=["dec-auto", "dec-single", "dec-ring", "dec-wave", "dec-fixed"])
