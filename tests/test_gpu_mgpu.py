@@ -1,0 +1,103 @@
+"""The sharded path with several processes on the GPU: world
+2 and 3, one process per rank, every rank on cuda:0 (RCCL needs one device
+per rank, so the one exchange goes over gloo; bench.py --dist-backend gloo
+runs the same rehearsal). Unlike tests/test_mgpu_gloo.py (oracle stand-in
+for the pack), each rank runs the real HIP path: device generator at its
+global offset, pass 1 (huff_enc_hist), mgpu.exchange of the weight rows and
+tail bytes, huff_enc_pack_shards (tree, bit base and shared first byte
+computed natively), decode of its own shard. The concatenation of the ranks'
+owned bytes must equal the oracle's encode of the whole input
+(comp.rs:419-451; the reference's CLI merge is huff/src/comp.rs:161-172).
+Shard sizes are ragged, so the shard boundaries fall inside bytes."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SEED = 0x5EED0077
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, n, kind, q):
+    sys.path[:0] = [os.path.join(ROOT, "huff-encoding_amd"), os.path.join(ROOT, "oracle")]
+    import torch
+    import torch.distributed as dist
+
+    import huff_coding as H
+    from huff_coding import device as D
+    from huff_coding import mgpu
+
+    try:
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+        torch.cuda.set_device(0)
+        ctx = H.Context(0)
+        x = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
+        D.generate(ctx, kind, SEED, x.data_ptr(), n, offset=rank * n,
+                   cdf=D.zipf_cdf(1.2) if kind == "zipf" else None)
+        job = H.EncodeJob(ctx, x.data_ptr(), n)
+        hists, tails = mgpu.exchange(job.hist(), x[n - 8:n].cpu().numpy().tobytes())
+        cap = n + 128
+        out = torch.zeros(cap, dtype=torch.uint8, device="cuda")
+        tree, base, bits = job.pack_shards(hists, rank, tails, out.data_ptr(), cap)
+        torch.cuda.synchronize()
+        nbytes = (base % 8 + bits + 7) // 8
+        mine = mgpu.owned_bytes(out[:nbytes].cpu().numpy(), base, bits, rank == world - 1)
+        dec = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
+        job.decode(tree, out.data_ptr(), dec.data_ptr())
+        torch.cuda.synchronize()
+        ok = bool(torch.equal(dec[:n], x[:n]))
+        got = [None] * world
+        dist.all_gather_object(got, (mine.tobytes(), tree.as_bin(), base, bits, ok))
+        if rank == 0:
+            q.put(("ok", got))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:  # noqa: BLE001
+        q.put(("err", f"rank {rank}: {type(e).__name__}: {e}"))
+        raise
+
+
+@pytest.mark.parametrize("world,kind", [(2, "text"), (3, "zipf")])
+def test_sharded_processes_on_gpu(world, kind, O):
+    import torch.multiprocessing as mp
+
+    n = (1 << 21) + 12345  # ragged: shard boundaries fall inside bytes of the stream
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n, kind, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        status, got = q.get(timeout=240)
+    finally:
+        for p in procs:
+            p.join(60)
+            if p.is_alive():
+                p.kill()
+    assert status == "ok", got
+    assert all(p.exitcode == 0 for p in procs)
+
+    gen = {"text": O.gen_text, "zipf": O.gen_zipf}[kind]
+    full = gen(SEED, world * n)
+    w = O.fast_hist(full, 8)
+    t = O.Tree.from_weights(O.weights_from_array(w))
+    code, ln = t.code_table()
+    want, wbits = O.fast_encode(full, code, ln, threads=8)
+    assert len({g[1] for g in got}) == 1, "ranks built different trees"
+    assert got[0][1] == t.as_bin()
+    assert all(g[4] for g in got), "a rank's own decode differs from its shard"
+    assert [g[2] for g in got] == list(np.cumsum([0] + [g[3] for g in got[:-1]]))
+    assert got[-1][2] + got[-1][3] == wbits
+    stream = b"".join(g[0] for g in got)
+    assert stream == want.tobytes()
