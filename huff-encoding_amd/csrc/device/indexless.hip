@@ -372,15 +372,15 @@ struct Cursor {
         for (int k = 0; k < kChunkSteps; ++k) {
             if ((k & 1) == 0) refill();
             const uint32_t e = wtab[static_cast<uint32_t>(buf >> 32) >> (32 - K)];
-            if (SLOW && (e & kWtSlow)) {
+            if (SLOW && (e & kSsSlow)) {
                 U += step<SLOW>(stab, K, glut, Kg);
                 N += 1;
             } else {
-                const uint32_t u = e & 15u;
+                const uint32_t u = (e >> 8) & 15u;
                 buf <<= u;
                 X -= u;
                 U += u;
-                N += (e >> 4) & 15u;
+                N += e >> 12;
             }
         }
     }
@@ -391,14 +391,13 @@ __device__ __forceinline__ uint32_t stab_words(const IndexlessArgs& a) {
     return ((((1u << a.stab_bits) + 1) / 2) + 3) & ~3u;
 }
 __device__ __forceinline__ uint32_t tables_words(const IndexlessArgs& a) {
-    return stab_words(a) * (a.wtab ? 2u : 1u);
+    return stab_words(a);
 }
 __device__ __forceinline__ const uint16_t* load_stab(const IndexlessArgs& a, uint32_t* lds) {
+    // the walk table when there is one (its low bits are stab's lengths), else stab
     const uint32_t words = ((1u << a.stab_bits) + 1) / 2;
-    for (uint32_t i = threadIdx.x; i < words; i += blockDim.x) lds[i] = reinterpret_cast<const uint32_t*>(a.stab)[i];
-    if (a.wtab)
-        for (uint32_t i = threadIdx.x; i < words; i += blockDim.x)
-            lds[stab_words(a) + i] = reinterpret_cast<const uint32_t*>(a.wtab)[i];
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(a.wtab ? a.wtab : a.stab);
+    for (uint32_t i = threadIdx.x; i < words; i += blockDim.x) lds[i] = src[i];
     return reinterpret_cast<const uint16_t*>(lds);
 }
 
@@ -406,7 +405,7 @@ template <bool SLOW>
 __global__ __launch_bounds__(kThreads) void k_spec_lds(IndexlessArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const uint16_t* stab = load_stab(a, lds);
-    const uint16_t* wtab = a.wtab ? stab + 2 * stab_words(a) : nullptr;
+    const uint16_t* wtab = a.wtab ? stab : nullptr;  // one table serves single and multi-code steps
     const Staged st = stage_block(a, lds + tables_words(a));
     __syncthreads();
     const uint64_t i0 = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
@@ -671,7 +670,7 @@ hipError_t launch_indexless_mark_lite(const IndexlessArgs& a, const uint64_t* of
 }
 
 static size_t lds_staged_bytes(const IndexlessArgs& a) {
-    return static_cast<size_t>(((((1u << a.stab_bits) + 1) / 2) + 3) & ~3u) * 4 * (a.wtab ? 2 : 1) +
+    return static_cast<size_t>(((((1u << a.stab_bits) + 1) / 2) + 3) & ~3u) * 4 +
            ((kThreads * a.seg_bits + 7) / 8 + 128 + 15) / 16 * 16;
 }
 

@@ -152,12 +152,13 @@ struct IndexlessArgs {
     uint32_t* fixlist;
     const uint16_t* stab;         // single-symbol table (k_decode_fixed's): the LDS-staged kernels
     uint32_t stab_bits;
-    // multi-code walk table over the same stab_bits-bit windows: bits [0, 4)
-    // = bits of the window's complete codes, [4, 8) = their count; kWtSlow:
-    // the first code is longer than the window (null: single steps only)
+    // walk table over the same stab_bits-bit windows, for the speculative
+    // pass (which needs lengths, not letters; it replaces stab there): bits
+    // [0, 6) = the first code's length and kSsSlow as in stab, [8, 12) = the
+    // bits of all the window's complete codes, [12, 16) = their count
+    // (null: single steps from stab only)
     const uint16_t* wtab;
 };
-constexpr uint32_t kWtSlow = 0x8000u;
 constexpr uint32_t kSampBits = 128;
 constexpr uint32_t kSampMax = 8;  // samples kept per segment (nsamp <= kSampMax)
 constexpr uint32_t kNoMerge = 0xFFFFFFFFu;

@@ -157,17 +157,18 @@ static void build_walk_table(const HuffTree& t, uint32_t sbits, DecTables& out) 
     uint16_t* w = reinterpret_cast<uint16_t*>(out.lut.data() + out.woff);
     const bool root_leaf = t.root_is_leaf();
     for (uint32_t i = 0; i < n; ++i) {
-        uint32_t used = 0, count = 0;
+        uint32_t used = 0, count = 0, first = 0;
         int32_t x = t.root();
         for (uint32_t p = 0; p < sbits; ++p) {
             if (!root_leaf) x = ((i >> (sbits - 1 - p)) & 1u) ? nodes[x].right : nodes[x].left;
             if (nodes[x].is_leaf) {
+                if (!count) first = p + 1;
                 ++count;
                 used = p + 1;
                 x = t.root();
             }
         }
-        w[i] = count ? static_cast<uint16_t>(used | (count << 4)) : static_cast<uint16_t>(dev::kWtSlow);
+        w[i] = count ? static_cast<uint16_t>(first | (used << 8) | (count << 12)) : static_cast<uint16_t>(dev::kSsSlow);
     }
 }
 
@@ -954,9 +955,12 @@ Status indexless_sync(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_bytes,
     uint32_t g = 0;
     for (const LeafCode& lc : t->t.leaves()) g = std::gcd(g, lc.len);
     if (g == 0) g = 1;
-    // codes <= 32 bits take the LDS-staged kernels: 1024-bit segments keep a
-    // workgroup's staging at 32 KiB (3 workgroups per CU); longer codes 2048
-    const uint64_t seg_target = dt->maxdepth <= 32 ? 1024 : 2048;
+    // codes <= 32 bits take the LDS-staged kernels, longer codes 2048-bit segments
+    // (~992 bits: with the one 8 KiB walk table a workgroup's LDS stays under
+    // 40 KiB, 4 workgroups per CU; 1024-bit segments measured ~1.5 % slower)
+    uint64_t seg_target = dt->maxdepth <= 32 ? 992 : 2048;
+    if (const char* e = std::getenv("HUFF_IDX_SEG"))  // experiment: segment bits
+        if (std::atoi(e) >= 256) seg_target = static_cast<uint64_t>(std::atoi(e));
     uint64_t S = static_cast<uint64_t>(g) * ((seg_target + g - 1) / g);
     // the LDS-staged kernels read lane i's bits from dword ~S/32 * i: with an
     // even dword stride every lane starts on the same few banks (1024 bits: all

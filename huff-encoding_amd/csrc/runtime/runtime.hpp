@@ -52,7 +52,7 @@ struct DecTables {
     // kSsSlow for windows whose first code is longer than sbits
     uint32_t sbits = 0, soff = 0;
     // multi-code walk table (indexless.hip's speculative pass): [1 << sbits]
-    // u16 entries at word `woff`, dev::kWtSlow / used | count << 4
+    // u16 entries at word `woff`: first length | kSsSlow | used << 8 | count << 12
     uint32_t woff = 0;
 };
 
