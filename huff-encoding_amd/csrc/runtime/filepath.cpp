@@ -25,6 +25,9 @@
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <condition_variable>
+#include <deque>
+#include <mutex>
 #include <string>
 #include <thread>
 
@@ -128,6 +131,84 @@ Status write_all(File& f, const void* src, size_t n, const char* path) {
     return Status::ok();
 }
 
+// One writer thread per call: writes run in submission order (a block's
+// first byte may overwrite the previous block's last one) while the calling
+// thread reads, uploads and waits on the GPU — on this path the page-cache
+// writes are the largest host cost. Large writes point at pinned buffers the
+// caller keeps until their ticket completes; small ones are copied.
+class AsyncWriter {
+public:
+    AsyncWriter(int fd, const char* path) : fd_(fd), path_(path), th_([this] { run(); }) {}
+    ~AsyncWriter() {
+        {
+            std::lock_guard<std::mutex> g(m_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        th_.join();
+    }
+    // a ticket: wait(ticket) returns once this write is on the file
+    uint64_t submit(const void* p, size_t n, uint64_t off) {
+        Job j{static_cast<const uint8_t*>(p), n, off, {}};
+        if (n <= 4096) {  // small: copied (headers, pad bytes)
+            j.copy.assign(j.p, j.p + n);
+            j.p = j.copy.data();
+        }
+        std::lock_guard<std::mutex> g(m_);
+        q_.push_back(std::move(j));
+        ++submitted_;
+        cv_.notify_all();
+        return submitted_;
+    }
+    Status wait(uint64_t ticket) {
+        Tick t(io_clock.write);
+        std::unique_lock<std::mutex> g(m_);
+        done_cv_.wait(g, [&] { return completed_ >= ticket || failed_; });
+        if (failed_) return io_err("failed to write", path_);
+        return Status::ok();
+    }
+    Status drain() { return wait(submitted_snapshot()); }
+
+private:
+    struct Job {
+        const uint8_t* p;
+        size_t n;
+        uint64_t off;
+        std::vector<uint8_t> copy;
+    };
+    uint64_t submitted_snapshot() {
+        std::lock_guard<std::mutex> g(m_);
+        return submitted_;
+    }
+    void run() {
+        for (;;) {
+            Job j;
+            {
+                std::unique_lock<std::mutex> g(m_);
+                cv_.wait(g, [&] { return stop_ || !q_.empty(); });
+                if (q_.empty()) return;  // stop requested and nothing left
+                j = std::move(q_.front());
+                q_.pop_front();
+            }
+            const bool ok = failed_ || !j.n || pio_one(true, fd_, const_cast<uint8_t*>(j.p), j.n, j.off);
+            {
+                std::lock_guard<std::mutex> g(m_);
+                if (!ok) failed_ = true;
+                ++completed_;
+            }
+            done_cv_.notify_all();
+        }
+    }
+    int fd_;
+    const char* path_;
+    std::mutex m_;
+    std::condition_variable cv_, done_cv_;
+    std::deque<Job> q_;
+    uint64_t submitted_ = 0, completed_ = 0;
+    bool stop_ = false, failed_ = false;
+    std::thread th_;  // last: started once the members above exist
+};
+
 // The file moves through pieces of at most kPiece bytes (a block longer than
 // that is split; a piece never spans two blocks). One piece's buffers: pinned
 // host bytes (the fread target and H2D source), the piece on the device,
@@ -175,7 +256,8 @@ struct FileWs {
     hipStream_t up = nullptr;  // uploads
     // decompress: payload windows (pinned), the window on the device (and
     // realigned), the symbols on the device and in pinned memory
-    PinnedBuf win[2], sym[2];
+    PinnedBuf win[2], sym[3];
+    PinnedBuf rres[3];  // compress pass 2: piece results, written out asynchronously
     DevBuf d_win, d_shift, d_sym, d_end;
     PinnedBuf end;
     ~FileWs() {
@@ -214,11 +296,12 @@ Status load_piece(huff_ctx* ctx, hipStream_t up, Slot& sl, File& f, size_t n, co
 
 // the piece's results, once its kernels are done, back to pinned memory on
 // the copy stream
-Status fetch_results(huff_ctx* ctx, Slot& sl, size_t bytes) {
-    HUFF_TRY(sl.res.ensure(bytes + 16));
+Status fetch_results(huff_ctx* ctx, Slot& sl, size_t bytes, PinnedBuf* to = nullptr) {
+    PinnedBuf& res = to ? *to : sl.res;
+    HUFF_TRY(res.ensure(bytes + 16));
     HIP_TRY_RT(hipEventRecord(sl.kern, ctx->stream));
     HIP_TRY_RT(hipStreamWaitEvent(ctx->copy_stream, sl.kern, 0));
-    if (bytes) HIP_TRY_RT(hipMemcpyAsync(sl.res.p, sl.dres.p, bytes, hipMemcpyDeviceToHost, ctx->copy_stream));
+    if (bytes) HIP_TRY_RT(hipMemcpyAsync(res.p, sl.dres.p, bytes, hipMemcpyDeviceToHost, ctx->copy_stream));
     HIP_TRY_RT(hipEventRecord(sl.done, ctx->copy_stream));
     return Status::ok();
 }
@@ -381,11 +464,13 @@ static Status file_compress_impl(huff_ctx* ctx, const char* src, const char* dst
         p.off = p.first ? qs[p.block] : pieces[i - 1].off + pieces[i - 1].bits;
         for (int b = 0; b < 256; ++b) p.bits += p.counts[b] * et.len[b];
     }
+    AsyncWriter writer(out.fd, dst);
+    uint64_t ticket[3] = {0, 0, 0};  // the write of the piece whose results sit in rres[i % 3]
     auto emit = [&](size_t i) -> Status {  // piece i's bytes, once copied back
         Slot& sl = slots[i % 2];
         const Piece& p = pieces[i];
         HUFF_TRY(sync_event(sl.done));
-        uint8_t* r = static_cast<uint8_t*>(sl.res.p);
+        uint8_t* r = static_cast<uint8_t*>(ws->rres[i % 3].p);
         const uint64_t packed = ((p.off & 7) + p.bits + 7) / 8;
         const uint64_t q = qs[p.block];
         if (p.first && q != 0) {
@@ -393,15 +478,21 @@ static Status file_compress_impl(huff_ctx* ctx, const char* src, const char* dst
             r[0] |= prev_byte;
         }
         const uint64_t whole = p.last ? packed : ((p.off & 7) + p.bits) / 8;
-        HUFF_TRY(write_all(out, r, whole, dst));
+        if (p.last) {  // read before the buffer is handed to the writer
+            const uint64_t L = (nbits[p.block] + 7) / 8;
+            const uint64_t size = q ? L + 1 : L, written = (q + nbits[p.block] + 7) / 8;
+            if (size) prev_byte = size > written ? 0 : r[packed - 1];
+        }
+        ticket[i % 3] = writer.submit(r, whole, out.pos);
+        out.pos += whole;
         if (p.last) {
             // offset_bytes re-emits all 8L bits of the block (its zero
             // padding too): the block is L bytes, L + 1 when q != 0
             const uint64_t L = (nbits[p.block] + 7) / 8;
             const uint64_t size = q ? L + 1 : L, written = (q + nbits[p.block] + 7) / 8;
             static const uint8_t zeros[2] = {};  // size - written <= 1
-            HUFF_TRY(write_all(out, zeros, size - written, dst));
-            if (size) prev_byte = size > written ? 0 : r[packed - 1];
+            if (size > written) writer.submit(zeros, size - written, out.pos);
+            out.pos += size - written;
         }
         return Status::ok();
     };
@@ -418,13 +509,13 @@ static Status file_compress_impl(huff_ctx* ctx, const char* src, const char* dst
         uint64_t bits = 0;
         HUFF_TRY(sl.job.pack(tree.get(), p.off, prev ? prev->tail : nullptr, prev ? prev->tail_len : 0,
                              static_cast<uint8_t*>(sl.dres.p), packed, &bits));
-        HUFF_TRY(fetch_results(ctx, sl, packed));
+        if (ticket[i % 3]) HUFF_TRY(writer.wait(ticket[i % 3]));  // piece i - 3's bytes are out
+        HUFF_TRY(fetch_results(ctx, sl, packed, &ws->rres[i % 3]));
     }
     for (size_t i = np >= 2 ? np - 2 : 0; i < np; ++i) HUFF_TRY(emit(i));
-    out.pos = 0;
     const uint8_t pb = static_cast<uint8_t>((tree_pad << 4) + prev_padding);
-    HUFF_TRY(write_all(out, &pb, 1, dst));
-    return Status::ok();
+    writer.submit(&pb, 1, 0);
+    return writer.drain();
 }
 
 // decompress in windows of the payload (at most kWindow compressed bytes at a
@@ -493,13 +584,11 @@ static Status file_decompress_impl(huff_ctx* ctx, const char* src, const char* d
         in.pos = 5 + tree_len + off;
         return read_exact(in, static_cast<uint8_t*>(ws->win[i].p), len[i], src);
     };
-    auto write_syms = [&](int i, uint64_t n) -> Status {
-        return write_all(out, ws->sym[i].p, n, dst);
-    };
+    AsyncWriter writer(out.fd, dst);
+    uint64_t ticket[3] = {0, 0, 0};  // the write of the window whose letters sit in sym[k % 3]
     HUFF_TRY(read_at(0, 0));
     uint64_t pos = 0;  // payload bit of the next code
     int cur = 0, k = 0;
-    uint64_t pending = 0;  // symbols of the previous window, not yet written (in sym[(k - 1) & 1])
     while (pos < valid_bits) {
         const size_t b0 = static_cast<size_t>(pos / 8);
         const uint32_t r = static_cast<uint32_t>(pos % 8);
@@ -517,12 +606,12 @@ static Status file_decompress_impl(huff_ctx* ctx, const char* src, const char* d
         uint64_t n = 0;
         HUFF_TRY(decode_indexless_dev(ctx, dwin, nb, wbits, tree.get(), ws->d_sym, &n, nullptr, 0,
                                       static_cast<unsigned long long*>(ws->d_end.p)));
-        const int so = k & 1;
+        const int so = k % 3;
+        if (ticket[so]) HUFF_TRY(writer.wait(ticket[so]));  // window k - 3's letters are out
         HUFF_TRY(ws->sym[so].ensure(n + 16));
         if (n) HIP_TRY_RT(hipMemcpyAsync(ws->sym[so].p, ws->d_sym.p, n, hipMemcpyDeviceToHost, ctx->stream));
         HIP_TRY_RT(hipMemcpyAsync(ws->end.p, ws->d_end.p, 8, hipMemcpyDeviceToHost, ctx->stream));
-        // beside the GPU: the previous window's symbols out, the next window's bytes in
-        HUFF_TRY(write_syms(so ^ 1, pending));
+        // beside the GPU (and the writer): the next window's bytes in
         const int nxt = cur ^ 1;
         if (!last) {
             const size_t ahead = base[cur] + len[cur] - kCarry;
@@ -532,7 +621,8 @@ static Status file_decompress_impl(huff_ctx* ctx, const char* src, const char* d
             Tick t(io_clock.wait);
             HUFF_TRY(ctx->sync());
         }
-        pending = n;
+        ticket[so] = writer.submit(ws->sym[so].p, n, out.pos);
+        out.pos += n;
         ++k;
         if (last) break;
         const uint64_t wend = *static_cast<const uint64_t*>(ws->end.p);
@@ -540,7 +630,7 @@ static Status file_decompress_impl(huff_ctx* ctx, const char* src, const char* d
         pos += wend;
         cur = nxt;
     }
-    return write_syms((k - 1) & 1, pending);
+    return writer.drain();
 }
 
 Status file_compress(huff_ctx* ctx, const char* src, const char* dst, size_t block_size) {
