@@ -40,7 +40,7 @@ constexpr uint32_t kInCap = 4608;                // input stage bytes per wave (
 // its 64 output rows of 64 B
 constexpr uint32_t kRowBytes = 64;  // 16-B pieces XOR-swizzled by (row >> 1) & 3: conflict-free ds_write_b128
 template <bool PAD>
-constexpr uint32_t fx_stage_bytes() { return PAD ? kInCap * 9 / 8 : kInCap; }  // input padded 1/8 when PAD
+constexpr uint32_t fx_stage_bytes() { return kInCap; }  // PAD (swizzled) or not: a permutation of the same bytes
 static_assert(64 * kRowBytes <= kInCap, "the output rows fit the stage");
 __device__ __forceinline__ uint32_t row_piece(uint32_t row, uint32_t q) { return row * kRowBytes + 16 * (q ^ ((row >> 1) & 3)); }
 constexpr uint32_t kInPieces = kInCap / 16;      // 288 16-B pieces
@@ -129,14 +129,18 @@ struct LdsWords {
     const uint32_t* w;
     __device__ __forceinline__ uint32_t operator()(uint32_t i) const { return w[i]; }
 };
-// k_decode_fixed's stage with one pad piece (16 B) after every 8: lanes whose
-// streams start a power-of-two number of dwords apart (8-bit codes: 16 dwords)
-// otherwise hit the same two banks on every refill (16-way conflicts)
+// PAD stages (DecodeArgs::pad_stage): dword i of the stream at i ^ (((i >> 5)
+// & 7) << 2) — the 16-B pieces of every 128-B block XOR-permuted by the
+// block index, so lanes whose starts are ~32 m / k dwords apart (mean code
+// lengths near 3.2, 4, 5.33, 8, 10.67 or 12 bits) spread over the banks
+// instead of queueing on a few; same size as the plain stage (the round-1
+// layout padded one piece per 8: 1/8 more LDS, 5 waves per SIMD instead of
+// 6). Zipf (10.6 dwords per lane) decode 0.505 -> 0.497 ms, same box.
 struct PaddedLdsWords {
     const uint32_t* w;
-    __device__ __forceinline__ uint32_t operator()(uint32_t i) const { return w[i + ((i >> 5) << 2)]; }
+    __device__ __forceinline__ uint32_t operator()(uint32_t i) const { return w[i ^ ((i >> 3) & 28u)]; }
 };
-__device__ __forceinline__ uint32_t padded_piece(uint32_t p) { return p + (p >> 3); }
+__device__ __forceinline__ uint32_t padded_piece(uint32_t p) { return p ^ ((p >> 3) & 7u); }
 struct GlobalWords {
     const uint8_t* comp;
     uint64_t nbytes;
@@ -590,10 +594,11 @@ __device__ __forceinline__ void decode_fixed_body(const DecodeArgs& a) {
     }
 }
 
-// Production kernels: the compiler's register allocation (k_decode_fixed 63
-// VGPRs / 8 waves per SIMD; the padded and slow variants 93-112 / 4-5 waves).
+// Production kernels: the compiler's register allocation (k_decode_fixed 71
+// VGPRs / 7 waves per SIMD, the LDS allows 6), the swizzled-stage variants
+// held to 6 waves (80 VGPRs; 74 without spills); the slow variants 92-112 / 4-5.
 template <bool PAD>
-__global__ __launch_bounds__(kThreads) void k_decode_fixed(DecodeArgs a) {
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(PAD ? 6 : 1, 8))) void k_decode_fixed(DecodeArgs a) {
     decode_fixed_body<false, PAD, false>(a);
 }
 template <bool PAD>
@@ -617,7 +622,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(8, 8))
 // index-free streams with k_mark_lite's entries: each lane first decodes and
 // drops its skip codes
 template <bool SLOW, bool PAD>
-__global__ __launch_bounds__(kThreads) void k_decode_fixed_skip(DecodeArgs a) {
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(PAD && !SLOW ? 6 : 1, 8))) void k_decode_fixed_skip(DecodeArgs a) {
     decode_fixed_body<SLOW, PAD, false, true>(a);
 }
 // diagnostics: the production body (no check) forced to >= 5 waves per SIMD

@@ -103,9 +103,10 @@ struct DecodeArgs {
     // sub_abs64 entries as k_mark_lite writes them: a boundary at or before
     // the symbol in bits [0, 48) and the codes to skip from it in [48, 64)
     uint32_t skip_packed;
-    // k_decode_fixed: pad the input stage (one 16-B piece per 8) — for mean
-    // code lengths near 4, 8 or 12 bits the lanes' streams start a multiple of
-    // 8 dwords apart and every refill would hit the same few LDS banks
+    // k_decode_fixed: swizzle the input stage (16-B pieces XOR-permuted per
+    // 128-B block, decode_wave.hip PaddedLdsWords): for mean code lengths
+    // where the lanes' streams start ~32 m / k dwords apart every refill
+    // would hit the same few LDS banks
     uint32_t pad_stage;
     // k_decode_fixed self-check builds (0: production kernel; 1: checked;
     // 2: checked, >= 5 waves per SIMD forced; 3: checked, 8 waves per
@@ -113,12 +114,17 @@ struct DecodeArgs {
     uint32_t check_mode;
     uint32_t* err;
 };
-// whether k_decode_fixed should pad its stage for this mean code length
+// whether k_decode_fixed should swizzle its stage for this mean code
+// length: the stride bands where a bank model of the 32-lane refill reads
+// (lane starts jittered 0.6 dwords per 64 symbols; tools/stage_banks.py)
+// gives the swizzled stage >= 1 LDS cycle fewer per read than the plain one
 inline bool fixed_decode_pad(uint64_t bits, uint64_t nsym) {
     if (nsym == 0) return false;
-    const double stride = 2.0 * static_cast<double>(bits) / static_cast<double>(nsym);  // dwords per 64 symbols
-    const double r = stride - 8.0 * static_cast<double>(static_cast<uint64_t>(stride / 8.0 + 0.5));
-    return stride >= 7.5 && stride <= 24.5 && r > -0.5 && r < 0.5;
+    const double s = 2.0 * static_cast<double>(bits) / static_cast<double>(nsym);  // dwords per 64 symbols
+    static const double band[][2] = {{6.35, 6.45}, {7.75, 8.25}, {10.45, 10.95}, {15.55, 16.45}, {21.05, 21.65}, {23.85, 24.15}};
+    for (const auto& b : band)
+        if (s >= b[0] && s <= b[1]) return true;
+    return false;
 }
 
 struct IndexlessArgs {
