@@ -510,6 +510,34 @@ __device__ __forceinline__ void decode_fixed_body(const DecodeArgs& a) {
     // 16-B pieces (all 16-B accesses through u32x4_alias)
     uint32_t* stage = lds + ((tab_words + 3) & ~3u) + wave * (fx_stage_bytes<PAD>() / 4);
     uint8_t* sb = reinterpret_cast<uint8_t*>(stage);
+#if HUFF_DEC_EARLY_LOADS
+    // Wrong-letter reproducer ("Co-resident wrong letters"),
+    // never in production builds: the first task's index and input loads go
+    // out before the table is staged, joined by a bare barrier. Correct in
+    // source order, yet its PAD instantiation (72 VGPRs) decodes wrong letters
+    // in ~3 % of the tasks of later-dispatched workgroups.
+    const uint64_t ntasks = (a.n + kTaskSym - 1) / kTaskSym;
+    const uint64_t step = static_cast<uint64_t>(gridDim.x) * kWaves;
+    uint64_t task = static_cast<uint64_t>(blockIdx.x) * kWaves + wave;
+    const bool have = task < ntasks;
+    const uint32_t tab_pieces = (tab_words + 3) / 4;
+    const auto rtab = buf_rsrc(a.stab, tab_words * 4);
+    uint4 tp[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) tp[i] = buf_ld16(rtab, (t + kThreads * i) * 16);
+    Task cur{};
+    uint4 pre[kLoadRounds];
+    if (have) {
+        cur = task_info<SKIP>(a, task, lane);
+        issue_task_loads(a, cur, lane, pre);
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+        if (t + kThreads * i < tab_pieces) st_stage16(lds + 4 * (t + kThreads * i), tp[i]);
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): table stores done; the input loads stay in flight
+    __builtin_amdgcn_s_barrier();
+    if (!have) return;
+#else
     for (uint32_t i = t; i < tab_words; i += kThreads) lds[i] = reinterpret_cast<const uint32_t*>(a.stab)[i];
     __syncthreads();
 
@@ -519,6 +547,7 @@ __device__ __forceinline__ void decode_fixed_body(const DecodeArgs& a) {
     if (task >= ntasks) return;
 
     Task cur = task_info<SKIP>(a, task, lane);
+#endif
 
     // no software prefetch of the next task: its 20 registers would cost a
     // wave per SIMD; the other resident waves hide the load latency instead.
@@ -527,8 +556,10 @@ __device__ __forceinline__ void decode_fixed_body(const DecodeArgs& a) {
     //   stage writes (input) -> sync -> lane reads -> sync -> row writes
     //   (output transpose) -> sync -> row reads -> sync -> next task's writes
     while (true) {
+#if !HUFF_DEC_EARLY_LOADS
         uint4 pre[kLoadRounds];
         issue_task_loads(a, cur, lane, pre);
+#endif
         const uint32_t np = cur.len <= kInCap ? cur.len / 16 : 0u;
 #pragma unroll
         for (uint32_t r = 0; r < kLoadRounds; ++r) {
@@ -591,6 +622,9 @@ __device__ __forceinline__ void decode_fixed_body(const DecodeArgs& a) {
         wave_sync();  // the input stage is reused by the next task
         task = nxt_task;
         cur = task_info<SKIP>(a, task, lane);
+#if HUFF_DEC_EARLY_LOADS
+        issue_task_loads(a, cur, lane, pre);
+#endif
     }
 }
 

@@ -1,0 +1,55 @@
+#!/usr/bin/env python3
+"""Locate wrong letters of the production fixed-count decoder (no self-check):
+decode a 16 MiB stream twice, compare with the input, and report the wrong
+bytes by task / lane / letter (4,096-symbol tasks, 64 letters per lane)."""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "huff-encoding_amd"))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import huff_coding as H  # noqa: E402
+from huff_coding import device as D  # noqa: E402
+
+
+def main():
+    ctx = H.Context(0)
+    for kind in sys.argv[1:] or ["zipf"]:
+        n = 1 << 24
+        seed = {"uniform": 0x5EED0001, "zipf": 0x5EED0002, "text": 0x5EED0005}[kind]
+        x = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
+        D.generate(ctx, kind, seed, x.data_ptr(), n, cdf=D.zipf_cdf(1.2) if kind == "zipf" else None)
+        os.environ["HUFF_DISABLE_FIXED8"] = "1"
+        job = H.EncodeJob(ctx, x.data_ptr(), n)
+        tree = H.HuffTree.from_weights(H.ByteWeights.from_array(job.hist()))
+        bits = job.bits(tree)
+        out = torch.zeros((bits + 7) // 8 + 64, dtype=torch.uint8, device="cuda")
+        job.pack(tree, out.data_ptr(), out.numel())
+        ref = x[:n].cpu().numpy()
+        prev = None
+        for rep in range(3):
+            dec = torch.zeros(n + 64, dtype=torch.uint8, device="cuda")
+            job.decode(tree, out.data_ptr(), dec.data_ptr())
+            torch.cuda.synchronize()
+            got = dec[:n].cpu().numpy()
+            bad = np.nonzero(got != ref)[0]
+            tasks = np.unique(bad // 4096)
+            first = {}
+            for t in tasks[:2000]:
+                b = bad[(bad >= t * 4096) & (bad < (t + 1) * 4096)] - t * 4096
+                lanes = np.unique(b // 64)
+                first[int(t)] = {"lanes": len(lanes), "first_letter_per_lane": sorted(set(int(min(b[b // 64 == l] % 64)) for l in lanes))[:8]}
+            same = prev is not None and np.array_equal(prev, bad)
+            prev = bad
+            letters = np.bincount(bad % 64, minlength=64)
+            print(json.dumps({"kind": kind, "rep": rep, "bits": bits, "wrong_bytes": int(bad.size), "wrong_tasks": int(tasks.size),
+                              "ntasks": (n + 4095) // 4096, "same_as_prev_rep": bool(same),
+                              "first_letter_hist": {i: int(c) for i, c in enumerate(letters) if c},
+                              "tasks": dict(list(first.items())[:6]),
+                              "task_mod4": np.bincount(tasks % 4, minlength=4).tolist()}), flush=True)
+
+
+main()
