@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Locate wrong letters of the production fixed-count decoder (no self-check):
-decode a 16 MiB stream twice, compare with the input, and report the wrong
-bytes by task / lane / letter (4,096-symbol tasks, 64 letters per lane)."""
+decode a stream DIAG_REPS times (default 3) at DIAG_MIB MiB (default 16),
+compare with the input, and report the wrong bytes by task / lane / letter
+(4,096-symbol tasks, 64 letters per lane)."""
 import json
 import os
 import sys
@@ -18,7 +19,7 @@ from huff_coding import device as D  # noqa: E402
 def main():
     ctx = H.Context(0)
     for kind in sys.argv[1:] or ["zipf"]:
-        n = 1 << 24
+        n = int(os.environ.get("DIAG_MIB", "16")) << 20
         seed = {"uniform": 0x5EED0001, "zipf": 0x5EED0002, "text": 0x5EED0005}[kind]
         x = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
         D.generate(ctx, kind, seed, x.data_ptr(), n, cdf=D.zipf_cdf(1.2) if kind == "zipf" else None)
@@ -30,7 +31,7 @@ def main():
         job.pack(tree, out.data_ptr(), out.numel())
         ref = x[:n].cpu().numpy()
         prev = None
-        for rep in range(3):
+        for rep in range(int(os.environ.get("DIAG_REPS", "3"))):
             dec = torch.zeros(n + 64, dtype=torch.uint8, device="cuda")
             job.decode(tree, out.data_ptr(), dec.data_ptr())
             torch.cuda.synchronize()

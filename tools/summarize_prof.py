@@ -18,7 +18,11 @@ def short(name: str) -> str:
     """the kernel's function name (k_hist1, k_decode_ring, ...), else a prefix"""
     m = re.search(r"\b(k_[A-Za-z0-9_]+)", name)
     if m:
-        return m.group(1) + ("<long>" if "<true" in name or "ILb1E" in name else "")
+        # the first template flag is LONG (codes > 32 bits) only for the pack
+        # and the chunk decoder; elsewhere it is a layout or variant flag
+        # (k_decode_fixed<PAD>: the swizzled stage) and the name stays plain
+        long_flag = m.group(1) in ("k_pack", "k_decode") and ("<true" in name or "ILb1E" in name)
+        return m.group(1) + ("<long>" if long_flag else "")
     return name[:40]
 
 
