@@ -734,7 +734,11 @@ hipError_t launch_decode_fixed(const DecodeArgs& a, hipStream_t s) {
     const char* o = std::getenv("HUFF_DEC_ONESHOT");
     if (!a.check_mode && !(o && *o == '0')) cap = want;
     const uint32_t grid = static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>(want, cap)));
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), lds, s, a);
+    // diagnostics (wrong-letter reproducer): HUFF_DEC_LDS_EXTRA bytes of unused
+    // dynamic LDS cap the workgroups per CU without changing the code object
+    size_t lds_launch = lds;
+    if (const char* x = std::getenv("HUFF_DEC_LDS_EXTRA")) lds_launch += static_cast<size_t>(std::max(0, std::atoi(x)));
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), lds_launch, s, a);
     return hipGetLastError();
 }
 
