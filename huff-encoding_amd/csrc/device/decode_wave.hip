@@ -632,7 +632,10 @@ __device__ __forceinline__ void decode_fixed_body(const DecodeArgs& a) {
 // VGPRs / 7 waves per SIMD, the LDS allows 6), the swizzled-stage variants
 // held to 6 waves (80 VGPRs; 74 without spills); the slow variants 92-112 / 4-5.
 template <bool PAD>
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(PAD ? 6 : 1, 8))) void k_decode_fixed(DecodeArgs a) {
+#ifndef HUFF_DEC_PAD_WAVES  // experiments only: the PAD body's minimum waves per SIMD
+#define HUFF_DEC_PAD_WAVES 6
+#endif
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(PAD ? HUFF_DEC_PAD_WAVES : 1, 8))) void k_decode_fixed(DecodeArgs a) {
     decode_fixed_body<false, PAD, false>(a);
 }
 template <bool PAD>
