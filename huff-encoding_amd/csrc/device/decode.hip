@@ -42,8 +42,8 @@ __device__ __forceinline__ uint4 load_slot(const uint8_t* __restrict__ comp, uin
     return make_uint4(x, y, z, w);
 }
 
-// Generic variant (any code length <= 57): per-lane 4 x 16-B ring, global
-// window slow path. Used when some code is longer than 32 bits.
+// Codes of 33-57 bits (a tree deeper than the fixed-count decoder's 32): per
+// lane a 4 x 16-B register ring, global window slow path.
 template <bool LONG>
 __global__ __launch_bounds__(kThreads) void k_decode(DecodeArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -184,136 +184,19 @@ __global__ __launch_bounds__(kThreads) void k_decode(DecodeArgs a) {
 #undef RING_SEEK
 }
 
-// Fast variant (every code <= 32 bits). Per lane:
-//  - input in 64-byte units: the 4 dwordx4 loads of a unit are issued
-//    together (one 64-B sector, fetched once) and the next unit is in flight
-//    while this one is decoded; the unit's 16 dwords are consumed at static
-//    register positions (no dynamically indexed registers, no scratch);
-//  - the primary table is replicated 2^lut_rep_log2 times (lane l reads copy
-//    l % R) to spread LDS bank conflicts;
-//  - output goes to a lane-private LDS row and leaves as one whole 64-byte
-//    sector (4 x dwordx4) every 64 symbols: no cross-lane synchronisation.
-__global__ __launch_bounds__(kThreads) void k_decode_short(DecodeArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    const uint32_t K = a.lut_bits;
-    const uint32_t LR = a.lut_rep_log2;
-    const uint32_t nprim = 1u << K;
-    uint32_t* plut = lds;
-    uint32_t* rows = lds + (((nprim << LR) + 3) & ~3u);
-    const uint32_t t = threadIdx.x;
-    for (uint32_t i = t; i < (nprim << LR); i += kThreads) plut[i] = a.lut[i >> LR];
-    __syncthreads();
-
-    const uint32_t rep = t & ((1u << LR) - 1);
-    const uint32_t c = blockIdx.x;
-    const uint64_t sym0 = static_cast<uint64_t>(c) * kChunk;
-    const uint64_t nsym = (a.n - sym0 < kChunk) ? a.n - sym0 : kChunk;
-    const uint64_t lsym0 = static_cast<uint64_t>(t) * kSub;
-    const uint32_t cnt = lsym0 >= nsym ? 0u : static_cast<uint32_t>(nsym - lsym0 < kSub ? nsym - lsym0 : kSub);
-    if (cnt == 0) return;
-
-    const uint64_t pos = a.chunk_start[c] + a.sub_bit[(sym0 + lsym0) / kIdx];
-    uint8_t* dst = a.out + sym0 + lsym0;
-    uint32_t* row = rows + t * kStageStride;
-    uint64_t unit = pos >> 9;                          // 64-byte units
-    uint32_t drop = static_cast<uint32_t>(pos & 511);  // bits of the first unit before pos
-    uint4 A0 = load_slot(a.comp, a.comp_bytes, unit * 4 + 0);
-    uint4 A1 = load_slot(a.comp, a.comp_bytes, unit * 4 + 1);
-    uint4 A2 = load_slot(a.comp, a.comp_bytes, unit * 4 + 2);
-    uint4 A3 = load_slot(a.comp, a.comp_bytes, unit * 4 + 3);
-    uint64_t buf = 0;
-    uint32_t nb = 0, j = 0, acc = 0;
-
-    auto flush64 = [&](uint32_t jend) {  // symbols [jend-64, jend) from the row
-        const uint64_t o = jend - 64;
-        uint4* d4 = reinterpret_cast<uint4*>(dst + o);
-        d4[0] = make_uint4(row[0], row[1], row[2], row[3]);
-        d4[1] = make_uint4(row[4], row[5], row[6], row[7]);
-        d4[2] = make_uint4(row[8], row[9], row[10], row[11]);
-        d4[3] = make_uint4(row[12], row[13], row[14], row[15]);
-    };
-
-#define DEC_POS(dw)                                                                        \
-    do {                                                                                   \
-        if (nb < 32) {                                                                     \
-            buf |= static_cast<uint64_t>(__builtin_bswap32(dw)) << (32 - nb);              \
-            nb += 32;                                                                      \
-        }                                                                                  \
-        if (drop) {                                                                        \
-            const uint32_t k_ = drop < nb ? drop : nb;                                     \
-            buf <<= k_;                                                                    \
-            nb -= k_;                                                                      \
-            drop -= k_;                                                                    \
-        }                                                                                  \
-        while (nb >= 32 && j < cnt) {                                                      \
-            uint32_t e = plut[(static_cast<uint32_t>(buf >> (64 - K)) << LR) | rep];       \
-            if (e & kLutPtr) {                                                             \
-                uint32_t d = K;                                                            \
-                do {                                                                       \
-                    const uint32_t idx = static_cast<uint32_t>((buf >> (56 - d)) & 0xFFu); \
-                    e = a.lut[(e & ~kLutPtr) + idx];                                       \
-                    d += 8;                                                                \
-                } while (e & kLutPtr);                                                     \
-            }                                                                              \
-            const uint32_t len = (e >> 8) & 0xFFu;                                         \
-            buf <<= len;                                                                   \
-            nb -= len;                                                                     \
-            acc |= (e & 0xFFu) << (8 * (j & 3));                                           \
-            if ((j & 3) == 3) {                                                            \
-                row[(j >> 2) & 15] = acc;                                                  \
-                acc = 0;                                                                   \
-                if ((j & 63) == 63) flush64(j + 1);                                        \
-            }                                                                              \
-            ++j;                                                                           \
-        }                                                                                  \
-    } while (0)
-
-    while (j < cnt) {
-        ++unit;
-        const uint4 B0 = load_slot(a.comp, a.comp_bytes, unit * 4 + 0);
-        const uint4 B1 = load_slot(a.comp, a.comp_bytes, unit * 4 + 1);
-        const uint4 B2 = load_slot(a.comp, a.comp_bytes, unit * 4 + 2);
-        const uint4 B3 = load_slot(a.comp, a.comp_bytes, unit * 4 + 3);
-        DEC_POS(A0.x); DEC_POS(A0.y); DEC_POS(A0.z); DEC_POS(A0.w);
-        DEC_POS(A1.x); DEC_POS(A1.y); DEC_POS(A1.z); DEC_POS(A1.w);
-        DEC_POS(A2.x); DEC_POS(A2.y); DEC_POS(A2.z); DEC_POS(A2.w);
-        DEC_POS(A3.x); DEC_POS(A3.y); DEC_POS(A3.z); DEC_POS(A3.w);
-        A0 = B0;
-        A1 = B1;
-        A2 = B2;
-        A3 = B3;
-    }
-#undef DEC_POS
-    // ragged end (only the last lane of the last chunk): bytes [j & ~63, j)
-    if (j & 63) {
-        if (j & 3) row[(j >> 2) & 15] = acc;
-        const uint32_t base = j & ~63u;
-        for (uint32_t i = base; i < j; ++i) dst[i] = static_cast<uint8_t>(row[(i >> 2) & 15] >> (8 * (i & 3)));
-    }
-}
-
-
 }  // namespace
 
-size_t decode_lds_bytes(uint32_t lut_bits, uint32_t rep_log2) {
-    const uint32_t nprim = (((1u << lut_bits) << rep_log2) + 3) & ~3u;
+size_t decode_lds_bytes(uint32_t lut_bits) {
+    const uint32_t nprim = ((1u << lut_bits) + 3) & ~3u;
     return static_cast<size_t>(nprim + kThreads * kStageStride) * 4;
 }
 
+// codes of 33-57 bits here; every code <= 32 bits: the fixed-count task
+// decoder (decode_wave.hip)
 hipError_t launch_decode(const DecodeArgs& a, hipStream_t s) {
     if (a.nchunks == 0) return hipSuccess;
-    if (a.max_len > 32) {
-        hipLaunchKernelGGL(k_decode<true>, dim3(a.nchunks), dim3(kThreads), decode_lds_bytes(a.lut_bits, 0), s, a);
-    } else if (a.variant == kDecodeFixed && a.stab) {
-        return launch_decode_fixed(a, s);
-    } else if (a.variant == kDecodeWave && a.mlut) {
-        return launch_decode_wave(a, s);
-    } else if (a.variant == kDecodeRing && a.mlut) {
-        return launch_decode_ring(a, s);
-    } else {
-        hipLaunchKernelGGL(k_decode_short, dim3(a.nchunks), dim3(kThreads),
-                           decode_lds_bytes(a.lut_bits, a.lut_rep_log2), s, a);
-    }
+    if (a.max_len <= 32) return a.stab ? launch_decode_fixed(a, s) : hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_decode<true>, dim3(a.nchunks), dim3(kThreads), decode_lds_bytes(a.lut_bits), s, a);
     return hipGetLastError();
 }
 

@@ -1,26 +1,19 @@
 // decode_wave.hip — restart-index decode with wave-contiguous memory traffic
-// (comp.rs:487-519 semantics; restart index = chunk_start + sub_bit, one
-// entry per kIdx = 64 symbols, written by pack).
+// (comp.rs:487-519 semantics; restart index = chunk_start + sub_bit or the
+// compact task_base + sub16 form, one entry per kIdx = 64 symbols, written by
+// pack).
 //
 // Work unit: a TASK of 4,096 consecutive symbols per wave (lane l decodes
 // symbols [64 l, 64 l + 64) of the task). A task's compressed bits are one
-// contiguous range, and so is its output, so both move as whole lines:
-//  1. the wave loads the task's compressed byte range (16-B aligned, with a
-//     small lookahead) into its LDS input stage with coalesced 16-B loads;
-//  2. every lane decodes its 64 symbols from the stage: a 64-bit window
-//     refilled 32 bits at a time (the next dword is read one refill ahead),
-//     one lookup of the top K (= 12) window bits in the multi-symbol table
-//     (LDS) per step giving up to 3 letters, ORed into the lane's current
-//     output dword, which is stored (aligned) after every step;
-//  3. the wave stores its 4 KiB of letters as 16-B coalesced stores.
-// The loads of task t+1 are issued before task t is decoded (register
-// staging), so the HBM latency of a wave's input overlaps its own decode.
-// A task whose range exceeds the stage (long local codes; never for byte
-// data whose mean code length is <= 8 bits in any 4,096-symbol window of
-// up to 9 bits/symbol) decodes straight from global memory instead.
+// contiguous range, and so is its output, so both move as whole lines: the
+// wave stages its compressed range in LDS with coalesced 16-B loads, every
+// lane decodes exactly 64 letters from the stage (k_decode_fixed below), and
+// the wave's 4 KiB of letters leave through an LDS transpose as 1 KiB
+// contiguous stores. A task whose range exceeds the stage (long local codes)
+// decodes straight from global memory instead.
 //
 // Roofline: HBM-bound; algorithmic traffic ceil(bits/8) (read) + n (write)
-// + 4 B per 64 symbols of index.
+// + the restart index (2 B per 64 symbols + 8 B per task in the compact form).
 #include <algorithm>
 #include <cstdlib>
 
@@ -34,7 +27,6 @@ constexpr int kThreads = 256;
 constexpr int kWaves = kThreads / 64;
 constexpr uint32_t kLaneSym = kIdx;              // symbols per lane per task
 static_assert(kTaskSym == 64 * kLaneSym, "4,096 symbols per wave task");
-constexpr uint32_t kOutWords = kLaneSym / 4 + 2; // output dwords per lane (64 letters + overshoot)
 constexpr uint32_t kInCap = 4608;                // input stage bytes per wave (9 bits per symbol)
 // k_decode_fixed's per-wave stage: the task's input, then (after the decode)
 // its 64 output rows of 64 B
@@ -45,8 +37,18 @@ static_assert(64 * kRowBytes <= kInCap, "the output rows fit the stage");
 __device__ __forceinline__ uint32_t row_piece(uint32_t row, uint32_t q) { return row * kRowBytes + 16 * (q ^ ((row >> 1) & 3)); }
 constexpr uint32_t kInPieces = kInCap / 16;      // 288 16-B pieces
 constexpr uint32_t kLoadRounds = (kInPieces + 63) / 64;  // 5
-constexpr uint32_t kWaveLds = kInCap + 64 * 4 * kOutWords;
 static_assert(kChunk % kTaskSym == 0, "a task never straddles a chunk");
+// The first task's loads issued before the table copy (HUFF_DEC_EARLY_LOADS=0
+// for the A/B build without), and the minimum waves per SIMD of the PAD
+// bodies (their register floor)
+#ifndef HUFF_DEC_EARLY_LOADS
+#define HUFF_DEC_EARLY_LOADS 1
+#endif
+#ifndef HUFF_DEC_PAD_WAVES
+#define HUFF_DEC_PAD_WAVES 5
+#endif
+constexpr bool kEarlyLoads = HUFF_DEC_EARLY_LOADS != 0;
+constexpr int kPadWaves = HUFF_DEC_PAD_WAVES;
 
 struct Task {
     uint64_t sym0;      // first symbol
@@ -123,7 +125,7 @@ __device__ __forceinline__ void issue_task_loads(const DecodeArgs& a, const Task
     for (uint32_t r = 0; r < R; ++r) pre[r] = buf_ld16(rs, (lane + 64 * r) * 16);
 }
 
-// dword sources for the lane decoder (stream order: the first byte is the
+// dword sources for the lane decoders (stream order: the first byte is the
 // most significant): the LDS stage (byte-swapped when staged), or global memory
 struct LdsWords {
     const uint32_t* w;
@@ -153,158 +155,6 @@ struct GlobalWords {
         return v;
     }
 };
-
-// Decode `cnt` symbols starting at bit `rel` of the word source into the
-// lane's output column (dword d of the lane at ocol[64 d]: the 64 lanes of
-// a wave write 64 consecutive dwords whatever their progress, conflict-free). The window holds >= 32 valid
-// bits before every pair of lookups; a multi-symbol entry uses <= K (= 12)
-// bits. SLOW: some code is longer than K (<= 32 bits): a window whose first
-// code is that long (entry kMsSlow, rare) is refilled, decoded with the
-// single-symbol tables (global, L2-resident) and refilled again, so the
-// invariant holds for the next lookup.
-template <bool SLOW, class Words>
-__device__ __forceinline__ void decode_lane(const Words& src, uint32_t rel, uint32_t cnt, uint32_t* ocol,
-                                            const uint32_t* __restrict__ mlut, uint32_t K,
-                                            const uint32_t* __restrict__ glut, uint32_t Ks) {
-    if (cnt == 0) return;
-    uint32_t rp = rel >> 5;
-    const uint32_t sh = rel & 31;
-    uint64_t buf = ((static_cast<uint64_t>(src(rp)) << 32) | src(rp + 1)) << sh;
-    uint32_t nb = 64 - sh;
-    rp += 2;
-    uint32_t nextw = src(rp);
-    uint32_t j = 0;    // letters decoded
-    uint32_t cur = 0;  // the output dword j / 4, partially filled (aligned LDS stores only:
-                       // an unaligned ds_write_b32 is replayed by the LDS)
-
-#define WV_REFILL()                                                                                 \
-    do {                                                                                            \
-        const bool need_ = nb < 32;                                                                 \
-        const uint64_t add_ = static_cast<uint64_t>(nextw) << ((32 - nb) & 63);                     \
-        buf |= need_ ? add_ : 0ull;                                                                 \
-        nb += need_ ? 32u : 0u;                                                                     \
-        rp += need_ ? 1u : 0u;                                                                      \
-        nextw = src(rp);                                                                            \
-    } while (0)
-
-#define WV_LOOKUP()                                                                                 \
-    do {                                                                                            \
-        uint32_t e = mlut[static_cast<uint32_t>(buf >> 32) >> (32 - K)];                            \
-        if (SLOW && (e & kMsSlow)) {                                                                \
-            WV_REFILL();                                                                            \
-            uint32_t e1 = glut[static_cast<uint32_t>(buf >> (64 - Ks))];                            \
-            uint32_t d = Ks;                                                                        \
-            while (e1 & kLutPtr) {                                                                  \
-                const uint32_t idx = static_cast<uint32_t>((buf >> (56 - d)) & 0xFFu);              \
-                e1 = glut[(e1 & ~kLutPtr) + idx];                                                   \
-                d += 8;                                                                             \
-            }                                                                                       \
-            const uint32_t l1 = (e1 >> 8) & 0xFFu;                                                  \
-            buf <<= l1;                                                                             \
-            nb -= l1;                                                                               \
-            WV_REFILL();                                                                            \
-            e = (e1 & 0xFFu) | (1u << 29);                                                          \
-        }                                                                                           \
-        const uint32_t used = (e >> 24) & 31u;                                                      \
-        buf <<= used;                                                                               \
-        nb -= used;                                                                                 \
-        const uint64_t v_ = static_cast<uint64_t>(e & 0xFFFFFFu) << ((j & 3u) * 8);                 \
-        cur |= static_cast<uint32_t>(v_);                                                           \
-        ocol[(j & ~3u) * 16] = cur;                                                                 \
-        const uint32_t j2_ = j + ((e >> 29) & 3u);                                                  \
-        cur = ((j2_ ^ j) & ~3u) ? static_cast<uint32_t>(v_ >> 32) : cur;                            \
-        j = j2_;                                                                                    \
-    } while (0)
-
-    while (j < cnt) {
-        WV_REFILL();
-        WV_LOOKUP();
-        WV_LOOKUP();
-    }
-    // letters carried into the next dword by the last step
-    ocol[(j & ~3u) * 16] = cur;
-#undef WV_LOOKUP
-#undef WV_REFILL
-}
-
-template <bool SLOW>
-__global__ __launch_bounds__(kThreads) void k_decode_wave(DecodeArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    const uint32_t K = a.mlut_bits;
-    const uint32_t nent = 1u << K;
-    const uint32_t t = threadIdx.x, lane = t & 63, wave = wave_index();
-    uint32_t* mlut = lds;
-    uint8_t* wbase = reinterpret_cast<uint8_t*>(lds + nent) + wave * kWaveLds;
-    uint4* in_stage = reinterpret_cast<uint4*>(wbase);
-    uint32_t* out_stage = reinterpret_cast<uint32_t*>(wbase + kInCap);
-    for (uint32_t i = t; i < nent; i += kThreads) mlut[i] = a.mlut[i];
-    __syncthreads();
-
-    const uint64_t ntasks = (a.n + kTaskSym - 1) / kTaskSym;
-    const uint64_t step = static_cast<uint64_t>(gridDim.x) * kWaves;
-    uint64_t task = static_cast<uint64_t>(blockIdx.x) * kWaves + wave;
-    if (task >= ntasks) return;
-
-    // register staging of the next task's input
-    uint4 pre[kLoadRounds];
-    Task cur = task_info(a, task, lane);
-    auto issue = [&](const Task& k) { issue_task_loads(a, k, lane, pre); };
-    issue(cur);
-
-    while (true) {
-        // the staged input of `cur` goes to LDS, then the next task's loads are issued
-        const uint32_t np = cur.len <= kInCap ? cur.len / 16 : 0u;
-#pragma unroll
-        for (uint32_t r = 0; r < kLoadRounds; ++r) {
-            const uint32_t p = lane + 64 * r;
-            if (p < np) {
-                const uint4 v = pre[r];
-                in_stage[p] = make_uint4(__builtin_bswap32(v.x), __builtin_bswap32(v.y), __builtin_bswap32(v.z),
-                                         __builtin_bswap32(v.w));
-            }
-        }
-        const uint64_t nxt_task = task + step;
-        Task nxt;
-        const bool more = nxt_task < ntasks;
-        if (more) {
-            nxt = task_info(a, nxt_task, lane);
-            issue(nxt);
-        }
-        wave_sync();
-
-        const uint32_t rel = static_cast<uint32_t>(cur.lane_bit - cur.b0 * 8);
-        uint32_t* ocol = out_stage + lane;
-        if (cur.len <= kInCap) {
-            decode_lane<SLOW>(LdsWords{reinterpret_cast<const uint32_t*>(in_stage)}, rel, cur.cnt, ocol, mlut, K,
-                              a.lut, a.lut_bits);
-        } else {
-            decode_lane<SLOW>(GlobalWords{a.comp, a.comp_bytes, cur.b0 / 4}, rel, cur.cnt, ocol, mlut, K, a.lut,
-                              a.lut_bits);
-        }
-        wave_sync();
-
-        // 4 KiB of letters: piece p (16 B) = dwords 4 (p%4) .. +3 of lane p/4
-        uint8_t* dst = a.out + cur.sym0;
-#pragma unroll
-        for (uint32_t r = 0; r < 4; ++r) {
-            const uint32_t p = lane + 64 * r;
-            const uint32_t o = p * 16;
-            if (o >= cur.nsym) continue;
-            const uint32_t* s = out_stage + (p & 3) * 4 * 64 + (p >> 2);
-            const uint4 x = make_uint4(s[0], s[64], s[128], s[192]);
-            if (o + 16 <= cur.nsym) {
-                *reinterpret_cast<uint4*>(dst + o) = x;
-            } else {
-                const uint32_t w[4] = {x.x, x.y, x.z, x.w};
-                for (uint32_t i = 0; o + i < cur.nsym; ++i) dst[o + i] = static_cast<uint8_t>(w[i >> 2] >> (8 * (i & 3)));
-            }
-        }
-        if (!more) break;
-        wave_sync();  // the stages are reused by the next task
-        task = nxt_task;
-        cur = nxt;
-    }
-}
 
 // ---------------------------------------------------------------------------
 // k_decode_fixed: the same tasks, one letter per lookup. Every lane makes
@@ -469,7 +319,7 @@ __device__ __forceinline__ uint4 ld_stage16(const void* p) {
     return make_uint4(v.x, v.y, v.z, v.w);
 }
 
-// Self-check (CHECK builds: HUFF_DEC_VARIANT 11-13): every lane's letters
+// Self-check (the CHECK build, HUFF_DEC_VARIANT=11): every lane's letters
 // must end exactly where the next lane's restart entry (or, for the task's
 // last lane, the next task's first bit) begins. A mismatch is counted in
 // err[0]; the first one records (task, lane, expected, got) in err[1..6]. No
@@ -510,44 +360,37 @@ __device__ __forceinline__ void decode_fixed_body(const DecodeArgs& a) {
     // 16-B pieces (all 16-B accesses through u32x4_alias)
     uint32_t* stage = lds + ((tab_words + 3) & ~3u) + wave * (fx_stage_bytes<PAD>() / 4);
     uint8_t* sb = reinterpret_cast<uint8_t*>(stage);
-#if HUFF_DEC_EARLY_LOADS
-    // Wrong-letter reproducer ("Co-resident wrong letters"),
-    // never in production builds: the first task's index and input loads go
-    // out before the table is staged, joined by a bare barrier. Correct in
-    // source order, yet its PAD instantiation (72 VGPRs) decodes wrong letters
-    // in ~3 % of the tasks of later-dispatched workgroups.
     const uint64_t ntasks = (a.n + kTaskSym - 1) / kTaskSym;
     const uint64_t step = static_cast<uint64_t>(gridDim.x) * kWaves;
     uint64_t task = static_cast<uint64_t>(blockIdx.x) * kWaves + wave;
-    const bool have = task < ntasks;
-    const uint32_t tab_pieces = (tab_words + 3) / 4;
-    const auto rtab = buf_rsrc(a.stab, tab_words * 4);
-    uint4 tp[2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i) tp[i] = buf_ld16(rtab, (t + kThreads * i) * 16);
     Task cur{};
     uint4 pre[kLoadRounds];
-    if (have) {
-        cur = task_info<SKIP>(a, task, lane);
-        issue_task_loads(a, cur, lane, pre);
-    }
+    if constexpr (kEarlyLoads) {
+        // the first task's index and input loads go out before the table is
+        // staged (they hide the table copy of the one-shot grid), joined by a
+        // bare barrier: the loads stay in flight across it
+        const bool have = task < ntasks;
+        const uint32_t tab_pieces = (tab_words + 3) / 4;
+        const auto rtab = buf_rsrc(a.stab, tab_words * 4);
+        uint4 tp[2];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
-        if (t + kThreads * i < tab_pieces) st_stage16(lds + 4 * (t + kThreads * i), tp[i]);
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): table stores done; the input loads stay in flight
-    __builtin_amdgcn_s_barrier();
-    if (!have) return;
-#else
-    for (uint32_t i = t; i < tab_words; i += kThreads) lds[i] = reinterpret_cast<const uint32_t*>(a.stab)[i];
-    __syncthreads();
-
-    const uint64_t ntasks = (a.n + kTaskSym - 1) / kTaskSym;
-    const uint64_t step = static_cast<uint64_t>(gridDim.x) * kWaves;
-    uint64_t task = static_cast<uint64_t>(blockIdx.x) * kWaves + wave;
-    if (task >= ntasks) return;
-
-    Task cur = task_info<SKIP>(a, task, lane);
-#endif
+        for (int i = 0; i < 2; ++i) tp[i] = buf_ld16(rtab, (t + kThreads * i) * 16);
+        if (have) {
+            cur = task_info<SKIP>(a, task, lane);
+            issue_task_loads(a, cur, lane, pre);
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+            if (t + kThreads * i < tab_pieces) st_stage16(lds + 4 * (t + kThreads * i), tp[i]);
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): table stores done; the input loads stay in flight
+        __builtin_amdgcn_s_barrier();
+        if (!have) return;
+    } else {
+        for (uint32_t i = t; i < tab_words; i += kThreads) lds[i] = reinterpret_cast<const uint32_t*>(a.stab)[i];
+        __syncthreads();
+        if (task >= ntasks) return;
+        cur = task_info<SKIP>(a, task, lane);
+    }
 
     // no software prefetch of the next task: its 20 registers would cost a
     // wave per SIMD; the other resident waves hide the load latency instead.
@@ -556,10 +399,7 @@ __device__ __forceinline__ void decode_fixed_body(const DecodeArgs& a) {
     //   stage writes (input) -> sync -> lane reads -> sync -> row writes
     //   (output transpose) -> sync -> row reads -> sync -> next task's writes
     while (true) {
-#if !HUFF_DEC_EARLY_LOADS
-        uint4 pre[kLoadRounds];
-        issue_task_loads(a, cur, lane, pre);
-#endif
+        if constexpr (!kEarlyLoads) issue_task_loads(a, cur, lane, pre);
         const uint32_t np = cur.len <= kInCap ? cur.len / 16 : 0u;
 #pragma unroll
         for (uint32_t r = 0; r < kLoadRounds; ++r) {
@@ -622,71 +462,36 @@ __device__ __forceinline__ void decode_fixed_body(const DecodeArgs& a) {
         wave_sync();  // the input stage is reused by the next task
         task = nxt_task;
         cur = task_info<SKIP>(a, task, lane);
-#if HUFF_DEC_EARLY_LOADS
-        issue_task_loads(a, cur, lane, pre);
-#endif
+        if constexpr (kEarlyLoads) issue_task_loads(a, cur, lane, pre);
     }
 }
 
-// Production kernels: the compiler's register allocation (k_decode_fixed 71
-// VGPRs / 7 waves per SIMD, the LDS allows 6), the swizzled-stage variants
-// held to 6 waves (80 VGPRs; 74 without spills); the slow variants 92-112 / 4-5.
+// Production kernels. The register allocation is the compiler's, with one
+// floor for every swizzled-stage (PAD) body, the plain and the index-free skip
+// build alike (kPadWaves waves per SIMD); `make` rejects any build in which a
+// 64-bit shift takes its amount from the last allocated VGPR
+// (tools/check_shift64.py, DESIGN.md §3 "The 64-bit shift hazard"), the
+// hardware hazard behind every wrong-letter build of rounds 1-2.
 template <bool PAD>
-#ifndef HUFF_DEC_PAD_WAVES  // experiments only: the PAD body's minimum waves per SIMD
-#define HUFF_DEC_PAD_WAVES 6
-#endif
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(PAD ? HUFF_DEC_PAD_WAVES : 1, 8))) void k_decode_fixed(DecodeArgs a) {
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(PAD ? kPadWaves : 1, 8))) void k_decode_fixed(DecodeArgs a) {
     decode_fixed_body<false, PAD, false>(a);
 }
 template <bool PAD>
 __global__ __launch_bounds__(kThreads) void k_decode_fixed_slow(DecodeArgs a) { decode_fixed_body<true, PAD, false>(a); }
 
-// Self-checking builds of the same body (HUFF_DEC_VARIANT): 11 = the
-// compiler's allocation; 12 = forced to >= 5 waves per SIMD (the occupancy a
-// round-1 experiment reported wrong letters at); 13 = 8 waves per SIMD (at
-// most 64 VGPRs), so the body spills more to scratch. They exist to prove the decoder's correctness
-// does not depend on register allocation or occupancy (tests/test_gpu_decode_check.py).
+// Self-checking build of the same body (HUFF_DEC_VARIANT=11): every lane's
+// end bit is compared with its successor's restart entry
+// (tests/test_gpu_decode_check.py)
 template <bool SLOW, bool PAD>
 __global__ __launch_bounds__(kThreads) void k_decode_fixed_chk(DecodeArgs a) { decode_fixed_body<SLOW, PAD, true>(a); }
-template <bool SLOW, bool PAD>
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(5, 8))) void k_decode_fixed_chk5(DecodeArgs a) {
-    decode_fixed_body<SLOW, PAD, true>(a);
-}
-template <bool SLOW, bool PAD>
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_decode_fixed_chk_spill(DecodeArgs a) {
-    decode_fixed_body<SLOW, PAD, true>(a);
-}
 // index-free streams with k_mark_lite's entries: each lane first decodes and
 // drops its skip codes
 template <bool SLOW, bool PAD>
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(PAD && !SLOW ? 6 : 1, 8))) void k_decode_fixed_skip(DecodeArgs a) {
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(PAD && !SLOW ? kPadWaves : 1, 8))) void k_decode_fixed_skip(DecodeArgs a) {
     decode_fixed_body<SLOW, PAD, false, true>(a);
-}
-// diagnostics: the production body (no check) forced to >= 5 waves per SIMD
-template <bool SLOW, bool PAD>
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(5, 8))) void k_decode_fixed_w5(DecodeArgs a) {
-    decode_fixed_body<SLOW, PAD, false>(a);
 }
 
 }  // namespace
-
-size_t decode_wave_lds_bytes(uint32_t mlut_bits) {
-    return static_cast<size_t>(1u << mlut_bits) * 4 + static_cast<size_t>(kWaves) * kWaveLds;
-}
-
-hipError_t launch_decode_wave(const DecodeArgs& a, hipStream_t s) {
-    if (a.n == 0) return hipSuccess;
-    const size_t lds = decode_wave_lds_bytes(a.mlut_bits);
-    const uint64_t ntasks = (a.n + kTaskSym - 1) / kTaskSym;
-    const uint32_t per_cu = static_cast<uint32_t>(std::max<size_t>(1, std::min<size_t>(8, (160 * 1024) / lds)));
-    const uint64_t want = (ntasks + kWaves - 1) / kWaves;
-    const uint32_t grid = static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>(want, uint64_t(a.cu_count ? a.cu_count : 256) * per_cu)));
-    if (a.max_len > a.mlut_bits)
-        hipLaunchKernelGGL(k_decode_wave<true>, dim3(grid), dim3(kThreads), lds, s, a);
-    else
-        hipLaunchKernelGGL(k_decode_wave<false>, dim3(grid), dim3(kThreads), lds, s, a);
-    return hipGetLastError();
-}
 
 }  // namespace huff::dev
 
@@ -705,43 +510,31 @@ hipError_t launch_decode_fixed(const DecodeArgs& a, hipStream_t s) {
     const bool pad = a.pad_stage != 0;
     using K = void (*)(DecodeArgs);
     // [check mode][slow][pad]
-    static const K table[5][2][2] = {
+    static const K table[2][2][2] = {
         {{k_decode_fixed<false>, k_decode_fixed<true>}, {k_decode_fixed_slow<false>, k_decode_fixed_slow<true>}},
         {{k_decode_fixed_chk<false, false>, k_decode_fixed_chk<false, true>},
          {k_decode_fixed_chk<true, false>, k_decode_fixed_chk<true, true>}},
-        {{k_decode_fixed_chk5<false, false>, k_decode_fixed_chk5<false, true>},
-         {k_decode_fixed_chk5<true, false>, k_decode_fixed_chk5<true, true>}},
-        {{k_decode_fixed_chk_spill<false, false>, k_decode_fixed_chk_spill<false, true>},
-         {k_decode_fixed_chk_spill<true, false>, k_decode_fixed_chk_spill<true, true>}},
-        {{k_decode_fixed_w5<false, false>, k_decode_fixed_w5<false, true>},
-         {k_decode_fixed_w5<true, false>, k_decode_fixed_w5<true, true>}},
     };
     static const K skip_table[2][2] = {{k_decode_fixed_skip<false, false>, k_decode_fixed_skip<false, true>},
                                        {k_decode_fixed_skip<true, false>, k_decode_fixed_skip<true, true>}};
-    if (a.check_mode > 4 || (a.check_mode && !a.err)) return hipErrorInvalidValue;
+    if (a.check_mode > 1 || (a.check_mode && !a.err)) return hipErrorInvalidValue;
     if (a.skip_packed && (a.check_mode || !a.sub_abs64)) return hipErrorInvalidValue;
     K kern = a.skip_packed ? skip_table[slow][pad] : table[a.check_mode][slow][pad];
     // persistent grid = resident workgroups (registers and LDS both limit)
     int per_cu = 0;
     hipError_t err = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kThreads, lds);
     if (err != hipSuccess || per_cu < 1) per_cu = 1;
-    if (a.check_mode)  // diagnostics of the check builds: HUFF_DEC_GRID caps the persistent grid
-        if (const char* g = std::getenv("HUFF_DEC_GRID")) per_cu = -std::max(1, std::atoi(g));
     const uint64_t want = (ntasks + kWaves - 1) / kWaves;
-    uint64_t cap = per_cu < 0 ? uint64_t(-per_cu) : uint64_t(a.cu_count ? a.cu_count : 256) * per_cu;
+    uint64_t cap = uint64_t(a.cu_count ? a.cu_count : 256) * per_cu;
     // production: one task per wave (a one-shot grid, as the byte map's): the
     // dispatcher refills the CUs as waves finish — same-box A/B against the
     // resident persistent grid Zipf 0.506 -> 0.501 ms, text 0.433 -> 0.423,
     // index-free text 1.18 -> 1.14 ms. HUFF_DEC_ONESHOT=0 restores the
-    // persistent grid; the check builds keep it (HUFF_DEC_GRID caps it).
+    // persistent grid; the check build keeps it.
     const char* o = std::getenv("HUFF_DEC_ONESHOT");
     if (!a.check_mode && !(o && *o == '0')) cap = want;
     const uint32_t grid = static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>(want, cap)));
-    // diagnostics (wrong-letter reproducer): HUFF_DEC_LDS_EXTRA bytes of unused
-    // dynamic LDS cap the workgroups per CU without changing the code object
-    size_t lds_launch = lds;
-    if (const char* x = std::getenv("HUFF_DEC_LDS_EXTRA")) lds_launch += static_cast<size_t>(std::max(0, std::atoi(x)));
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), lds_launch, s, a);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), lds, s, a);
     return hipGetLastError();
 }
 

@@ -19,7 +19,7 @@ namespace huff::dev {
 
 constexpr uint32_t kChunk = 65536;      // input bytes (= symbols) per chunk / workgroup
 constexpr uint32_t kRound = 4096;       // bytes per workgroup round (256 lanes x 16 B)
-constexpr uint32_t kSub = 256;          // symbols per lane of the chunk decoders (decode.hip, decode_ring.hip)
+constexpr uint32_t kSub = 256;          // symbols per lane of the long-code chunk decoder (decode.hip)
 constexpr uint32_t kIdx = 64;           // restart index stride of the byte path (sub_bit): symbols
 constexpr uint32_t kShortMaxLen = 27;   // u32 table entries: code << (32 - len) | len
 constexpr uint32_t kLongMaxLen = 57;    // u64 table entries: code << 6 | len
@@ -81,15 +81,11 @@ struct DecodeArgs {
     const uint32_t* sub_bit;      // [ceil(n / kIdx)]
     uint32_t nchunks;
     uint32_t max_len;             // longest code (> 32: window slow path)
-    uint32_t lut_rep_log2;        // primary table copies in LDS (bank spread)
     const uint64_t* sub_abs;      // non-null: absolute start bit of every 256-symbol run
                                   // (index-free decode), instead of chunk_start + sub_bit
-    const uint32_t* mlut;         // multi-symbol table [1 << mlut_bits] (null: none)
-    uint32_t mlut_bits;
     const uint16_t* stab;         // single-symbol table [1 << stab_bits] (k_decode_fixed)
     uint32_t stab_bits;
-    uint32_t variant;             // kDecodeFixed, kDecodeWave, kDecodeRing or kDecodeSingle (codes <= 32 bits)
-    uint32_t cu_count;            // persistent grid of k_decode_wave
+    uint32_t cu_count;            // persistent grid of the checked k_decode_fixed
     uint64_t n;
     uint8_t* out;
     // k_decode_fixed on an index-free stream: absolute start bit of every
@@ -97,7 +93,7 @@ struct DecodeArgs {
     const uint64_t* sub_abs64;
     uint64_t end_bit;
     // the compact restart index (PackArgs::sub16 / task_base), instead of
-    // chunk_start + sub_bit (k_decode_fixed, k_decode_wave)
+    // chunk_start + sub_bit (k_decode_fixed)
     const uint16_t* sub16;
     const uint64_t* task_base;
     // sub_abs64 entries as k_mark_lite writes them: a boundary at or before
@@ -108,9 +104,8 @@ struct DecodeArgs {
     // where the lanes' streams start ~32 m / k dwords apart every refill
     // would hit the same few LDS banks
     uint32_t pad_stage;
-    // k_decode_fixed self-check builds (0: production kernel; 1: checked;
-    // 2: checked, >= 5 waves per SIMD forced; 3: checked, 8 waves per
-    // SIMD forced). err: u32[8] mismatch count + first (task, lane, want, got)
+    // k_decode_fixed self-check build (0: production kernel; 1: checked).
+    // err: u32[8] mismatch count + first (task, lane, want, got)
     uint32_t check_mode;
     uint32_t* err;
 };
@@ -273,14 +268,11 @@ hipError_t launch_decode_deep_serial(const DeepSerialArgs& a, hipStream_t s);
 
 size_t pack_lds_bytes(bool long_codes, uint32_t max_len, uint32_t stage_words);
 uint32_t pack_waves_per_group(bool long_codes);
-size_t decode_lds_bytes(uint32_t lut_bits, uint32_t rep_log2);
-constexpr uint32_t kDecodeSingle = 1;  // decode.hip k_decode_short
-constexpr uint32_t kDecodeRing = 7;    // decode_ring.hip k_decode_ring
-constexpr uint32_t kDecodeWave = 9;    // decode_wave.hip k_decode_wave (codes <= 32 bits)
-constexpr uint32_t kDecodeFixed = 10;  // decode_wave.hip k_decode_fixed (codes <= 32 bits)
-constexpr uint32_t kDecodeFixedCheck = 11;       // k_decode_fixed with the lane-end self-check
-constexpr uint32_t kDecodeFixedCheck5 = 12;      //  ... forced to >= 5 waves per SIMD
-constexpr uint32_t kDecodeFixedCheckSpill = 13;  //  ... forced to 8 waves per SIMD (spills)
+size_t decode_lds_bytes(uint32_t lut_bits);
+// HUFF_DEC_VARIANT: 10 = k_decode_fixed (the default for codes <= 32 bits),
+// 11 = its self-checking build
+constexpr uint32_t kDecodeFixed = 10;
+constexpr uint32_t kDecodeFixedCheck = 11;
 
 // Pass 1's totals straight to pinned host memory (device-visible pointer):
 // host[b] = (tag << 48) | total_b. host == nullptr: the totals stay in gw.
@@ -314,11 +306,7 @@ hipError_t launch_scan(const uint64_t* bits, uint32_t nchunks, uint64_t base, ui
                        hipStream_t s);
 hipError_t launch_pack(bool long_codes, const PackArgs& a, hipStream_t s);
 hipError_t launch_decode(const DecodeArgs& a, hipStream_t s);
-hipError_t launch_decode_ring(const DecodeArgs& a, hipStream_t s);
-size_t decode_ring_lds_bytes(uint32_t mlut_bits);
-hipError_t launch_decode_wave(const DecodeArgs& a, hipStream_t s);
 hipError_t launch_decode_fixed(const DecodeArgs& a, hipStream_t s);
-size_t decode_wave_lds_bytes(uint32_t mlut_bits);
 hipError_t launch_indexless_spec(const IndexlessArgs& a, hipStream_t s);
 // kFixRounds fix-up rounds (each a no-op once the previous one changed
 // nothing), then the sequential sweep only if the last round still changed an

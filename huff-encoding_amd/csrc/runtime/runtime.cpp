@@ -62,12 +62,9 @@ bool fixed8_disabled() {
 uint32_t decode_check_mode() {
     const char* e = std::getenv("HUFF_DEC_VARIANT");  // read per call: tests flip it
     if (!e) return 0;
-    const int v = std::atoi(e);
-    if (v == static_cast<int>(dev::kDecodeFixedCheck)) return 1;
-    if (v == static_cast<int>(dev::kDecodeFixedCheck5)) return 2;
-    if (v == static_cast<int>(dev::kDecodeFixedCheckSpill)) return 3;
-    if (v == 14) return 4;  // diagnostics: the unchecked body forced to >= 5 waves per SIMD
-    return 0;
+    // 11: k_decode_fixed's self-checking build; every other value is the
+    // production decoder (the round-2 diagnostics 12-14 are not in the library)
+    return std::atoi(e) == static_cast<int>(dev::kDecodeFixedCheck) ? 1u : 0u;
 }
 
 // a checked k_decode_fixed launch: zero the mismatch record before, read it
@@ -677,48 +674,31 @@ huff::Status huff_enc::decode(const huff_tree* t, const uint8_t* d_comp, uint64_
     a.sub_bit = static_cast<const uint32_t*>(sub_bit.p);
     a.nchunks = nchunks;
     a.max_len = dt->maxdepth;
-    // single-symbol kernel: primary table replicated up to 4 KiB of LDS
-    // (fewer bank conflicts, occupancy kept)
-    a.lut_rep_log2 = static_cast<uint32_t>(std::max(0, std::min(5, 10 - static_cast<int>(dt->bits))));
-    // kernel choice: the fixed-count single-symbol decoder (decode_wave.hip,
-    // k_decode_fixed) for every tree with codes <= 32 bits. 1 GiB, ms:
-    //                 fixed  wave(multi-symbol)  ring  single
-    //   Zipf(1.2)     0.59   0.73                1.10  -
-    //   text          0.56   0.61                0.90  -
-    //   8-bit codes   0.74   1.06                -     0.94
-    // HUFF_DEC_VARIANT=1|7|9|10 forces one (tests, measurements).
-    // HUFF_DEC_VARIANT=11|12|13: k_decode_fixed's self-checking builds
-    a.variant = huff::dev::kDecodeFixed;
+    // codes <= 32 bits: the fixed-count decoder (decode_wave.hip,
+    // k_decode_fixed; the round-1 ring, multi-symbol and single-symbol
+    // decoders were 1.2-1.9x slower and are retired); HUFF_DEC_VARIANT=11
+    // runs its self-checking build. Longer codes: k_decode<LONG> (decode.hip).
     a.check_mode = huff::decode_check_mode();
-    if (const char* env = std::getenv("HUFF_DEC_VARIANT")) {
-        const int v = std::atoi(env);
-        if (v == static_cast<int>(huff::dev::kDecodeRing) || v == static_cast<int>(huff::dev::kDecodeSingle) ||
-            v == static_cast<int>(huff::dev::kDecodeWave) || v == static_cast<int>(huff::dev::kDecodeFixed))
-            a.variant = static_cast<uint32_t>(v);
-    }
-    // the wave decoders store 16-B pieces: a misaligned output (e.g. a tensor
+    // the task decoder stores 16-B pieces: a misaligned output (e.g. a tensor
     // view at an odd offset) is decoded into an aligned buffer of the context
-    // and copied on the stream (one extra n-byte copy, against 1.5-2x for the
-    // older unaligned-capable decoders)
+    // and copied on the stream
     uint8_t* dst = d_out;
-    if (compact_index) {  // the task decoders read it as is; the others get sub_bit
-        if (a.variant == huff::dev::kDecodeWave || a.variant == huff::dev::kDecodeFixed) {
+    const bool fixed = dt->maxdepth <= 32;
+    if (compact_index) {  // the task decoder reads it as is; k_decode<LONG> gets sub_bit
+        if (fixed) {
             a.sub16 = static_cast<const uint16_t*>(sub16.p);
             a.task_base = static_cast<const uint64_t*>(task_base.p);
         } else {
             HUFF_TRY(expand_index());
         }
     }
-    const bool bounce = (a.variant == huff::dev::kDecodeWave || a.variant == huff::dev::kDecodeFixed) &&
-                        (reinterpret_cast<uintptr_t>(d_out) & 15);
+    const bool bounce = fixed && (reinterpret_cast<uintptr_t>(d_out) & 15);
     if (bounce) {
         HUFF_TRY(ctx->d_align.ensure(n + 64));
         dst = static_cast<uint8_t*>(ctx->d_align.p);
     }
     a.cu_count = static_cast<uint32_t>(ctx->cu_count);
     a.pad_stage = huff::dev::fixed_decode_pad(total_bits, n);
-    a.mlut = static_cast<const uint32_t*>(ctx->d_lut.p) + dt->moff;
-    a.mlut_bits = dt->mbits;
     a.stab = reinterpret_cast<const uint16_t*>(static_cast<const uint32_t*>(ctx->d_lut.p) + dt->soff);
     a.stab_bits = dt->sbits;
     a.n = n;
@@ -1129,7 +1109,7 @@ Status decode_indexless_dev(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_
         // a restart point every 64 symbols, then the fixed-count decoder
         // (k_mark_lite: a boundary and the codes to skip from it, the
         // decoder's lanes walk those codes themselves; the self-check builds,
-        // HUFF_DEC_VARIANT 11-13, need exact lane starts: k_mark_lds walks)
+        // HUFF_DEC_VARIANT=11, needs exact lane starts: k_mark_lds walks)
         DevBuf& sub_abs = ctx->idx_sub_abs;
         const uint32_t check = decode_check_mode();
         if (check) {

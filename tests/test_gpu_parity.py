@@ -280,11 +280,12 @@ def _device_gen(H, ctx, kind, seed, n):
     return x
 
 
-@pytest.mark.parametrize("dec", ["auto", "1", "7", "9", "10"], ids=["dec-auto", "dec-single", "dec-ring", "dec-wave", "dec-fixed"])
+@pytest.mark.parametrize("dec", ["auto", "10", "11"], ids=["dec-auto", "dec-fixed", "dec-checked"])
 @pytest.mark.parametrize("kind,seed", [("uniform", 0x5EED0001), ("zipf", 0x5EED0002), ("text", 0x5EED0005)])
 def test_device_job_medium(H, O, ctx, kind, seed, dec, monkeypatch):
     """16 MiB + ragged tail of each workload; decode through the kernel the
-    runtime picks and through each decode kernel forced (HUFF_DEC_VARIANT)"""
+    runtime picks, the general decoder forced (HUFF_DEC_VARIANT=10 with the
+    byte map off) and its self-checking build (11)"""
     import torch
 
     forced = dec != "auto"
@@ -355,10 +356,10 @@ def test_indexfree_misaligned_output(H, O, ctx):
     assert got == n and torch.equal(out[:n], x[:n])
 
 
-@pytest.mark.parametrize("dec", ["auto", "1", "7", "9", "10"], ids=["dec-auto", "dec-single", "dec-ring", "dec-wave", "dec-fixed"])
+@pytest.mark.parametrize("dec", ["auto", "11"], ids=["dec-auto", "dec-checked"])
 def test_device_job_long_tail_codes(H, O, ctx, dec, monkeypatch):
     """geometric bytes: codes from 1 to > 12 bits (the multi-symbol table's
-    slow path); each decode kernel forced"""
+    slow path); production and the self-checking build"""
     import torch
 
     if dec != "auto":
@@ -765,7 +766,7 @@ def test_bytemap_pack_then_bit_decoder(H, O, ctx, monkeypatch):
         tree, bits = job.compress(out.data_ptr(), out.numel())
         assert bits == 8 * n
         monkeypatch.setenv("HUFF_DISABLE_FIXED8", "1")
-        for var in ("10", "1", "7"):
+        for var in ("10", "11"):
             monkeypatch.setenv("HUFF_DEC_VARIANT", var)
             dec = torch.zeros(n + 64, dtype=torch.uint8, device="cuda")
             job.decode(tree, out.data_ptr(), dec.data_ptr())

@@ -1,0 +1,19 @@
+#!/usr/bin/env bash
+# Round 3, first GPU pass: full GPU suite + smoke on the cleaned library
+# (retired decoders, shift64-checked build, early-loads prologue), then a
+# same-box interleaved decode A/B against lib/ab (round-2 prologue).
+set -uo pipefail
+root=${GRAFT_REPO_ROOT:-$(pwd)}
+out=$root/gpurun_out/${1:-r3a}; mkdir -p $out
+cd $root
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread > $out/gpu_tests.log 2>&1 || { tail -30 $out/gpu_tests.log; exit 1; }
+tail -2 $out/gpu_tests.log
+timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $out/smoke.log 2>&1 || { tail -20 $out/smoke.log; exit 1; }
+tail -1 $out/smoke.log
+for rep in 1 2; do for w in zipf text; do for v in new ab; do
+  if [ $v = new ]; then unset HUFF_LIB_AB; else export HUFF_LIB_AB=ab; fi
+  timeout -k 10 120 python tools/kbench.py --phase decode --workload $w --iters 20 > $out/dec_${w}_${v}_$rep.json 2>>$out/err.log || exit 1
+  timeout -k 10 120 python tools/kbench.py --phase indexless --workload $w --iters 10 > $out/idx_${w}_${v}_$rep.json 2>>$out/err.log || exit 1
+done; done; done
+unset HUFF_LIB_AB
+echo "r3a done"
