@@ -478,11 +478,21 @@ int huff_dev_calibrate(huff_ctx* ctx, const uint8_t* d_src, uint8_t* d_dst, size
     return guarded([&]() -> huff::Status {
         HUFF_TRY(ctx->activate());
         const uint64_t m = n & ~uint64_t(15);
-        hipEvent_t a, b;
-        HIP_TRY_RT(hipEventCreate(&a));
-        HIP_TRY_RT(hipEventCreate(&b));
-        unsigned* sink = nullptr;
-        HIP_TRY_RT(hipMalloc(&sink, 16));
+        // events and the sink released on every path (RAII)
+        struct Res {
+            hipEvent_t a = nullptr, b = nullptr;
+            unsigned* sink = nullptr;
+            ~Res() {
+                if (sink) hipFree(sink);
+                if (a) hipEventDestroy(a);
+                if (b) hipEventDestroy(b);
+            }
+        } r;
+        HIP_TRY_RT(hipEventCreate(&r.a));
+        HIP_TRY_RT(hipEventCreate(&r.b));
+        HIP_TRY_RT(hipMalloc(&r.sink, 16));
+        hipEvent_t a = r.a, b = r.b;
+        unsigned* sink = r.sink;
         float best[2] = {1e30f, 1e30f};  // [read, copy] over the two shapes of each
         hipError_t er = hipSuccess;
         for (int mode = 0; mode < 4 && er == hipSuccess; ++mode)
@@ -495,9 +505,6 @@ int huff_dev_calibrate(huff_ctx* ctx, const uint8_t* d_src, uint8_t* d_dst, size
                 hipEventElapsedTime(&ms, a, b);
                 if (it) best[mode / 2] = std::min(best[mode / 2], ms);
             }
-        hipFree(sink);
-        hipEventDestroy(a);
-        hipEventDestroy(b);
         if (er != hipSuccess) return huff::Status::err(HUFF_E_HIP, hipGetErrorString(er));
         *read_gbps = static_cast<double>(m) / (best[0] * 1e-3) / 1e9;
         *copy_gbps = 2.0 * static_cast<double>(m) / (best[1] * 1e-3) / 1e9;

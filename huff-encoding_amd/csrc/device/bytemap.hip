@@ -72,7 +72,8 @@ __global__ __launch_bounds__(kThreads) void k_bytemap(BytemapArgs a) {
         for (uint64_t i = nvec * 16 + t; i < a.n; i += kThreads) a.dst[i] = static_cast<uint8_t>(tab[(a.src[i] << 5) | copy]);
     // restart index of an 8-bit-per-symbol stream
     if (a.chunk_start)
-        for (uint64_t c = gid; c <= a.nchunks; c += stride) a.chunk_start[c] = a.base_bits + c * kChunk * 8;
+        for (uint64_t c = gid; c <= a.nchunks; c += stride)
+            a.chunk_start[c] = a.base_bits + (c * kChunk < a.n ? c * kChunk : a.n) * 8;
     if (a.sub_bit) {
         const uint64_t nsub = (a.n + kIdx - 1) / kIdx;
         for (uint64_t g = gid; g < nsub; g += stride) a.sub_bit[g] = static_cast<uint32_t>(((g * kIdx) % kChunk) * 8);
@@ -83,7 +84,9 @@ __global__ __launch_bounds__(256) void k_arith_index(uint64_t n, uint32_t nchunk
                                                      uint64_t* __restrict__ chunk_start, uint32_t* __restrict__ sub_bit) {
     const uint64_t gid = static_cast<uint64_t>(blockIdx.x) * 256 + threadIdx.x;
     const uint64_t stride = static_cast<uint64_t>(gridDim.x) * 256;
-    for (uint64_t c = gid; c <= nchunks; c += stride) chunk_start[c] = base_bits + c * kChunk * 8;
+    // the last entry is the stream's end (n symbols), as the bit pack writes it
+    for (uint64_t c = gid; c <= nchunks; c += stride)
+        chunk_start[c] = base_bits + (c * kChunk < n ? c * kChunk : n) * 8;
     const uint64_t nsub = (n + kIdx - 1) / kIdx;
     for (uint64_t g = gid; g < nsub; g += stride) sub_bit[g] = static_cast<uint32_t>(((g * kIdx) % kChunk) * 8);
 }

@@ -160,6 +160,36 @@ struct IndexlessArgs {
     // (null: single steps from stab only)
     const uint16_t* wtab;
 };
+// single-pass index-free decode (ifdec.hip)
+constexpr uint32_t kIfdPrefixCap = 32;  // letters a lane's fix-up walk keeps before it gives up (slow lane)
+struct IfdArgs {
+    const uint8_t* comp;          // stream; bit 0 = MSB of comp[0]
+    uint64_t comp_bytes;
+    uint64_t valid_bits;          // B
+    uint32_t seg_bits;            // S (multiple of the gcd of the code lengths)
+    uint64_t nseg;
+    uint32_t nblocks;             // ifd_blocks(nseg) workgroups
+    const uint16_t* stab;         // single-symbol table (k_decode_fixed's)
+    uint32_t stab_bits;
+    const uint32_t* lut;          // multi-level table (codes longer than stab_bits)
+    uint32_t lut_bits;
+    uint32_t max_len;             // <= 32
+    uint8_t* out;                 // 16-B aligned
+    uint64_t out_cap;
+    unsigned long long* status;   // [nblocks] look-back words, zeroed
+    unsigned long long* exits;    // [nblocks] a block's true exit + 1 (for a repair of the next block's anchor)
+    unsigned int* ticket;         // zeroed
+    unsigned int* flags;          // zeroed; 2: out_cap too small, 4: the look-back gave up
+    unsigned long long* total;    // letters
+    unsigned long long* end_bit;  // may be null: the bit after the last complete code
+    // LDS layout (ifd_layout)
+    uint32_t stage_off, stage_bytes, qm_off, pf_off, ex_off, cnt_off, misc_off, out_off, out_img;
+};
+IfdArgs ifd_layout(uint32_t stab_bits, uint32_t seg_bits, uint32_t max_len);  // LDS fields only
+uint32_t ifd_blocks(uint64_t nseg);
+size_t ifd_lds_bytes(const IfdArgs& a);
+hipError_t launch_ifd(const IfdArgs& a, hipStream_t s);
+
 constexpr uint32_t kSampBits = 128;
 constexpr uint32_t kSampMax = 8;  // samples kept per segment (nsamp <= kSampMax)
 constexpr uint32_t kNoMerge = 0xFFFFFFFFu;
@@ -228,10 +258,23 @@ inline size_t wide_table_lds_bytes(uint32_t width, uint32_t log2_slots, bool val
 hipError_t launch_wide_bits(const WideArgs& a, hipStream_t s);
 hipError_t launch_wide_pack(const WideArgs& a, hipStream_t s);
 hipError_t launch_wide_decode(const WideDecArgs& a, hipStream_t s);
-// build_weights_map on the device (wweights.hip): sorted distinct letters and
-// their counts. d_tmp == nullptr: *tmp_bytes = scratch needed.
-hipError_t wide_weights(uint32_t width, const void* d_in, uint64_t n, void* d_sorted, void* d_uniq,
-                        uint64_t* d_counts, uint64_t* d_nruns, void* d_tmp, size_t* tmp_bytes, hipStream_t s);
+// build_weights_map on the device (wweights.hip). width <= 2: counts = the
+// 2^(8 width) bins (zeroed). width >= 4: an HBM table of `slots`
+// (wcount_slots) keys_lo (all ones), counts (zero), width 16 also keys_hi and
+// state (zero); the used slots are appended to out_lo / out_hi / out_c
+// (capacity min(n, slots)), their number to *nout (zero), the all-ones u64
+// letter's count to *sent (zero; width 8).
+struct WCountArgs {
+    const uint8_t* in;  // n letters, 4-B aligned (width >= 4: width-aligned)
+    uint64_t n;
+    uint32_t width;
+    uint64_t slots;
+    unsigned long long *keys_lo, *keys_hi, *counts, *sent;
+    unsigned int* state;
+    unsigned long long *out_lo, *out_hi, *out_c, *nout;
+};
+uint64_t wcount_slots(uint32_t width, uint64_t n);
+hipError_t wcount_launch(const WCountArgs& a, hipStream_t s);
 
 // codes longer than kLongMaxLen (deep.hip): up to 255 bits, kDeepWords
 // left-aligned words per letter

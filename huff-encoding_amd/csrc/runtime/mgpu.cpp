@@ -5,7 +5,8 @@
 // a unique id on rank 0 (huff_comm_unique_id), hands its 128 bytes to every
 // rank over any channel it has (MPI, TCP, a file), and each rank joins with
 // huff_comm_init. huff_mgpu_compress then runs the whole sharded encode of
-// the rank's job in one call:
+// the rank's job in one call (huff_mgpu_pack_rows is its host half, for
+// callers that exchange the rows over their own channel):
 //
 //   pass 1 (hist256 + row kernel)  -> ncclAllGather of a 258 x int64 row per
 //   rank on the context stream     -> one device-to-host copy, ONE host wait
@@ -21,6 +22,7 @@
 #include <rccl/rccl.h>
 
 #include <cstring>
+#include <string>
 #include <memory>
 #include <vector>
 
@@ -97,43 +99,77 @@ int huff_comm_world(const huff_comm* c, int* world, int* rank) {
     return HUFF_OK;
 }
 
-int huff_mgpu_compress(huff_comm* c, huff_enc* e, uint8_t* d_out, size_t out_cap, huff_tree** tree_out,
-                       uint64_t* bit_base_out, uint64_t* bits_out, uint64_t* owned_bytes_out) {
-    if (!c || !e || !d_out || !tree_out || e->ctx != c->ctx)
-        return fail(HUFF_E_INVALID_ARG, "null argument, or a job of another context");
+int huff_mgpu_pack_rows(huff_enc* e, const int64_t* rows, int world, int rank, uint8_t* d_out, size_t out_cap,
+                        huff_tree** tree_out, uint64_t* bit_base_out, uint64_t* bits_out,
+                        uint64_t* owned_bytes_out) {
+    if (!e || !rows || !d_out || !tree_out || world < 1 || rank < 0 || rank >= world)
+        return fail(HUFF_E_INVALID_ARG, "null or out-of-range argument");
     if (reinterpret_cast<uintptr_t>(d_out) & 15) return fail(HUFF_E_INVALID_ARG, "d_out must be 16-byte aligned");
     *tree_out = nullptr;
     return guarded([&]() -> huff::Status {
-        huff_ctx* ctx = c->ctx;
-        HUFF_TRY(ctx->activate());
-        const size_t world = static_cast<size_t>(c->world);
-        // pass 1 + the row, then the collective, in stream order
-        HUFF_TRY(e->hist_row(static_cast<long long*>(c->row.p)));
-        NCCL_TRY(ncclAllGather(c->row.p, c->rows.p, kRowWords, ncclInt64, c->comm, ctx->stream));
-        HIP_TRY_RT(hipMemcpyAsync(c->host_rows.p, c->rows.p, kRowWords * 8 * world, hipMemcpyDeviceToHost,
-                                  ctx->stream));
-        HUFF_TRY(ctx->sync());
-        const int64_t* rows = static_cast<const int64_t*>(c->host_rows.p);
-        std::vector<uint64_t> hists(world * 256);
-        std::vector<uint8_t> tails(world * 8), tail_lens(world);
-        for (size_t q = 0; q < world; ++q) {
+        const size_t W = static_cast<size_t>(world);
+        std::vector<uint64_t> hists(W * 256);
+        std::vector<uint8_t> tails(W * 8), tail_lens(W);
+        for (size_t q = 0; q < W; ++q) {
+            const int64_t tl = rows[q * kRowWords + 257];
+            if (tl < 0) return huff::Status::err(HUFF_E_INVALID_ARG, "rank " + std::to_string(q) +
+                                                 " failed before the exchange");
+            if (tl > 8) return huff::Status::err(HUFF_E_INVALID_ARG, "malformed row: tail count > 8");
             std::memcpy(&hists[q * 256], rows + q * kRowWords, 256 * 8);
             std::memcpy(&tails[q * 8], rows + q * kRowWords + 256, 8);  // little-endian: stream order
-            tail_lens[q] = static_cast<uint8_t>(rows[q * kRowWords + 257]);
+            tail_lens[q] = static_cast<uint8_t>(tl);
         }
         uint64_t base = 0, bits = 0;
         huff_tree* t = nullptr;
-        const int rc = huff_enc_pack_shards(e, hists.data(), static_cast<uint32_t>(world),
-                                            static_cast<uint32_t>(c->rank), tails.data(), tail_lens.data(), d_out,
-                                            out_cap, &t, &base, &bits);
+        const int rc = huff_enc_pack_shards(e, hists.data(), static_cast<uint32_t>(world), static_cast<uint32_t>(rank),
+                                            tails.data(), tail_lens.data(), d_out, out_cap, &t, &base, &bits);
         if (bit_base_out) *bit_base_out = base;
         if (bits_out) *bits_out = bits;
         if (rc != HUFF_OK) return huff::Status::err(rc, huff::capi::last_error());
         // the rank owns its first (shared) byte and leaves its partial last
         // byte to the next rank, except the last rank (mgpu.owned_bytes)
         const uint64_t end = (base & 7) + bits;
-        if (owned_bytes_out) *owned_bytes_out = c->rank + 1 == c->world ? (end + 7) / 8 : end / 8;
+        if (owned_bytes_out) *owned_bytes_out = rank + 1 == world ? (end + 7) / 8 : end / 8;
         *tree_out = t;
+        return huff::Status::ok();
+    });
+}
+
+int huff_mgpu_compress(huff_comm* c, huff_enc* e, uint8_t* d_out, size_t out_cap, huff_tree** tree_out,
+                       uint64_t* bit_base_out, uint64_t* bits_out, uint64_t* owned_bytes_out) {
+    if (!c) return fail(HUFF_E_INVALID_ARG, "null communicator");
+    if (tree_out) *tree_out = nullptr;
+    // A rank that cannot run its pass 1 still takes part in the collective,
+    // with a row that marks it failed (tail count -1): every rank then
+    // returns an error instead of the others blocking in ncclAllGather.
+    std::string local;
+    if (!e || !d_out || !tree_out) local = "null argument";
+    else if (e->ctx != c->ctx) local = "a job of another context";
+    else if (reinterpret_cast<uintptr_t>(d_out) & 15) local = "d_out must be 16-byte aligned";
+    return guarded([&]() -> huff::Status {
+        huff_ctx* ctx = c->ctx;
+        HUFF_TRY(ctx->activate());
+        const size_t world = static_cast<size_t>(c->world);
+        if (local.empty()) {
+            const huff::Status st = e->hist_row(static_cast<long long*>(c->row.p));
+            if (st) local = st.msg;
+        }
+        if (!local.empty()) {
+            static const std::vector<int64_t> bad = [] {
+                std::vector<int64_t> r(kRowWords, 0);
+                r[257] = -1;
+                return r;
+            }();
+            HIP_TRY_RT(hipMemcpyAsync(c->row.p, bad.data(), kRowWords * 8, hipMemcpyHostToDevice, ctx->stream));
+        }
+        NCCL_TRY(ncclAllGather(c->row.p, c->rows.p, kRowWords, ncclInt64, c->comm, ctx->stream));
+        HIP_TRY_RT(hipMemcpyAsync(c->host_rows.p, c->rows.p, kRowWords * 8 * world, hipMemcpyDeviceToHost,
+                                  ctx->stream));
+        HUFF_TRY(ctx->sync());
+        if (!local.empty()) return huff::Status::err(HUFF_E_INVALID_ARG, local);
+        const int rc = huff_mgpu_pack_rows(e, static_cast<const int64_t*>(c->host_rows.p), c->world, c->rank, d_out,
+                                           out_cap, tree_out, bit_base_out, bits_out, owned_bytes_out);
+        if (rc != HUFF_OK) return huff::Status::err(rc, huff::capi::last_error());
         return huff::Status::ok();
     });
 }

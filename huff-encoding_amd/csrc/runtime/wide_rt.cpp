@@ -208,6 +208,8 @@ namespace huff {
 
 Status wweights_map_host(huff_ctx* ctx, uint32_t width, const uint8_t* letters, size_t n,
                          std::vector<uint8_t>& uniq, std::vector<uint64_t>& counts) {
+    // build_weights_map (weights.rs:82-123) on the device (wweights.hip),
+    // distinct letters in ascending order
     uniq.clear();
     counts.clear();
     if (!valid_width(width)) return Status::err(HUFF_E_INVALID_ARG, "letter width must be 1, 2, 4, 8 or 16 bytes");
@@ -217,26 +219,69 @@ Status wweights_map_host(huff_ctx* ctx, uint32_t width, const uint8_t* letters, 
     const size_t nb = n * width;
     HUFF_TRY(ctx->d_in.ensure(nb + 16));
     HIP_TRY(hipMemcpyAsync(ctx->d_in.p, letters, nb, hipMemcpyHostToDevice, s));
-    DevBuf sorted, du, dc, dn, tmp;
-    size_t tmp_bytes = 0;
-    HIP_TRY(dev::wide_weights(width, ctx->d_in.p, n, nullptr, nullptr, nullptr, nullptr, nullptr, &tmp_bytes, s));
-    HUFF_TRY(sorted.ensure(nb + 16));
-    HUFF_TRY(du.ensure(nb + 16));
-    HUFF_TRY(dc.ensure(n * 8 + 8));
-    HUFF_TRY(dn.ensure(8));
-    HUFF_TRY(tmp.ensure(tmp_bytes + 16));
-    HUFF_TRY(ctx->timed("wweights", [&] {
-        return dev::wide_weights(width, ctx->d_in.p, n, sorted.p, du.p, static_cast<uint64_t*>(dc.p),
-                                 static_cast<uint64_t*>(dn.p), tmp.p, &tmp_bytes, s);
-    }));
-    uint64_t runs = 0;
-    HIP_TRY(hipMemcpyAsync(&runs, dn.p, 8, hipMemcpyDeviceToHost, s));
+    dev::WCountArgs a{};
+    a.in = static_cast<const uint8_t*>(ctx->d_in.p);
+    a.n = n;
+    a.width = width;
+    a.slots = dev::wcount_slots(width, n);
+    DevBuf cnt, klo, khi, state, olo, ohi, oc, misc;
+    HUFF_TRY(cnt.ensure(a.slots * 8));
+    HIP_TRY(hipMemsetAsync(cnt.p, 0, a.slots * 8, s));
+    a.counts = static_cast<unsigned long long*>(cnt.p);
+    auto put = [&](uint64_t lo, uint64_t hi, uint64_t c) {
+        for (uint32_t j = 0; j < width; ++j) uniq.push_back(static_cast<uint8_t>(j < 8 ? lo >> (8 * j) : hi >> (8 * (j - 8))));
+        counts.push_back(c);
+    };
+    if (width <= 2) {  // direct bins: ascending by construction
+        HUFF_TRY(ctx->timed("wweights", [&] { return dev::wcount_launch(a, s); }));
+        std::vector<uint64_t> bins(a.slots);
+        HIP_TRY(hipMemcpyAsync(bins.data(), cnt.p, a.slots * 8, hipMemcpyDeviceToHost, s));
+        HUFF_TRY(ctx->sync());
+        for (uint64_t k = 0; k < a.slots; ++k)
+            if (bins[k]) put(k, 0, bins[k]);
+        return Status::ok();
+    }
+    const uint64_t cap = std::min<uint64_t>(n, a.slots);
+    HUFF_TRY(klo.ensure(a.slots * 8));
+    HIP_TRY(hipMemsetAsync(klo.p, 0xFF, a.slots * 8, s));
+    a.keys_lo = static_cast<unsigned long long*>(klo.p);
+    if (width == 16) {
+        HUFF_TRY(khi.ensure(a.slots * 8));
+        HUFF_TRY(state.ensure(a.slots * 4));
+        HIP_TRY(hipMemsetAsync(state.p, 0, a.slots * 4, s));
+        HUFF_TRY(ohi.ensure(cap * 8));
+        a.keys_hi = static_cast<unsigned long long*>(khi.p);
+        a.state = static_cast<unsigned int*>(state.p);
+        a.out_hi = static_cast<unsigned long long*>(ohi.p);
+    }
+    HUFF_TRY(olo.ensure(cap * 8));
+    HUFF_TRY(oc.ensure(cap * 8));
+    HUFF_TRY(misc.ensure(16));
+    HIP_TRY(hipMemsetAsync(misc.p, 0, 16, s));
+    a.out_lo = static_cast<unsigned long long*>(olo.p);
+    a.out_c = static_cast<unsigned long long*>(oc.p);
+    a.nout = static_cast<unsigned long long*>(misc.p);
+    a.sent = a.nout + 1;
+    HUFF_TRY(ctx->timed("wweights", [&] { return dev::wcount_launch(a, s); }));
+    uint64_t m[2] = {};
+    HIP_TRY(hipMemcpyAsync(m, misc.p, 16, hipMemcpyDeviceToHost, s));
     HUFF_TRY(ctx->sync());
-    uniq.resize(runs * width);
-    counts.resize(runs);
-    HIP_TRY(hipMemcpyAsync(uniq.data(), du.p, uniq.size(), hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipMemcpyAsync(counts.data(), dc.p, runs * 8, hipMemcpyDeviceToHost, s));
-    return ctx->sync();
+    std::vector<uint64_t> lo(m[0]), hi(width == 16 ? m[0] : 0), c(m[0]);
+    if (m[0]) {
+        HIP_TRY(hipMemcpyAsync(lo.data(), olo.p, m[0] * 8, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(c.data(), oc.p, m[0] * 8, hipMemcpyDeviceToHost, s));
+        if (width == 16) HIP_TRY(hipMemcpyAsync(hi.data(), ohi.p, m[0] * 8, hipMemcpyDeviceToHost, s));
+        HUFF_TRY(ctx->sync());
+    }
+    std::vector<uint64_t> order(m[0]);
+    for (uint64_t i = 0; i < m[0]; ++i) order[i] = i;
+    std::sort(order.begin(), order.end(), [&](uint64_t x, uint64_t y) {
+        if (width == 16 && hi[x] != hi[y]) return hi[x] < hi[y];
+        return lo[x] < lo[y];
+    });
+    for (uint64_t i : order) put(lo[i], width == 16 ? hi[i] : 0, c[i]);
+    if (m[1]) put(~0ull, 0, m[1]);  // the all-ones u64 letter (the table's empty marker) sorts last
+    return Status::ok();
 }
 
 Status wcompress_host(huff_ctx* ctx, uint32_t width, const uint8_t* letters, size_t n, const huff_wtree* t,

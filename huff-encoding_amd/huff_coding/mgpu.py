@@ -96,6 +96,33 @@ class DeviceExchange:
         return rows_to_hists(self.host.numpy().reshape(self.world, 258))
 
 
+def pack_rows(job, rows: np.ndarray, rank: int, d_out: int, out_cap: int):
+    """huff_mgpu_pack_rows: the native host half of huff_mgpu_compress over
+    rows the caller gathered itself ([world, 258] int64, each rank's
+    huff_enc_hist_row output, rank order) -> (HuffTree, bit_base, bits,
+    owned_bytes); a short buffer raises HuffError with .bits_needed /
+    .bit_base"""
+    import ctypes as C
+
+    from ._lib import load
+
+    from . import HuffError, HuffTree, _check
+
+    rows = np.ascontiguousarray(rows, np.int64)
+    world = rows.shape[0]
+    tree_h = C.c_void_p()
+    base, bits, owned = C.c_uint64(), C.c_uint64(), C.c_uint64()
+    rc = load().huff_mgpu_pack_rows(job.h, rows.ctypes.data_as(C.c_void_p), world, rank, C.c_void_p(d_out), out_cap,
+                                    C.byref(tree_h), C.byref(base), C.byref(bits), C.byref(owned))
+    try:
+        _check(rc)
+    except HuffError as e:
+        e.bits_needed = bits.value
+        e.bit_base = base.value
+        raise
+    return HuffTree(tree_h), base.value, bits.value, owned.value
+
+
 def plan(hists: np.ndarray, tails: List[bytes], code_len: np.ndarray, rank: int) -> ShardPlan:
     per = hists.astype(np.uint64) @ np.asarray(code_len, np.uint64)
     before = b"".join(tails[:rank])

@@ -248,6 +248,19 @@ int huff_comm_world(const huff_comm* c, int* world, int* rank);
  * HUFF_E_BUFFER_TOO_SMALL *bits_out / *bit_base_out still hold the need. */
 int huff_mgpu_compress(huff_comm* c, huff_enc* e, uint8_t* d_out, size_t out_cap, huff_tree** tree_out,
                        uint64_t* bit_base_out, uint64_t* bits_out, uint64_t* owned_bytes_out);
+/* The host half of huff_mgpu_compress, for a caller that exchanges the rows
+ * over its own channel: rows = world x 258 int64 in rank order, each what
+ * huff_enc_hist_row wrote for that rank's shard (host memory, already
+ * gathered); e is this rank's job after huff_enc_hist_row. Unpacks the rows
+ * (weights, tail bytes; a tail count < 0 marks a rank that failed before the
+ * exchange and makes every rank return HUFF_E_INVALID_ARG), builds the tree of
+ * the summed weights, this shard's bit base and shared first byte, and packs
+ * as huff_mgpu_compress does; same outputs. A rank whose pass 1 cannot run
+ * still joins huff_mgpu_compress's collective with such a failed row, so no
+ * rank is left blocked in it. */
+int huff_mgpu_pack_rows(huff_enc* e, const int64_t* rows, int world, int rank, uint8_t* d_out, size_t out_cap,
+                        huff_tree** tree_out, uint64_t* bit_base_out, uint64_t* bits_out,
+                        uint64_t* owned_bytes_out);
 
 /* decompress (comp.rs:487-519) of a device-resident stream that has no
  * restart index (e.g. written by the reference CPU path): comp_bytes bytes at

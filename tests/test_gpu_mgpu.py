@@ -5,7 +5,9 @@ runs the same rehearsal). Unlike tests/test_mgpu_gloo.py (oracle stand-in
 for the pack), each rank runs the real HIP path: device generator at its
 global offset, pass 1 (huff_enc_hist), mgpu.exchange of the weight rows and
 tail bytes, huff_enc_pack_shards (tree, bit base and shared first byte
-computed natively), decode of its own shard. The concatenation of the ranks'
+computed natively), decode of its own shard; the pack_rows cases gather the
+rows huff_enc_hist_row wrote and hand them to huff_mgpu_pack_rows, the host
+half of huff_mgpu_compress (its row unpacking at world > 1). The concatenation of the ranks'
 owned bytes must equal the oracle's encode of the whole input
 (comp.rs:419-451; the reference's CLI merge is huff/src/comp.rs:161-172).
 Shard sizes are ragged, so the shard boundaries fall inside bytes."""
@@ -28,7 +30,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, n, kind, q):
+def _worker(rank, world, port, n, kind, q, native):
     sys.path[:0] = [os.path.join(ROOT, "huff-encoding_amd"), os.path.join(ROOT, "oracle")]
     import torch
     import torch.distributed as dist
@@ -45,13 +47,25 @@ def _worker(rank, world, port, n, kind, q):
         D.generate(ctx, kind, SEED, x.data_ptr(), n, offset=rank * n,
                    cdf=D.zipf_cdf(1.2) if kind == "zipf" else None)
         job = H.EncodeJob(ctx, x.data_ptr(), n)
-        hists, tails = mgpu.exchange(job.hist(), x[n - 8:n].cpu().numpy().tobytes())
         cap = n + 128
         out = torch.zeros(cap, dtype=torch.uint8, device="cuda")
-        tree, base, bits = job.pack_shards(hists, rank, tails, out.data_ptr(), cap)
+        if native:
+            # huff_enc_hist_row on the device, rows gathered over gloo, then
+            # the library's own row unpacking + pack (huff_mgpu_pack_rows)
+            row = torch.empty(258, dtype=torch.int64, device="cuda")
+            job.hist_row(row.data_ptr())
+            torch.cuda.synchronize()
+            rows = [torch.empty(258, dtype=torch.int64) for _ in range(world)]
+            dist.all_gather(rows, row.cpu())
+            tree, base, bits, owned = mgpu.pack_rows(job, torch.stack(rows).numpy(), rank, out.data_ptr(), cap)
+        else:
+            hists, tails = mgpu.exchange(job.hist(), x[n - 8:n].cpu().numpy().tobytes())
+            tree, base, bits = job.pack_shards(hists, rank, tails, out.data_ptr(), cap)
         torch.cuda.synchronize()
         nbytes = (base % 8 + bits + 7) // 8
         mine = mgpu.owned_bytes(out[:nbytes].cpu().numpy(), base, bits, rank == world - 1)
+        if native:
+            assert owned == mine.size, (owned, mine.size)
         dec = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
         job.decode(tree, out.data_ptr(), dec.data_ptr())
         torch.cuda.synchronize()
@@ -67,15 +81,16 @@ def _worker(rank, world, port, n, kind, q):
         raise
 
 
+@pytest.mark.parametrize("native", [False, True], ids=["pack_shards", "pack_rows"])
 @pytest.mark.parametrize("world,kind", [(2, "text"), (3, "zipf")])
-def test_sharded_processes_on_gpu(world, kind, O):
+def test_sharded_processes_on_gpu(world, kind, native, O):
     import torch.multiprocessing as mp
 
     n = (1 << 21) + 12345  # ragged: shard boundaries fall inside bytes of the stream
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, n, kind, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n, kind, q, native)) for r in range(world)]
     for p in procs:
         p.start()
     try:
