@@ -162,6 +162,7 @@ struct IndexlessArgs {
 };
 // single-pass index-free decode (ifdec.hip)
 constexpr uint32_t kIfdPrefixCap = 32;  // letters a lane's fix-up walk keeps before it gives up (slow lane)
+constexpr uint32_t kIfdStageMax = 4 * 256 * 16;  // a block's staged bytes (4 pieces per thread in flight)
 struct IfdArgs {
     const uint8_t* comp;          // stream; bit 0 = MSB of comp[0]
     uint64_t comp_bytes;
@@ -174,6 +175,7 @@ struct IfdArgs {
     const uint32_t* lut;          // multi-level table (codes longer than stab_bits)
     uint32_t lut_bits;
     uint32_t max_len;             // <= 32
+    uint32_t cu_count;            // the persistent grid
     uint8_t* out;                 // 16-B aligned
     uint64_t out_cap;
     unsigned long long* status;   // [nblocks] look-back words, zeroed

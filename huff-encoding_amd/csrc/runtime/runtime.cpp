@@ -1067,10 +1067,14 @@ Status indexless_mark(huff_ctx* ctx, IndexlessSync& st, DevBuf& sub_abs, uint32_
     return Status::ok();
 }
 
-// HUFF_IFD=0 turns the single-pass index-free decoder off (A/B, tests)
+// The single-pass index-free decoder (ifdec.hip) is opt-in: HUFF_IFD=1 runs
+// it for self-synchronising codes, =2 for every stream. Measured slower than
+// the multi-kernel path on 1 GiB (Zipf 3.4-3.6 ms vs 1.31, text 2.0 vs 1.16:
+// its blocks are latency-bound at 3 workgroups per CU and the look-back stalls
+// whole generations of blocks), so it is not the default.
 static bool ifd_enabled() {
     const char* e = std::getenv("HUFF_IFD");
-    return !(e && *e == '0');
+    return e && (*e == '1' || *e == '2');
 }
 
 // The single-pass decoder (ifdec.hip) for codes <= 32 bits. *done = false
@@ -1130,17 +1134,18 @@ static Status decode_indexless_single(huff_ctx* ctx, const uint8_t* d_comp, uint
     a.lut = static_cast<const uint32_t*>(ctx->d_lut.p);
     a.lut_bits = dt->bits;
     a.max_len = dt->maxdepth;
+    a.cu_count = static_cast<uint32_t>(ctx->cu_count);
     a.end_bit = d_end;
-    if (dev::ifd_lds_bytes(a) > 160 * 1024) return Status::ok();
-    // scratch: flags[4] | ticket | pad | total | status[nblocks] | exits[nblocks]
+    if (dev::ifd_lds_bytes(a) > 160 * 1024 || a.stage_bytes > dev::kIfdStageMax) return Status::ok();
+    // scratch: flags[16] | stats timers u64[8] | ticket | pad | total | status[nblocks] | exits[nblocks]
     IndexlessSync& st = ctx->indexless_ws();
-    const size_t scratch = 32 + 16 * static_cast<size_t>(a.nblocks);
+    const size_t scratch = 144 + 16 * static_cast<size_t>(a.nblocks);
     HUFF_TRY(st.ifd.ensure(scratch));
     uint8_t* sp = static_cast<uint8_t*>(st.ifd.p);
     a.flags = reinterpret_cast<unsigned int*>(sp);
-    a.ticket = reinterpret_cast<unsigned int*>(sp + 16);
-    a.total = reinterpret_cast<unsigned long long*>(sp + 24);
-    a.status = reinterpret_cast<unsigned long long*>(sp + 32);
+    a.ticket = reinterpret_cast<unsigned int*>(sp + 128);
+    a.total = reinterpret_cast<unsigned long long*>(sp + 136);
+    a.status = reinterpret_cast<unsigned long long*>(sp + 144);
     a.exits = a.status + a.nblocks;
     // the output: the caller's buffer, or `out` sized for the tree's
     // expected letters (grown and rerun if the stream has more)
@@ -1163,25 +1168,33 @@ static Status decode_indexless_single(huff_ctx* ctx, const uint8_t* d_comp, uint
     };
     HUFF_TRY(place(static_cast<uint64_t>(1.25 * static_cast<double>(valid_bits) / std::max(mean, 1.0)) + 4096));
     hipStream_t strm = ctx->stream;
-    uint64_t res[4] = {};
+    uint64_t res[18] = {};
     for (int attempt = 0; attempt < 2; ++attempt) {
         a.out = dst;
         a.out_cap = cap;
         HIP_TRY(hipMemsetAsync(st.ifd.p, 0, scratch, strm));
         HUFF_TRY(ctx->timed("indexless_decode", [&] { return dev::launch_ifd(a, strm); }));
-        HIP_TRY(hipMemcpyAsync(res, st.ifd.p, 32, hipMemcpyDeviceToHost, strm));
+        HIP_TRY(hipMemcpyAsync(res, st.ifd.p, 144, hipMemcpyDeviceToHost, strm));
         HUFF_TRY(ctx->sync());
         const uint32_t flags = static_cast<uint32_t>(res[0]);
-        if (std::getenv("HUFF_IFD_TRACE"))
-            std::fprintf(stderr, "ifd: S=%llu nseg=%llu blocks=%u flags=%u total=%llu cap=%llu\n",
-                         static_cast<unsigned long long>(S), static_cast<unsigned long long>(nseg), a.nblocks, flags,
-                         static_cast<unsigned long long>(res[3]), static_cast<unsigned long long>(cap));
+        if (std::getenv("HUFF_IFD_TRACE")) {
+            const uint32_t* f = reinterpret_cast<const uint32_t*>(res);
+            std::fprintf(stderr, "ifd: S=%llu nseg=%llu blocks=%u flags=%u total=%llu cap=%llu slow=%u ovf=%u "
+                         "settle=%u repair=%u big=%u\n", static_cast<unsigned long long>(S),
+                         static_cast<unsigned long long>(nseg), a.nblocks, flags,
+                         static_cast<unsigned long long>(res[17]), static_cast<unsigned long long>(cap), f[8], f[9],
+                         f[10], f[11], f[12]);
+            std::fprintf(stderr, "ifd cycles (sum over blocks, thread 0): decode %.3g fix %.3g count %.3g image %.3g "
+                         "lookback %.3g final %.3g copy %.3g stage %.3g\n", double(res[8]), double(res[9]),
+                         double(res[10]), double(res[11]), double(res[12]), double(res[13]), double(res[14]),
+                         double(res[15]));
+        }
         if (flags & 4u) return Status::err(HUFF_E_HIP, "index-free decode: the look-back did not complete");
         if (flags & 1u) return Status::ok();  // not self-synchronising here: the multi-kernel path
-        *nsym = res[3];
+        *nsym = res[17];
         if (!(flags & 2u)) break;
         if (d_user) return Status::err(HUFF_E_BUFFER_TOO_SMALL, "output buffer too small");
-        HUFF_TRY(place(res[3]));
+        HUFF_TRY(place(res[17]));
     }
     if (dst != (d_user ? d_user : static_cast<uint8_t*>(out.p)) && *nsym)
         HIP_TRY(hipMemcpyAsync(d_user ? d_user : out.p, dst, *nsym, hipMemcpyDeviceToDevice, strm));

@@ -74,7 +74,7 @@ def test_ifd_matches_oracle(H, O, ctx, cases, mode, monkeypatch):
         _roundtrip(H, O, ctx, data)
 
 
-@pytest.mark.parametrize("seg", ["16", "24", "40", "97", "700"])
+@pytest.mark.parametrize("seg", ["16", "24", "40", "97", "400"])
 def test_ifd_forced_segments(H, O, ctx, cases, seg, monkeypatch):
     """tiny segments: most lanes do not resynchronise inside their segment
     (slow lanes, re-walks, broken anchors -> the multi-kernel fallback);
@@ -87,7 +87,8 @@ def test_ifd_forced_segments(H, O, ctx, cases, seg, monkeypatch):
         _roundtrip(H, O, ctx, data)
 
 
-def test_ifd_misaligned_output(H, O, ctx, cases):
+def test_ifd_misaligned_output(H, O, ctx, cases, monkeypatch):
+    monkeypatch.setenv("HUFF_IFD", "2")
     for name, data in cases[:3]:
         _roundtrip(H, O, ctx, data[:1_000_003], misalign=3)
 
@@ -110,12 +111,14 @@ def test_ifd_equals_multikernel_path(H, O, ctx, monkeypatch):
     assert torch.equal(outs[0], outs[1])
 
 
-def test_ifd_garbage_payloads(H, O, ctx):
+@pytest.mark.parametrize("mode", ["0", "2"], ids=["multikernel", "single-pass"])
+def test_ifd_garbage_payloads(H, O, ctx, mode, monkeypatch):
     """random payloads under a fixed tree: whatever the bits, the letters and
     the dropped final code match the reference walk"""
     import torch
     from huff_coding import device as D
 
+    monkeypatch.setenv("HUFF_IFD", mode)
     rng = np.random.default_rng(5)
     t = O.Tree.from_weights(O.weights_from_bytes(O.gen_text(0x5EED0005, 1 << 16).tobytes()))
     tree = H.HuffTree.try_from_bin(t.as_bin())

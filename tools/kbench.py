@@ -65,7 +65,7 @@ def main():
         pad = (8 - bits % 8) % 8
         got = D.decompress_dev(ctx, tree, out.data_ptr(), comp_bytes, pad, dec.data_ptr(), n + 64)
         torch.cuda.synchronize()
-        assert got == n and (args.no_verify or torch.equal(dec[:n], x[:n]))
+        assert args.no_verify or (got == n and torch.equal(dec[:n], x[:n]))
         ctx.set_timing(True)
         ctx.reset_timing()
         t0 = time.perf_counter()
