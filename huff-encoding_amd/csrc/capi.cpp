@@ -451,6 +451,43 @@ int huff_dev_decompress(huff_ctx* ctx, const huff_tree* t, const uint8_t* d_comp
     });
 }
 
+int huff_batch_hist(huff_ctx* ctx, const uint8_t* d_in, const uint64_t* d_offsets, uint32_t nstreams,
+                    uint64_t* d_hist) {
+    if (!ctx || (nstreams && (!d_offsets || !d_hist))) return fail(HUFF_E_INVALID_ARG, "null argument");
+    return guarded([&]() -> huff::Status {
+        HUFF_TRY(ctx->activate());
+        HUFF_TRY(ctx->timed("hist_batch",
+                            [&] { return huff::dev::launch_hist_batch(d_in, d_offsets, nstreams, d_hist, ctx->stream); }));
+        return ctx->sync();
+    });
+}
+
+int huff_batch_trees(huff_ctx* ctx, const uint64_t* d_hist, uint32_t nstreams, uint8_t* d_tree_bits,
+                     size_t tree_stride, uint32_t* d_tree_nbits, uint64_t* d_codes, uint32_t* d_max_len,
+                     uint32_t* d_status) {
+    if (!ctx || (nstreams && (!d_hist || !d_tree_bits || !d_tree_nbits || !d_codes || !d_max_len || !d_status)))
+        return fail(HUFF_E_INVALID_ARG, "null argument");
+    if (tree_stride < HUFF_TREE_BITS_MAX_BYTES || tree_stride > 0xFFFFFFFFu)
+        return fail(HUFF_E_INVALID_ARG, "tree_stride < HUFF_TREE_BITS_MAX_BYTES");
+    static_assert(HUFF_TREE_BITS_MAX_BYTES == huff::dev::kTreeBitsMaxBytes, "as_bin of 257 leaves");
+    static_assert(huff::dev::kTreeEmpty == HUFF_E_EMPTY_WEIGHTS && huff::dev::kTreeDeep == HUFF_E_CODE_TOO_LONG,
+                  "the kernel writes the C ABI's status codes");
+    return guarded([&]() -> huff::Status {
+        HUFF_TRY(ctx->activate());
+        huff::dev::TreeBatchArgs a{};
+        a.hist = d_hist;
+        a.nstreams = nstreams;
+        a.tree_bits = d_tree_bits;
+        a.tree_stride = static_cast<uint32_t>(tree_stride);
+        a.tree_nbits = d_tree_nbits;
+        a.codes = d_codes;
+        a.max_len = d_max_len;
+        a.status = d_status;
+        HUFF_TRY(ctx->timed("tree_batch", [&] { return huff::dev::launch_tree_batch(a, ctx->stream); }));
+        return ctx->sync();
+    });
+}
+
 int huff_dev_generate(huff_ctx* ctx, int kind, uint64_t seed, uint64_t offset, const uint64_t* cdf, uint8_t* d_out,
                       size_t n) {
     if (!ctx || (!d_out && n) || (kind == 1 && !cdf)) return fail(HUFF_E_INVALID_ARG, "null argument");

@@ -218,25 +218,36 @@ constexpr uint32_t kTaskSym = 4096;  // symbols per decode task (k_decode_fixed)
 hipError_t launch_index_expand(uint64_t n, const uint64_t* task_base, const uint16_t* sub16,
                                const uint64_t* chunk_start, uint32_t* sub_bit, hipStream_t s);
 
-// wider letters (wide.hip): W-byte keys, hash-table code lookup
+// wider letters (wide.hip): W-byte keys, hash-table code lookup. The
+// encoder's chunk is kWideChunk letters (one wave: 64 runs of kSub), its
+// restart index chunk_start per chunk + u32 sub_bit per run.
+constexpr uint32_t kWideChunk = 64 * kSub;
 struct WideArgs {
     const uint8_t* in;            // n letters of `width` bytes, native layout, 16-B aligned
     uint64_t n;
     uint32_t width;               // 1, 2, 4, 8, 16
-    uint32_t log2_slots;          // cuckoo table: 2^log2_slots slots in buckets of 2
-    uint64_t fold;                // 16-byte keys: hash of lo ^ hi * fold (host/wide.hpp wide_buckets)
-    const uint8_t* keys;          // [slots * max(4, width)]
-    const void* vals;             // [slots] (code << 8) | len, 0 = empty; u32 if val32 else u64
-    uint32_t val32;               // every code <= 24 bits
-    uint32_t table_in_lds;        // stage the table in LDS (wide_table_lds_bytes)
-    uint32_t nchunks;             // ceil(n / kChunk)
+    // code table (host/wide.hpp WideEncTables): `slots` slots of slot_bytes,
+    // {key, value}; a letter's slots are wide_slots(wide_hkey(letter))
+    const void* table;
+    uint32_t slots, slot_bytes, mul1;
+    uint64_t fold;
+    uint32_t long_codes;          // values u64 code << 6 | len, else u32 code << (32 - len) | len
+    uint32_t max_len;
+    uint32_t table_in_lds;        // stage the table in LDS (wide_lds_bytes <= kWideLdsMax)
+    uint32_t nchunks;             // ceil(n / kWideChunk)
     uint32_t cu_count;            // persistent grid size
+    uint32_t stage_words;         // pack: LDS staging words per wave (wide_stage_words)
     uint64_t* chunk_bits;         // [nchunks]            (bits pass)
     const uint64_t* chunk_start;  // [nchunks + 1]        (pack pass)
-    uint32_t* sub_bit;            // [ceil(n / kSub)]
+    uint32_t* sub_bit;            // [ceil(n / kSub)] run start - chunk start
     unsigned long long* first_missing;  // min index of a letter without a code
-    uint32_t* out;                // 4-B aligned, ceil(bits / 32) words
+    uint8_t* out;                 // any alignment: ceil(bits / 8) bytes
 };
+// LDS of a pass's workgroup (the table when in_lds, pack's staging images);
+// the table is staged when a workgroup's total fits kWideLdsMax
+constexpr size_t kWideLdsMax = 160 * 1024;
+uint32_t wide_stage_words(uint32_t width, uint32_t max_len);
+size_t wide_lds_bytes(const WideArgs& a, bool pack_pass, bool in_lds);
 struct WideDecArgs {
     const uint8_t* comp;          // 4-B aligned
     uint64_t comp_bytes;
@@ -254,9 +265,6 @@ struct WideDecArgs {
     uint64_t n;
     uint8_t* out;                 // n * width bytes
 };
-inline size_t wide_table_lds_bytes(uint32_t width, uint32_t log2_slots, bool val32) {
-    return (size_t(1) << log2_slots) * ((val32 ? 4 : 8) + (width < 4 ? 4 : width));
-}
 hipError_t launch_wide_bits(const WideArgs& a, hipStream_t s);
 hipError_t launch_wide_pack(const WideArgs& a, hipStream_t s);
 hipError_t launch_wide_decode(const WideDecArgs& a, hipStream_t s);
@@ -277,6 +285,25 @@ struct WCountArgs {
 };
 uint64_t wcount_slots(uint32_t width, uint64_t n);
 hipError_t wcount_launch(const WCountArgs& a, hipStream_t s);
+
+// HuffTree of many small byte streams in one launch (tree_batch.hip)
+constexpr uint32_t kTreeBitsMaxBytes = (2 * 257 - 1 + 8 * 257 + 7) / 8;  // as_bin of 257 leaves
+constexpr uint32_t kTreeCodeMax = 56;  // codes[] holds code << 8 | len
+enum : uint32_t { kTreeOk = 0, kTreeEmpty = 2, kTreeDeep = 7 };  // = HUFF_OK, HUFF_E_EMPTY_WEIGHTS, HUFF_E_CODE_TOO_LONG
+struct TreeBatchArgs {
+    const uint64_t* hist;   // [nstreams][256] byte weights
+    uint32_t nstreams;
+    uint8_t* tree_bits;     // [nstreams][tree_stride]: as_bin (tree_inner.rs:637-663), MSB first
+    uint32_t tree_stride;   // >= kTreeBitsMaxBytes
+    uint32_t* tree_nbits;   // [nstreams]
+    uint64_t* codes;        // [nstreams][256]: code << 8 | len; 0 = no code (or longer than kTreeCodeMax)
+    uint32_t* max_len;      // [nstreams]
+    uint32_t* status;       // [nstreams]: kTreeOk, kTreeEmpty (no weights), kTreeDeep (a code > kTreeCodeMax)
+};
+// hist[s] = the byte weights of in[off[s], off[s + 1])
+hipError_t launch_hist_batch(const uint8_t* in, const uint64_t* off, uint32_t nstreams, uint64_t* hist,
+                             hipStream_t s);
+hipError_t launch_tree_batch(const TreeBatchArgs& a, hipStream_t s);
 
 // codes longer than kLongMaxLen (deep.hip): up to 255 bits, kDeepWords
 // left-aligned words per letter

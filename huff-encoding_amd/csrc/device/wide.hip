@@ -2,113 +2,483 @@
 // their signed twins; SURVEY.md §8f-3, letter.rs:41-60) with
 // compress_with_tree / decompress semantics (comp.rs:419-451, 487-519).
 //
-// Layout is that of the byte path: a chunk of 65,536 letters per workgroup,
-// one lane per 256-letter run, a restart index of u32 sub_bit per run and u64
-// chunk_bits / chunk_start per chunk (kernels.hpp). What changes is the code
-// lookup: letters are W-byte keys, so the tree's codes live in an
-// open-addressing hash table (<= 50 % full, so a probe always ends), staged
-// into LDS when it fits.
+// Encode is the byte path's two passes (pass 1 + pack, pack.hip) with the
+// code lookup in a cuckoo hash table instead of a 256-entry array. Work unit:
+// one wide chunk of kWideChunk = 16,384 letters per WAVE; 16 waves per
+// workgroup share the table in LDS (when it fits, else it is read from L2).
+// Every round a wave reads 1 KiB (W = 1) or 2 KiB of letters, 16 or 32
+// consecutive bytes per lane (coalesced dwordx4, two rounds in flight through
+// a buffer resource clamped to the chunk: loads past it read zero).
 //
-//  k_wbits   pass A: look up every letter, sum code lengths per run, scan the
-//            256 runs of the chunk (-> sub_bit, chunk_bits); the first letter
-//            with no code (input order) goes to first_missing (CompressError).
-//  k_wpack   pass B: every lane re-emits its run's codes as 32-bit words. A
-//            lane writes exactly the words whose first bit lies in its run
-//            (no atomics, no zero fill): it drops the bits before its first
-//            word boundary and completes its last word by looking ahead into
-//            the following letters.
+//  lookup    a letter is in one of two slots (host/wide.hpp wide_slots: two
+//            multiplicative hashes of its 32-bit hash key, reduced to the
+//            table size by a high multiply). Slots are {key, value} in one
+//            ds_read_b64 (keys of <= 4 bytes, short codes) or _b128. All the
+//            lane's first slots are read; then the second slots of the
+//            letters that missed, with every other lane reading slot 0 (one
+//            broadcast address): the second read costs only the misses'
+//            bank conflicts. The host inserts letters shortest code first,
+//            so frequent letters sit in their first slot.
+//  k_wbits   pass 1: per-lane code-length sums, a wave scan per round, and
+//            the run totals (a run = kSub letters = 16 / 8W lanes) gathered
+//            lane j <- run j; at the chunk end one more wave scan gives
+//            sub_bit (run start - chunk start) and chunk_bits. The first
+//            letter with no code (input order) goes to first_missing
+//            (CompressError, comp.rs:426-432).
+//  k_wpack   pass 2 (pack.hip's scheme, pack_emit.hpp): a wave scan of the
+//            round's lengths gives each lane its bit offset; the codes are
+//            ORed into the wave's LDS staging image (short codes in groups of
+//            G per OR pair), whole 16-byte segments leave as dwordx4 stores.
+//            A chunk owns output bytes [cs / 8, ce / 8) (the last one through
+//            ceil(ce / 8)); the bits of its first byte that belong to the
+//            letters before it are recomputed from those letters, so no byte
+//            is written twice and the output needs no zero fill. Any output
+//            alignment: the image is aligned to the 16-byte granule below.
 //  k_wdecode one lane per 256-letter run from the restart index (or from the
 //            index-free decoder's sub_abs), primary table in LDS, secondary
 //            tables and the leaf letters in global memory.
 //
-// Roofline: HBM-bound in principle (pass A reads n*W, pass B n*W + writes C);
-// in practice latency-bound on the per-letter probe chain.
+// Roofline: HBM-bound. Pass 1 reads n W bytes, pass 2 n W + writes C.
 #include <type_traits>
 
-#include "bitreader.hpp"
+#include "pack_emit.hpp"
 
 namespace huff::dev {
 
 namespace {
 
-constexpr int kThreads = 256;
+constexpr int kThreads = 256;    // decoder workgroup
+constexpr int kEncWaves = 16;    // encoder workgroup: waves sharing one LDS table
 constexpr size_t kLetterLdsMax = 32 * 1024;  // stage the decoder's leaf letters in LDS up to this
 
 struct U128 {
     uint64_t lo, hi;
 };
 
-template <typename T>
-struct KeyOps {
-    __device__ static uint64_t lo(T v) { return static_cast<uint64_t>(v); }
-    __device__ static uint64_t hi(T) { return 0; }
-    __device__ static bool eq(T a, T b) { return a == b; }
-    // letter j of a 16-byte vector (little-endian)
-    __device__ static T get(const uint4& v, uint32_t j) {
-        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-        if (sizeof(T) == 8) return static_cast<T>(w[2 * j] | (static_cast<uint64_t>(w[2 * j + 1]) << 32));
-        constexpr uint32_t per = 4 / (sizeof(T) < 4 ? sizeof(T) : 4);  // letters per dword
-        const uint32_t word = w[j / per];
-        return static_cast<T>(word >> (8 * sizeof(T) * (j % per)));
-    }
+// ---------------------------------------------------------------------------
+// code table (host/wide.hpp wide_slot_layout)
+template <uint32_t W>
+using KeyT = std::conditional_t<(W <= 4), uint32_t, std::conditional_t<(W == 8), uint64_t, U128>>;
+
+template <typename K, typename V>
+struct Slot;
+template <>
+struct alignas(8) Slot<uint32_t, uint32_t> {
+    uint32_t key, val;
 };
 template <>
-struct KeyOps<U128> {
-    __device__ static uint64_t lo(U128 v) { return v.lo; }
-    __device__ static uint64_t hi(U128 v) { return v.hi; }
-    __device__ static bool eq(U128 a, U128 b) { return a.lo == b.lo && a.hi == b.hi; }
-    __device__ static U128 get(const uint4& v, uint32_t) {
-        return {v.x | (static_cast<uint64_t>(v.y) << 32), v.z | (static_cast<uint64_t>(v.w) << 32)};
+struct alignas(16) Slot<uint32_t, uint64_t> {
+    uint32_t key, pad;
+    uint64_t val;
+};
+template <>
+struct alignas(16) Slot<uint64_t, uint32_t> {
+    uint64_t key;
+    uint32_t val, pad;
+};
+template <>
+struct alignas(16) Slot<uint64_t, uint64_t> {
+    uint64_t key, val;
+};
+template <>
+struct alignas(16) Slot<U128, uint32_t> {
+    U128 key;
+    uint32_t val, pad[3];
+};
+template <>
+struct alignas(16) Slot<U128, uint64_t> {
+    U128 key;
+    uint64_t val, pad;
+};
+static_assert(sizeof(Slot<uint32_t, uint32_t>) == 8 && sizeof(Slot<uint32_t, uint64_t>) == 16 &&
+                  sizeof(Slot<uint64_t, uint32_t>) == 16 && sizeof(Slot<U128, uint64_t>) == 32,
+              "slots as host/wide.hpp wide_slot_layout");
+
+__device__ __forceinline__ bool key_eq(uint32_t a, uint32_t b) { return a == b; }
+__device__ __forceinline__ bool key_eq(uint64_t a, uint64_t b) { return a == b; }
+__device__ __forceinline__ bool key_eq(U128 a, U128 b) { return a.lo == b.lo && a.hi == b.hi; }
+
+// host/wide.hpp wide_hkey
+template <uint32_t W>
+__device__ __forceinline__ uint32_t hkey(KeyT<W> k, uint64_t fold) {
+    if constexpr (W <= 4) {
+        return k;
+    } else if constexpr (W == 8) {
+        return static_cast<uint32_t>((k * fold) >> 32);
+    } else {
+        const uint64_t x = k.lo ^ (k.hi * fold);
+        return static_cast<uint32_t>((x * fold) >> 32);
     }
+}
+
+// host/wide.hpp wide_slots: s1 = the high half of (x * mul) * slots; s2 =
+// s1 + 1 + bits 8..15 of x * mul, modulo slots (one quarter-rate multiply
+// pair per letter, the second slot from full-rate ops)
+__device__ __forceinline__ void wslots(uint32_t x, uint32_t mul, uint32_t slots, uint32_t& s1, uint32_t& s2) {
+    const uint32_t h = x * mul;
+    s1 = __umulhi(h, slots);
+    const uint32_t t = s1 + ((h >> 8) & 255u) + 1u;
+    s2 = min(t, t - slots);  // t < slots: t; else t - slots (t - slots wraps above t otherwise)
+}
+
+template <uint32_t W, typename V>
+struct Tab {
+    const Slot<KeyT<W>, V>* s;
+    uint32_t slots, mul1;
+    uint64_t fold;
 };
 
-// stored key type: keys of <= 4 bytes are kept as u32 (host/wide.hpp wide_key_bytes)
-template <typename T>
-using KeyStore = std::conditional_t<(sizeof(T) < 4), uint32_t, T>;
-
-template <typename T>
-__device__ __forceinline__ KeyStore<T> to_store(T v) {
-    if constexpr (sizeof(T) < 4) return static_cast<uint32_t>(v);
-    else return v;
+// the values of N letters (0 = no code), two reads per letter as above.
+// Selects as masks: a select between two loaded values is otherwise turned
+// into a load from a selected address (flat, through scratch).
+template <typename V>
+__device__ __forceinline__ V keep_if(bool c, V v) {
+    return v & (V(0) - V(c));
+}
+template <uint32_t W, typename V, int B>
+__device__ __forceinline__ void lookup_group(const Tab<W, V>& t, const KeyT<W>* key, V* val) {
+    using S = Slot<KeyT<W>, V>;
+    uint32_t s1[B], s2[B];
+#pragma unroll
+    for (int k = 0; k < B; ++k) wslots(hkey<W>(key[k], t.fold), t.mul1, t.slots, s1[k], s2[k]);
+    S e1[B];
+#pragma unroll
+    for (int k = 0; k < B; ++k) e1[k] = t.s[s1[k]];
+    // an empty slot's key is no letter of the table (host/wide.hpp), so a
+    // key match alone means the slot holds the letter
+    bool m1[B];
+    uint32_t a2[B];
+#pragma unroll
+    for (int k = 0; k < B; ++k) {
+        m1[k] = key_eq(e1[k].key, key[k]);
+        a2[k] = m1[k] ? 0u : s2[k];
+    }
+    S e2[B];
+#pragma unroll
+    for (int k = 0; k < B; ++k) e2[k] = t.s[a2[k]];
+#pragma unroll
+    for (int k = 0; k < B; ++k) val[k] = keep_if(m1[k], e1[k].val) | keep_if(key_eq(e2[k].key, key[k]), e2[k].val);
+}
+// in groups of <= 8 letters (4 with long values and small keys): the
+// slots of a group are in flight together
+template <uint32_t W, typename V, int N>
+__device__ __forceinline__ void lookup_n(const Tab<W, V>& t, const KeyT<W> (&key)[N], V (&val)[N]) {
+    constexpr int B0 = sizeof(V) == 8 && W <= 2 ? 4 : 8;
+    constexpr int B = N < B0 ? N : B0;
+#pragma unroll
+    for (int g = 0; g < N; g += B) lookup_group<W, V, B>(t, key + g, val + g);
 }
 
-// host/wide.hpp wide_buckets
-template <typename T>
-__device__ __forceinline__ void buckets_of(T key, uint32_t lgb, uint64_t fold, uint32_t& b1, uint32_t& b2) {
-    using K = KeyOps<T>;
-    if constexpr (sizeof(T) <= 4) {
-        const uint32_t x = static_cast<uint32_t>(K::lo(key));
-        b1 = (x * 0x9E3779B1u) >> (32 - lgb);
-        b2 = (x * 0x85EBCA77u + 0x165667B1u) >> (32 - lgb);
+// bytes of letters per lane per round, and the round
+// lane bytes per round (16 or 32) of pass 1 and pass 2 by letter width, and
+// the rounds of loads in flight ahead of the encoder (tuning knobs)
+#ifndef WIDE_LB_BITS2
+#define WIDE_LB_BITS2 32
+#endif
+#ifndef WIDE_LB_BITS4
+#define WIDE_LB_BITS4 32
+#endif
+#ifndef WIDE_LB_PACK2
+#define WIDE_LB_PACK2 32
+#endif
+#ifndef WIDE_LB_PACK4
+#define WIDE_LB_PACK4 32
+#endif
+#ifndef WIDE_BITS_AHEAD
+#define WIDE_BITS_AHEAD 2
+#endif
+#ifndef WIDE_PACK_AHEAD
+#define WIDE_PACK_AHEAD 2
+#endif
+#ifndef WIDE_BITS_WAVES
+#define WIDE_BITS_WAVES 1
+#endif
+template <uint32_t W, bool PACK>
+constexpr uint32_t lane_bytes() {
+    if constexpr (W == 1) return 16u;
+    if constexpr (W == 2) return PACK ? WIDE_LB_PACK2 : WIDE_LB_BITS2;
+    if constexpr (W == 4) return PACK ? WIDE_LB_PACK4 : WIDE_LB_BITS4;
+    return 32u;
+}
+template <uint32_t LB>
+struct LaneIn {
+    uint4 v[LB / 16];
+};
+template <uint32_t LB>
+__device__ __forceinline__ LaneIn<LB> load_round(__amdgpu_buffer_rsrc_t r, uint32_t round, uint32_t lane) {
+    LaneIn<LB> x;
+#pragma unroll
+    for (uint32_t q = 0; q < LB / 16; ++q) x.v[q] = buf_ld16(r, round * 64 * LB + lane * LB + 16 * q);
+    return x;
+}
+
+// letter k of the lane's bytes
+template <uint32_t W, int NW>
+__device__ __forceinline__ KeyT<W> letter_of(const uint32_t (&w)[NW], int k) {
+    if constexpr (W == 1) {
+        return (w[k >> 2] >> (8 * (k & 3))) & 0xFFu;
+    } else if constexpr (W == 2) {
+        return (w[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
+    } else if constexpr (W == 4) {
+        return w[k];
+    } else if constexpr (W == 8) {
+        return w[2 * k] | (static_cast<uint64_t>(w[2 * k + 1]) << 32);
     } else {
-        const uint64_t k = K::lo(key) ^ (K::hi(key) * fold);
-        b1 = static_cast<uint32_t>((k * 0x9E3779B97F4A7C15ull) >> (64 - lgb));
-        b2 = static_cast<uint32_t>((k * 0xD6E8FEB86659FD93ull + 0x165667B19E3779F9ull) >> (64 - lgb));
+        return U128{w[4 * k] | (static_cast<uint64_t>(w[4 * k + 1]) << 32),
+                    w[4 * k + 2] | (static_cast<uint64_t>(w[4 * k + 3]) << 32)};
     }
 }
 
-// value of a key: the four slots of its two buckets, no loop, no branch (a
-// key is stored once; empty slots hold value 0)
-template <typename T, typename V>
-__device__ __forceinline__ V lookup(const KeyStore<T>* keys, const V* vals, uint32_t lgs, uint64_t fold, T key) {
-    using K = KeyOps<KeyStore<T>>;
-    uint32_t b1, b2;
-    buckets_of<T>(key, lgs - 1, fold, b1, b2);
-    const KeyStore<T> k = to_store<T>(key);
-    const uint32_t s1 = 2 * b1, s2 = 2 * b2;
-    const KeyStore<T> k10 = keys[s1], k11 = keys[s1 + 1], k20 = keys[s2], k21 = keys[s2 + 1];
-    const V v10 = vals[s1], v11 = vals[s1 + 1], v20 = vals[s2], v21 = vals[s2 + 1];
-    return (K::eq(k10, k) ? v10 : V(0)) | (K::eq(k11, k) ? v11 : V(0)) | (K::eq(k20, k) ? v20 : V(0)) |
-           (K::eq(k21, k) ? v21 : V(0));
+template <uint32_t W>
+__device__ __forceinline__ KeyT<W> letter_at(const uint8_t* __restrict__ in, uint64_t i) {
+    if constexpr (W == 1) return in[i];
+    else if constexpr (W == 2) return reinterpret_cast<const uint16_t*>(in)[i];
+    else if constexpr (W == 4) return reinterpret_cast<const uint32_t*>(in)[i];
+    else if constexpr (W == 8) return reinterpret_cast<const uint64_t*>(in)[i];
+    else return U128{reinterpret_cast<const uint64_t*>(in)[2 * i], reinterpret_cast<const uint64_t*>(in)[2 * i + 1]};
 }
 
-// the values of the letters of a 16-byte vector (0 = no code)
-template <typename T, typename V, uint32_t L>
-__device__ __forceinline__ void probe_vec(const KeyStore<T>* keys, const V* vals, uint32_t lgs, uint64_t fold,
-                                          const uint4& in, V (&e)[L]) {
-#pragma unroll
-    for (uint32_t j = 0; j < L; ++j) e[j] = lookup<T, V>(keys, vals, lgs, fold, KeyOps<T>::get(in, j));
+template <typename V>
+__device__ __forceinline__ uint32_t len_of(V v) {
+    return static_cast<uint32_t>(v) & (sizeof(V) == 8 ? 63u : 31u);
 }
+
+__host__ __device__ constexpr uint32_t table_lds_bytes(uint32_t slots, uint32_t slot_bytes) {
+    return (slots * slot_bytes + 15u) & ~15u;
+}
+
+// the table: copied into LDS (the host pads it to 16 bytes), or read in place
+template <uint32_t W, typename V, bool LDS>
+__device__ __forceinline__ Tab<W, V> stage_table(const WideArgs& a, uint8_t* lds) {
+    using S = Slot<KeyT<W>, V>;
+    Tab<W, V> t{nullptr, a.slots, a.mul1, a.fold};
+    if constexpr (LDS) {
+        const uint32_t q = table_lds_bytes(a.slots, a.slot_bytes) / 16;
+        for (uint32_t i = threadIdx.x; i < q; i += blockDim.x)
+            reinterpret_cast<uint4*>(lds)[i] = static_cast<const uint4*>(a.table)[i];
+        t.s = reinterpret_cast<const S*>(lds);
+    } else {
+        t.s = static_cast<const S*>(a.table);
+    }
+    return t;
+}
+
+// ---------------------------------------------------------------------------
+// pass 1
+template <uint32_t W, typename V, bool LDS>
+__global__ __launch_bounds__(kEncWaves * 64) __attribute__((amdgpu_waves_per_eu(WIDE_BITS_WAVES, 8))) void k_wbits(WideArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t wlds[];
+    constexpr uint32_t LB = lane_bytes<W, false>(), RB = 64 * LB;
+    constexpr int N = static_cast<int>(LB / W);
+    const Tab<W, V> tab = stage_table<W, V, LDS>(a, wlds);
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63, wave = wave_index();
+    unsigned long long first_miss = ~0ull;
+    for (uint32_t c = blockIdx.x * kEncWaves + wave; c < a.nchunks; c += gridDim.x * kEncWaves) {
+        const uint64_t i0 = static_cast<uint64_t>(c) * kWideChunk;
+        const uint32_t cnt = static_cast<uint32_t>(a.n - i0 < kWideChunk ? a.n - i0 : kWideChunk);
+        const auto rin = buf_rsrc(a.in + i0 * W, (cnt * W + 15) & ~15u);
+        const uint32_t nrounds = (cnt * W + RB - 1) / RB;
+        LaneIn<LB> v0 = load_round<LB>(rin, 0, lane);
+#if WIDE_BITS_AHEAD > 1
+        LaneIn<LB> v1 = load_round<LB>(rin, 1, lane);
+#endif
+        uint32_t runacc = 0;  // lane j: the code bits of run j
+        for (uint32_t r = 0; r < nrounds; ++r) {
+            const LaneIn<LB> v = v0;
+#if WIDE_BITS_AHEAD > 1
+            v0 = v1;
+            v1 = load_round<LB>(rin, r + 2, lane);
+#else
+            v0 = load_round<LB>(rin, r + 1, lane);
+#endif
+            uint32_t w[LB / 4];
+#pragma unroll
+            for (uint32_t q = 0; q < LB / 16; ++q) {
+                w[4 * q] = v.v[q].x;
+                w[4 * q + 1] = v.v[q].y;
+                w[4 * q + 2] = v.v[q].z;
+                w[4 * q + 3] = v.v[q].w;
+            }
+            KeyT<W> key[N];
+#pragma unroll
+            for (int k = 0; k < N; ++k) key[k] = letter_of<W>(w, k);
+            V val[N];
+            lookup_n<W, V, N>(tab, key, val);
+            const uint32_t l0 = (r * RB + lane * LB) / W;  // the lane's first letter in the chunk
+            if ((r + 1) * RB > cnt * W) {  // the chunk's last round (wave-uniform): letters past the end count nothing
+#pragma unroll
+                for (int k = 0; k < N; ++k) val[k] = l0 + k < cnt ? val[k] : V(1u << 31);  // length 0, not missing
+            }
+            uint32_t bits = 0, nocode = 0;
+#pragma unroll
+            for (int k = 0; k < N; ++k) {
+                bits += len_of(val[k]);
+                nocode |= val[k] == 0 ? 1u << k : 0u;
+            }
+            if (nocode) {  // a letter without a code (rare): the lane's first one
+                const uint64_t i = i0 + l0 + static_cast<uint32_t>(__builtin_ctz(nocode));
+                first_miss = i < first_miss ? i : first_miss;
+            }
+            const uint32_t incl = wave_scan_incl(bits);
+            if constexpr (RB / W >= kSub) {
+                constexpr uint32_t RPR = RB / W / kSub;  // runs per round
+                constexpr uint32_t LPR = 64 / RPR;       // lanes per run
+                uint32_t prev = 0;
+#pragma unroll
+                for (uint32_t q = 0; q < RPR; ++q) {
+                    const uint32_t e = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(incl), (q + 1) * LPR - 1));
+                    runacc = lane == r * RPR + q ? e - prev : runacc;
+                    prev = e;
+                }
+            } else {  // a run spans several rounds
+                constexpr uint32_t RPN = kSub * W / RB;
+                const uint32_t e = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(incl), 63));
+                runacc += lane == r / RPN ? e : 0u;
+            }
+        }
+        const uint32_t incl = wave_scan_incl(runacc);
+        if (lane * kSub < cnt) a.sub_bit[static_cast<uint64_t>(c) * 64 + lane] = incl - runacc;
+        if (lane == 63) a.chunk_bits[c] = incl;
+    }
+    if (first_miss != ~0ull) atomicMin(a.first_missing, first_miss);
+}
+
+// ---------------------------------------------------------------------------
+// pass 2
+template <uint32_t W, typename V, bool LDS, int G>
+__global__ __launch_bounds__(kEncWaves * 64) void k_wpack(WideArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t wlds[];
+    constexpr bool LONG = sizeof(V) == 8;
+    constexpr uint32_t LB = lane_bytes<W, true>(), RB = 64 * LB;
+    constexpr int N = static_cast<int>(LB / W);
+    using E = Entry<LONG>;
+    const Tab<W, V> tab = stage_table<W, V, LDS>(a, wlds);
+    const uint32_t lane = threadIdx.x & 63, wave = wave_index();
+    uint32_t* stage = reinterpret_cast<uint32_t*>(wlds + (LDS ? table_lds_bytes(a.slots, a.slot_bytes) : 0u)) +
+                      wave * a.stage_words;
+    for (uint32_t i = lane; i < a.stage_words; i += 64) stage[i] = 0;
+    __syncthreads();
+    // the output as 16-byte granules: bit b of the stream is bit b + 8 mis of base
+    const uint32_t mis = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(a.out) & 15);
+    uint8_t* const base = a.out - mis;
+
+    for (uint32_t c = blockIdx.x * kEncWaves + wave; c < a.nchunks; c += gridDim.x * kEncWaves) {
+        const uint64_t i0 = static_cast<uint64_t>(c) * kWideChunk;
+        const uint32_t cnt = static_cast<uint32_t>(a.n - i0 < kWideChunk ? a.n - i0 : kWideChunk);
+        const auto rin = buf_rsrc(a.in + i0 * W, (cnt * W + 15) & ~15u);
+        const uint32_t nrounds = (cnt * W + RB - 1) / RB;
+        const uint64_t cs = a.chunk_start[c] + 8ull * mis;
+        const uint64_t ce = a.chunk_start[c + 1] + 8ull * mis;
+        uint64_t stage_bit0 = (cs >> 7) << 7;  // bit of base at stage word 0's MSB (16-B aligned)
+        const uint64_t own_lo = cs >> 3;
+        const uint64_t own_hi = (c + 1 == a.nchunks) ? (ce + 7) >> 3 : ce >> 3;
+        LaneIn<LB> v0 = load_round<LB>(rin, 0, lane);
+#if WIDE_PACK_AHEAD > 1
+        LaneIn<LB> v1 = load_round<LB>(rin, 1, lane);
+#endif
+
+        // bits of the shared first byte that belong to the letters before the chunk
+        if (lane == 0 && (cs & 7)) {
+            const int64_t floor8 = static_cast<int64_t>(cs & ~7ull);
+            int64_t pos = static_cast<int64_t>(cs);
+            for (uint64_t k = 1; k <= 8 && k <= i0 && pos > floor8; ++k) {
+                const KeyT<W> key[1] = {letter_at<W>(a.in, i0 - k)};
+                V val[1];
+                lookup_n<W, V, 1>(tab, key, val);
+                const int64_t len = static_cast<int64_t>(len_of(val[0]));
+                const uint64_t code = E::code(static_cast<typename E::T>(val[0]));
+                if (len == 0) break;
+                const int64_t start = pos - len;
+                for (int64_t q = (start > floor8 ? start : floor8); q < pos; ++q) {
+                    if ((code >> (pos - 1 - q)) & 1) {
+                        const uint64_t sb = static_cast<uint64_t>(q) - stage_bit0;
+                        stage[sb >> 5] |= 0x80000000u >> (sb & 31);
+                    }
+                }
+                pos = start;
+            }
+        }
+        wave_sync();
+
+        uint64_t round_bit = cs;
+        for (uint32_t r = 0; r < nrounds; ++r) {
+            const LaneIn<LB> v = v0;
+#if WIDE_PACK_AHEAD > 1
+            v0 = v1;
+            v1 = load_round<LB>(rin, r + 2, lane);
+#else
+            v0 = load_round<LB>(rin, r + 1, lane);
+#endif
+            uint32_t w[LB / 4];
+#pragma unroll
+            for (uint32_t q = 0; q < LB / 16; ++q) {
+                w[4 * q] = v.v[q].x;
+                w[4 * q + 1] = v.v[q].y;
+                w[4 * q + 2] = v.v[q].z;
+                w[4 * q + 3] = v.v[q].w;
+            }
+            KeyT<W> key[N];
+#pragma unroll
+            for (int k = 0; k < N; ++k) key[k] = letter_of<W>(w, k);
+            V ent[N];
+            lookup_n<W, V, N>(tab, key, ent);
+            const uint32_t l0 = (r * RB + lane * LB) / W;
+            if ((r + 1) * RB > cnt * W) {  // the chunk's last round (wave-uniform): letters past the end emit nothing
+#pragma unroll
+                for (int k = 0; k < N; ++k) ent[k] = l0 + k < cnt ? ent[k] : V(0);
+            }
+            uint32_t bits = 0;
+            uint32_t Lp[N / 2];  // pair lengths (SDWA) for the grouped emit
+            if constexpr (!LONG && G >= 2) {
+#pragma unroll
+                for (int k = 0; k < N / 2; ++k) {
+                    Lp[k] = len2(ent[2 * k], ent[2 * k + 1]);
+                    bits += Lp[k];
+                }
+            } else {
+#pragma unroll
+                for (int k = 0; k < N; ++k) bits += len_of(ent[k]);
+            }
+            const uint32_t incl = wave_scan_incl(bits);
+            const uint32_t tot = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(incl), 63));
+            const uint32_t excl = incl - bits;
+            if constexpr (LONG) {
+                if (bits) emit_codes<true, N>(stage, round_bit - stage_bit0 + excl, ent);
+            } else {
+                emit_codes_or<G, N>(stage, static_cast<uint32_t>(round_bit - stage_bit0 + excl), ent, Lp);
+            }
+            wave_order();
+
+            const uint64_t end_bit = round_bit + tot;
+            const bool last = (r + 1 == nrounds);
+            const uint32_t nseg_done = static_cast<uint32_t>((end_bit - stage_bit0) >> 7);
+            const uint32_t nseg_store = last ? static_cast<uint32_t>((end_bit - stage_bit0 + 127) >> 7) : nseg_done;
+            const uint64_t sb0 = stage_bit0 >> 3;  // byte of base at stage segment 0
+            const uint32_t full_lo = own_lo > sb0 ? static_cast<uint32_t>((own_lo - sb0 + 15) >> 4) : 0u;
+            const uint64_t hi_rel = own_hi > sb0 ? (own_hi - sb0) >> 4 : 0;
+            const uint32_t full_hi = static_cast<uint32_t>(hi_rel < 0x7FFFFFFFull ? hi_rel : 0x7FFFFFFFull);
+            for (uint32_t s = lane; s < nseg_store; s += 64)
+                store_segment(stage, s, sb0 + 16ull * s, full_lo, full_hi, own_lo, own_hi, base);
+            const uint32_t used_words = static_cast<uint32_t>((end_bit - stage_bit0 + 31) >> 5);
+            uint32_t keep = 0;
+            if (!last && lane < 4) keep = stage[nseg_done * 4 + lane];
+            wave_order();
+            for (uint32_t i = lane; i < (used_words + 3) / 4; i += 64)
+                reinterpret_cast<uint4*>(stage)[i] = make_uint4(0, 0, 0, 0);
+            wave_order();
+            if (!last) {
+                if (lane < 4) stage[lane] = keep;
+                stage_bit0 += static_cast<uint64_t>(nseg_done) << 7;
+                wave_order();
+            }
+            round_bit = end_bit;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// decode
 
 // the last partial 16 bytes of a buffer (zero past the end); out of line:
 // it runs once per stream end and would otherwise be inlined at every load
@@ -125,184 +495,12 @@ __device__ __forceinline__ uint4 load_vec(const uint8_t* __restrict__ p, uint64_
     return load_tail(p, off, nbytes);
 }
 
-// a lane's letters as 16-byte vectors, four in flight: vector q of group g
-// is handed out by take(q, g) and replaced by the load of vector q of the
-// next group (a run is 256 letters, so every group but the last is whole)
-template <uint32_t W>
-struct InRing {
-    static constexpr uint32_t L = 16 / W;
-    const uint8_t* p;
-    uint64_t base;  // byte offset of the run
-    uint32_t cnt;
-    uint64_t nbytes;
-    uint4 v[4];
-    __device__ InRing(const uint8_t* p_, uint64_t i0, uint32_t cnt_, uint64_t nbytes_)
-        : p(p_), base(i0 * W), cnt(cnt_), nbytes(nbytes_) {
-#pragma unroll
-        for (uint32_t q = 0; q < 4; ++q) v[q] = q * L < cnt ? load_vec(p, base + q * 16, nbytes) : make_uint4(0, 0, 0, 0);
-    }
-    __device__ __forceinline__ uint4 take(uint32_t q, uint32_t g) {
-        const uint4 r = v[q];
-        const uint32_t nx = g + 4 * L;
-        if (nx < cnt) v[q] = load_vec(p, base + static_cast<uint64_t>(nx) * W, nbytes);
-        return r;
-    }
-};
-
-// the table, from LDS (staged here) or global memory
-template <typename T, bool LDS, typename V>
-__device__ __forceinline__ void table(const WideArgs& a, uint64_t* lds, const KeyStore<T>*& keys, const V*& vals) {
-    if (!LDS) {
-        keys = reinterpret_cast<const KeyStore<T>*>(a.keys);
-        vals = static_cast<const V*>(a.vals);
-        return;
-    }
-    const uint32_t slots = 1u << a.log2_slots;
-    V* lv = reinterpret_cast<V*>(lds);
-    KeyStore<T>* lk = reinterpret_cast<KeyStore<T>*>(lv + slots);
-    const uint32_t vq = slots * sizeof(V) / 16, kq = slots * sizeof(KeyStore<T>) / 16;  // slots >= 64
-    for (uint32_t i = threadIdx.x; i < vq; i += kThreads)
-        reinterpret_cast<uint4*>(lv)[i] = static_cast<const uint4*>(a.vals)[i];
-    for (uint32_t i = threadIdx.x; i < kq; i += kThreads)
-        reinterpret_cast<uint4*>(lk)[i] = reinterpret_cast<const uint4*>(a.keys)[i];
-    __syncthreads();
-    keys = lk;
-    vals = lv;
+// workgroups of 256 runs (4 wide chunks)
+__device__ __forceinline__ uint32_t dec_groups(const WideDecArgs& a) {
+    return static_cast<uint32_t>((a.n + uint64_t(kThreads) * kSub - 1) / (uint64_t(kThreads) * kSub));
 }
-
-template <typename T, typename V>
-__device__ __forceinline__ void wbits_chunk(const WideArgs& a, const KeyStore<T>* keys, const V* vals, uint32_t chunk,
-                                            uint32_t* wsum) {
-    constexpr uint32_t W = sizeof(T);
-    constexpr uint32_t L = 16 / W;  // letters per 16-byte load
-    const uint32_t t = threadIdx.x;
-    const uint64_t run = static_cast<uint64_t>(chunk) * kThreads + t;
-    const uint64_t i0 = run * kSub;
-    const uint32_t cnt = i0 >= a.n ? 0u : static_cast<uint32_t>(a.n - i0 < kSub ? a.n - i0 : kSub);
-    const uint64_t nbytes = a.n * W;
-    uint32_t bits = 0;
-    InRing<W> in(a.in, i0, cnt, nbytes);
-    uint64_t miss = ~0ull;
-    for (uint32_t g = 0; g < cnt; g += 4 * L) {
-#pragma unroll
-        for (uint32_t q = 0; q < 4; ++q) {
-            const uint32_t gg = g + q * L;
-            const uint4 v = in.take(q, gg);
-            V e[L];
-            probe_vec<T, V, L>(keys, vals, a.log2_slots, a.fold, v, e);
-#pragma unroll
-            for (uint32_t j = 0; j < L; ++j) {
-                const bool ok = gg + j < cnt;
-                const uint64_t idx = i0 + gg + j;
-                miss = (ok && e[j] == 0 && idx < miss) ? idx : miss;
-                bits += ok ? static_cast<uint32_t>(e[j] & 0xFF) : 0u;
-            }
-        }
-    }
-    if (miss != ~0ull) atomicMin(a.first_missing, static_cast<unsigned long long>(miss));
-    // exclusive scan of the 256 runs' bit counts
-    const uint32_t lane = t & 63, wave = wave_index();
-    const uint32_t incl = wave_scan_incl(bits);
-    if (lane == 63) wsum[wave] = incl;
-    __syncthreads();
-    uint32_t before = 0, total = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < kThreads / 64; ++k) {
-        before += k < wave ? wsum[k] : 0u;
-        total += wsum[k];
-    }
-    if (cnt) a.sub_bit[run] = before + incl - bits;
-    if (t == 0) a.chunk_bits[chunk] = total;
-}
-
-// persistent: the table is staged once per workgroup, chunks taken in turn
-template <typename T, bool LDS, typename V>
-__global__ __launch_bounds__(kThreads) void k_wbits(WideArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
-    __shared__ uint32_t wsum[kThreads / 64];
-    const KeyStore<T>* keys;
-    const V* vals;
-    table<T, LDS, V>(a, lds, keys, vals);
-    for (uint32_t c = blockIdx.x; c < a.nchunks; c += gridDim.x) {
-        wbits_chunk<T, V>(a, keys, vals, c, wsum);
-        __syncthreads();  // wsum is reused
-    }
-}
-
-template <typename T, typename V>
-__device__ __forceinline__ void wpack_chunk(const WideArgs& a, const KeyStore<T>* keys, const V* vals, uint32_t chunk) {
-    constexpr uint32_t W = sizeof(T);
-    constexpr uint32_t L = 16 / W;
-    const uint32_t t = threadIdx.x;
-    const uint64_t run = static_cast<uint64_t>(chunk) * kThreads + t;
-    const uint64_t i0 = run * kSub;
-    if (i0 >= a.n) return;
-    const uint32_t cnt = static_cast<uint32_t>(a.n - i0 < kSub ? a.n - i0 : kSub);
-    const uint64_t nbytes = a.n * W;
-    const uint64_t start = a.chunk_start[chunk] + a.sub_bit[run];
-    uint32_t skip = (32u - static_cast<uint32_t>(start & 31)) & 31u;  // bits of the word before ours
-    uint64_t w = (start + 31) >> 5;                                    // first word we own
-    uint64_t acc = 0;
-    uint32_t nacc = 0;
-    uint32_t* __restrict__ out = a.out;
-    // append <= 32 bits; a completed word is stored; returns whether one was
-    auto append = [&](uint64_t code, uint32_t len) -> bool {
-        acc = (acc << len) | code;
-        nacc += len;
-        if (nacc < 32) return false;
-        out[w++] = __builtin_bswap32(static_cast<uint32_t>(acc >> (nacc - 32)));
-        nacc -= 32;
-        return true;
-    };
-    // a code (<= 56 bits), minus the leading bits that belong to the word before ours
-    auto put = [&](uint64_t e, bool stop_after_word) -> bool {
-        uint32_t len = static_cast<uint32_t>(e & 0xFF);
-        uint64_t code = e >> 8;
-        if (skip) {
-            if (len <= skip) {
-                skip -= len;
-                return false;
-            }
-            len -= skip;
-            code &= (1ull << len) - 1;
-            skip = 0;
-        }
-        if (len > 32) {
-            if (append(code >> 32, len - 32) && stop_after_word) return true;
-            return append(code & 0xFFFFFFFFull, 32);
-        }
-        return append(code, len);
-    };
-    InRing<W> in(a.in, i0, cnt, nbytes);
-    for (uint32_t g = 0; g < cnt; g += 4 * L) {
-#pragma unroll
-        for (uint32_t q = 0; q < 4; ++q) {
-            const uint32_t gg = g + q * L;
-            const uint4 v = in.take(q, gg);
-            if (gg < cnt) {
-                V e[L];
-                probe_vec<T, V, L>(keys, vals, a.log2_slots, a.fold, v, e);
-#pragma unroll
-                for (uint32_t j = 0; j < L; ++j) put(gg + j < cnt ? static_cast<uint64_t>(e[j]) : 0ull, false);
-            }
-        }
-    }
-    if (skip || nacc == 0) return;  // no word starts in our run, or the last one is complete
-    // complete the last word from the letters after the run (the next lanes'
-    // first bits), or pad it with zeros at the end of the stream
-    const T* letters = reinterpret_cast<const T*>(a.in);
-    for (uint64_t i = i0 + cnt; i < a.n; ++i)
-        if (put(lookup<T, V>(keys, vals, a.log2_slots, a.fold, letters[i]), true)) return;
-    out[w] = __builtin_bswap32(static_cast<uint32_t>(acc << (32 - nacc)));
-}
-
-template <typename T, bool LDS, typename V>
-__global__ __launch_bounds__(kThreads) void k_wpack(WideArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
-    const KeyStore<T>* keys;
-    const V* vals;
-    table<T, LDS, V>(a, lds, keys, vals);
-    for (uint32_t c = blockIdx.x; c < a.nchunks; c += gridDim.x) wpack_chunk<T, V>(a, keys, vals, c);
+inline uint32_t dec_groups_host(const WideDecArgs& a) {
+    return static_cast<uint32_t>((a.n + uint64_t(kThreads) * kSub - 1) / (uint64_t(kThreads) * kSub));
 }
 
 // letter j of a 16-byte vector of letters
@@ -330,7 +528,7 @@ __device__ __forceinline__ void wdecode_chunk(const WideDecArgs& a, const uint32
     const uint32_t cnt = static_cast<uint32_t>(a.n - i0 < kSub ? a.n - i0 : kSub);
     const BitSrc src{reinterpret_cast<const uint32_t*>(a.comp), a.comp, a.comp_bytes};
     T* out = reinterpret_cast<T*>(a.out) + i0;
-    uint64_t pos = a.sub_abs ? a.sub_abs[run] : a.chunk_start[chunk] + a.sub_bit[run];
+    uint64_t pos = a.sub_abs ? a.sub_abs[run] : a.chunk_start[run >> 6] + a.sub_bit[run];
     // the lane's stream through a 4 x 16-byte register ring (48 bytes in
     // flight ahead of the dword being consumed), as decode.hip k_decode
     uint4 cur, n1, n2, n3;
@@ -426,11 +624,11 @@ __global__ __launch_bounds__(kThreads) void k_wdecode(WideDecArgs a) {
         const uint32_t words = (a.nleaves * static_cast<uint32_t>(sizeof(T)) + 3) / 4;
         for (uint32_t i = threadIdx.x; i < words; i += kThreads) ll[i] = reinterpret_cast<const uint32_t*>(a.letters)[i];
         __syncthreads();
-        for (uint32_t c = blockIdx.x; c < a.nchunks; c += gridDim.x)
+        for (uint32_t c = blockIdx.x; c < dec_groups(a); c += gridDim.x)
             wdecode_chunk<T>(a, plut, reinterpret_cast<const T*>(ll), c);
     } else {
         __syncthreads();
-        for (uint32_t c = blockIdx.x; c < a.nchunks; c += gridDim.x)
+        for (uint32_t c = blockIdx.x; c < dec_groups(a); c += gridDim.x)
             wdecode_chunk<T>(a, plut, reinterpret_cast<const T*>(a.letters), c);
     }
 }
@@ -456,7 +654,7 @@ __device__ __forceinline__ void wdecode_short_chunk(const WideDecArgs& a, const 
     const uint32_t cnt = static_cast<uint32_t>(a.n - i0 < kSub ? a.n - i0 : kSub);
     T* out = reinterpret_cast<T*>(a.out) + i0;
     uint32_t* row = rows + t * kRowStride;
-    const uint64_t pos = a.sub_abs ? a.sub_abs[run] : a.chunk_start[chunk] + a.sub_bit[run];
+    const uint64_t pos = a.sub_abs ? a.sub_abs[run] : a.chunk_start[run >> 6] + a.sub_bit[run];
     uint64_t unit = pos >> 9;
     uint32_t drop = static_cast<uint32_t>(pos & 511);
     uint4 A0 = load_vec(a.comp, unit * 64 + 0, a.comp_bytes);
@@ -546,64 +744,92 @@ __global__ __launch_bounds__(kThreads) void k_wdecode_short(WideDecArgs a) {
         uint32_t* ll = plut + nprim;
         for (uint32_t i = threadIdx.x; i < lw; i += kThreads) ll[i] = reinterpret_cast<const uint32_t*>(a.letters)[i];
         __syncthreads();
-        for (uint32_t c = blockIdx.x; c < a.nchunks; c += gridDim.x)
+        for (uint32_t c = blockIdx.x; c < dec_groups(a); c += gridDim.x)
             wdecode_short_chunk<T>(a, plut, reinterpret_cast<const T*>(ll), rows, c);
     } else {
         __syncthreads();
-        for (uint32_t c = blockIdx.x; c < a.nchunks; c += gridDim.x)
+        for (uint32_t c = blockIdx.x; c < dec_groups(a); c += gridDim.x)
             wdecode_short_chunk<T>(a, plut, reinterpret_cast<const T*>(a.letters), rows, c);
     }
 }
 
+
 // persistent grid: as many 256-thread workgroups as fit on the chip at once
-// (LDS and the 8-workgroup-per-CU wave limit), at most one per chunk
-inline uint32_t grid_for(uint32_t nchunks, uint32_t cus, size_t lds) {
+// (LDS and the 8-workgroup-per-CU wave limit), at most one per group
+inline uint32_t grid_for(uint32_t ngroups, uint32_t cus, size_t lds) {
     uint32_t per_cu = 8;
     if (lds) {
         const uint32_t f = static_cast<uint32_t>((160 * 1024) / (lds + 64));
         per_cu = f < 1 ? 1 : (f < 8 ? f : 8);
     }
     const uint32_t g = (cus ? cus : 256) * per_cu;
-    return nchunks < g ? nchunks : g;
+    return ngroups < g ? ngroups : g;
 }
 
-struct BitsL {
-    template <typename T, bool LDS, typename V>
-    static void go(const WideArgs& a, size_t lds, hipStream_t s) {
-        hipLaunchKernelGGL((k_wbits<T, LDS, V>), dim3(grid_for(a.nchunks, a.cu_count, lds)), dim3(kThreads), lds, s, a);
-    }
-};
-struct PackL {
-    template <typename T, bool LDS, typename V>
-    static void go(const WideArgs& a, size_t lds, hipStream_t s) {
-        hipLaunchKernelGGL((k_wpack<T, LDS, V>), dim3(grid_for(a.nchunks, a.cu_count, lds)), dim3(kThreads), lds, s, a);
-    }
-};
+// encoder grid: 1024-thread workgroups, at most 2 per CU (32 waves), fewer
+// where the LDS table and stages do not fit twice
+inline uint32_t enc_grid(const WideArgs& a, size_t lds) {
+    const uint32_t per_cu = lds * 2 + 2048 <= 160 * 1024 ? 2u : 1u;
+    const uint32_t g = (a.cu_count ? a.cu_count : 256) * per_cu;
+    const uint32_t need = (a.nchunks + kEncWaves - 1) / kEncWaves;
+    return need < g ? need : g;
+}
 
-template <class L, typename T>
-void by_table(const WideArgs& a, hipStream_t s) {
-    const size_t lds = a.table_in_lds ? wide_table_lds_bytes(a.width, a.log2_slots, a.val32) : 0;
-    if (a.table_in_lds) {
-        if (a.val32) L::template go<T, true, uint32_t>(a, lds, s);
-        else L::template go<T, true, uint64_t>(a, lds, s);
+template <typename K>
+hipError_t allow_lds(K kernel, size_t lds) {
+    if (lds <= 64 * 1024) return hipSuccess;
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                               160 * 1024);
+}
+
+template <uint32_t W, typename V, bool LDS>
+hipError_t bits_go(const WideArgs& a, hipStream_t s) {
+    const size_t lds = wide_lds_bytes(a, false, LDS);
+    static const hipError_t attr = allow_lds(k_wbits<W, V, LDS>, 128 * 1024);
+    if (attr != hipSuccess) return attr;
+    hipLaunchKernelGGL((k_wbits<W, V, LDS>), dim3(enc_grid(a, lds)), dim3(kEncWaves * 64), lds, s, a);
+    return hipGetLastError();
+}
+
+template <uint32_t W, typename V, bool LDS, int G>
+hipError_t pack_go(const WideArgs& a, hipStream_t s) {
+    const size_t lds = wide_lds_bytes(a, true, LDS);
+    static const hipError_t attr = allow_lds(k_wpack<W, V, LDS, G>, 128 * 1024);
+    if (attr != hipSuccess) return attr;
+    hipLaunchKernelGGL((k_wpack<W, V, LDS, G>), dim3(enc_grid(a, lds)), dim3(kEncWaves * 64), lds, s, a);
+    return hipGetLastError();
+}
+
+template <uint32_t W, bool PACK>
+hipError_t enc_as(const WideArgs& a, hipStream_t s) {
+    if constexpr (!PACK) {
+        if (a.long_codes) return a.table_in_lds ? bits_go<W, uint64_t, true>(a, s) : bits_go<W, uint64_t, false>(a, s);
+        return a.table_in_lds ? bits_go<W, uint32_t, true>(a, s) : bits_go<W, uint32_t, false>(a, s);
     } else {
-        if (a.val32) L::template go<T, false, uint32_t>(a, 0, s);
-        else L::template go<T, false, uint64_t>(a, 0, s);
+        if (a.long_codes)
+            return a.table_in_lds ? pack_go<W, uint64_t, true, 1>(a, s) : pack_go<W, uint64_t, false, 1>(a, s);
+        if constexpr (W <= 4) {  // groups of codes per OR pair, as pack.hip
+            if (a.max_len <= 8)
+                return a.table_in_lds ? pack_go<W, uint32_t, true, 4>(a, s) : pack_go<W, uint32_t, false, 4>(a, s);
+            if (a.max_len <= 16)
+                return a.table_in_lds ? pack_go<W, uint32_t, true, 2>(a, s) : pack_go<W, uint32_t, false, 2>(a, s);
+        }
+        return a.table_in_lds ? pack_go<W, uint32_t, true, 1>(a, s) : pack_go<W, uint32_t, false, 1>(a, s);
     }
 }
 
-template <class L>
+template <bool PACK>
 hipError_t by_width(const WideArgs& a, hipStream_t s) {
     if (a.nchunks == 0) return hipSuccess;
+    if (a.table_in_lds && wide_lds_bytes(a, PACK, true) > kWideLdsMax) return hipErrorInvalidValue;
     switch (a.width) {
-        case 1: by_table<L, uint8_t>(a, s); break;
-        case 2: by_table<L, uint16_t>(a, s); break;
-        case 4: by_table<L, uint32_t>(a, s); break;
-        case 8: by_table<L, uint64_t>(a, s); break;
-        case 16: by_table<L, U128>(a, s); break;
+        case 1: return enc_as<1, PACK>(a, s);
+        case 2: return enc_as<2, PACK>(a, s);
+        case 4: return enc_as<4, PACK>(a, s);
+        case 8: return enc_as<8, PACK>(a, s);
+        case 16: return enc_as<16, PACK>(a, s);
         default: return hipErrorInvalidValue;
     }
-    return hipGetLastError();
 }
 
 template <typename T>
@@ -614,7 +840,7 @@ void decode_as(const WideDecArgs& a, hipStream_t s) {
     if (a.max_len <= 32) {
         const size_t rows = sizeof(T) <= 4 ? size_t(kThreads) * kRowStride * 4 : 0;
         const size_t lds = prim + (llds ? lw : 0) + rows;
-        const uint32_t g = grid_for(a.nchunks, a.cu_count, lds);
+        const uint32_t g = grid_for(dec_groups_host(a), a.cu_count, lds);
         if (llds)
             hipLaunchKernelGGL((k_wdecode_short<T, true>), dim3(g), dim3(kThreads), lds, s, a);
         else
@@ -622,20 +848,31 @@ void decode_as(const WideDecArgs& a, hipStream_t s) {
         return;
     }
     if (llds)
-        hipLaunchKernelGGL((k_wdecode<T, true>), dim3(grid_for(a.nchunks, a.cu_count, prim + lw)), dim3(kThreads),
+        hipLaunchKernelGGL((k_wdecode<T, true>), dim3(grid_for(dec_groups_host(a), a.cu_count, prim + lw)), dim3(kThreads),
                            prim + lw, s, a);
     else
-        hipLaunchKernelGGL((k_wdecode<T, false>), dim3(grid_for(a.nchunks, a.cu_count, prim)), dim3(kThreads), prim,
+        hipLaunchKernelGGL((k_wdecode<T, false>), dim3(grid_for(dec_groups_host(a), a.cu_count, prim)), dim3(kThreads), prim,
                            s, a);
 }
 
 }  // namespace
 
-hipError_t launch_wide_bits(const WideArgs& a, hipStream_t s) { return by_width<BitsL>(a, s); }
-hipError_t launch_wide_pack(const WideArgs& a, hipStream_t s) { return by_width<PackL>(a, s); }
+size_t wide_lds_bytes(const WideArgs& a, bool pack_pass, bool in_lds) {
+    return (in_lds ? table_lds_bytes(a.slots, a.slot_bytes) : 0) +
+           (pack_pass ? size_t(kEncWaves) * a.stage_words * 4 : 0);
+}
+
+uint32_t wide_stage_words(uint32_t width, uint32_t max_len) {
+    const uint32_t lb = width == 1 ? 16u : width == 2 ? WIDE_LB_PACK2 : width == 4 ? WIDE_LB_PACK4 : 32u;
+    const uint32_t letters = 64u * lb / width;  // per round
+    return (letters / 32 * (max_len ? max_len : 1) + 12 + 3) & ~3u;
+}
+
+hipError_t launch_wide_bits(const WideArgs& a, hipStream_t s) { return by_width<false>(a, s); }
+hipError_t launch_wide_pack(const WideArgs& a, hipStream_t s) { return by_width<true>(a, s); }
 
 hipError_t launch_wide_decode(const WideDecArgs& a, hipStream_t s) {
-    if (a.nchunks == 0) return hipSuccess;
+    if (a.n == 0) return hipSuccess;
     switch (a.width) {
         case 1: decode_as<uint8_t>(a, s); break;
         case 2: decode_as<uint16_t>(a, s); break;

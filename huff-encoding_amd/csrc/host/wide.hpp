@@ -82,27 +82,32 @@ private:
 };
 
 // Device tables of a wide tree.
-//  encode: two-choice cuckoo table (wide_buckets) of 2^k >= 2 * distinct
-//          slots, keys of wide_key_bytes (native layout), value
-//          (code << 8) | len (len 0 = empty); codes must fit 56 bits.
+//  encode: a two-choice cuckoo table of single-slot buckets (wide_slots):
+//          `slots` slots of slot_bytes, each {key, value} (wide_slot_layout),
+//          value 0 = empty. Short codes (<= kWideShortMax bits): value u32
+//          code << (32 - len) | len; long codes (<= 56 bits): u64
+//          code << 6 | len (the byte path's CodeTable entries, kernels.hpp).
+//          Letters are inserted shortest code first, so the frequent ones
+//          sit in their first slot and a lookup rarely needs the second.
 //  decode: primary table of 2^bits entries then 8-bit secondaries; leaf =
 //          (len << 24) | leaf index, pointer = kLutPtr | secondary offset;
 //          letters[leaf index] (W bytes each) in `letters`.
 constexpr uint32_t kWideLutPtr = 0x80000000u;  // = dev::kLutPtr
 constexpr uint32_t kWideLutMaxBits = 12;        // = dev::kLutMaxBits
 constexpr uint32_t kWideMaxDecodeLen = 57;      // = dev::kLongMaxLen
-constexpr uint32_t kWideMaxEncodeLen = 56;      // (code << 8) | len in a u64
+constexpr uint32_t kWideMaxEncodeLen = 56;      // code << 6 | len in a u64 (= dev::kLongMaxLen - 1)
+constexpr uint32_t kWideShortMax = 27;          // = dev::kShortMaxLen
 constexpr uint64_t kWideFold0 = 0xC2B2AE3D27D4EB4Full;
 
 struct WideEncTables {
     uint32_t width = 1;
-    uint32_t log2_slots = 0;     // slots = 2 * buckets
-    // 16-byte keys fold to lo ^ hi * fold before hashing; distinct keys that
-    // fold alike under one multiplier separate under another (re-seeded)
-    uint64_t fold = kWideFold0;
-    std::vector<uint8_t> keys;   // slots * wide_key_bytes(width)
-    std::vector<uint64_t> vals;  // slots
-    std::vector<uint32_t> vals32;  // the same when every code has <= 24 bits (else empty)
+    uint32_t slots = 0;
+    uint32_t slot_bytes = 8;
+    uint32_t val_off = 4;
+    uint32_t mul1 = 0;            // odd hash multiplier (wide_slots)
+    uint64_t fold = kWideFold0;   // 8- and 16-byte keys: 64-bit fold multiplier (wide_hkey)
+    bool long_codes = false;
+    std::vector<uint8_t> table;   // slots * slot_bytes
     uint32_t maxlen = 0;
     size_t distinct = 0;
 };
@@ -112,22 +117,33 @@ struct WideDecTables {
     std::vector<uint8_t> letters;  // leaves * W
 };
 
-// Two-choice cuckoo table for encode: buckets of 2 slots (slot = 2 b + j);
-// a key lives in one of the slots of bucket b1 or b2, so a lookup is four
-// fixed loads and no loop. Keys of <= 4 bytes are stored as u32. Same hashes
-// on host and device (device/wide.hip buckets_of).
+// Slot layout: the key at offset 0 (keys of <= 4 bytes as u32, native
+// little-endian), the value at val_off, slots of 8 bytes ({u32 key, u32
+// value}) or multiples of 16. Same layout as device/wide.hip Slot<>. An
+// empty slot holds value 0 and a key that is no letter of the table, so a
+// key match alone finds a letter.
 inline uint32_t wide_key_bytes(uint32_t width) { return width < 4 ? 4 : width; }
-inline void wide_buckets(uint64_t lo, uint64_t hi, uint32_t lgb, uint32_t width, uint64_t fold, uint32_t* b1,
-                         uint32_t* b2) {
-    if (width <= 4) {
-        const uint32_t x = static_cast<uint32_t>(lo);
-        *b1 = static_cast<uint32_t>((static_cast<uint64_t>(x * 0x9E3779B1u)) >> (32 - lgb));
-        *b2 = static_cast<uint32_t>((static_cast<uint64_t>(x * 0x85EBCA77u + 0x165667B1u)) >> (32 - lgb));
-        return;
-    }
-    const uint64_t k = lo ^ (hi * fold);
-    *b1 = static_cast<uint32_t>((k * 0x9E3779B97F4A7C15ull) >> (64 - lgb));
-    *b2 = static_cast<uint32_t>((k * 0xD6E8FEB86659FD93ull + 0x165667B19E3779F9ull) >> (64 - lgb));
+inline void wide_slot_layout(uint32_t width, bool long_codes, uint32_t* val_off, uint32_t* slot_bytes) {
+    const uint32_t kb = wide_key_bytes(width), vb = long_codes ? 8 : 4;
+    *val_off = (kb + vb - 1) / vb * vb;
+    *slot_bytes = kb + vb <= 8 ? 8 : (*val_off + vb + 15) / 16 * 16;
+}
+// The 32-bit hash key of a letter: the letter itself for <= 4 bytes, else
+// the high half of a 64-bit multiply (16-byte letters fold lo ^ hi * fold
+// first). Letters with equal hash keys share both slots, so at most two of
+// them fit: the builder re-seeds `fold` when that fails.
+inline uint32_t wide_hkey(uint64_t lo, uint64_t hi, uint32_t width, uint64_t fold) {
+    if (width <= 4) return static_cast<uint32_t>(lo);
+    const uint64_t k = width == 16 ? lo ^ (hi * fold) : lo;
+    return static_cast<uint32_t>((k * fold) >> 32);
+}
+// The two slots of a hash key: s1 = the high half of (x * mul) * slots;
+// s2 = s1 + 1 + bits 8..15 of x * mul, modulo slots (slots > 256)
+inline void wide_slots(uint32_t x, uint32_t mul, uint32_t slots, uint32_t* s1, uint32_t* s2) {
+    const uint32_t h = x * mul;
+    *s1 = static_cast<uint32_t>((static_cast<uint64_t>(h) * slots) >> 32);
+    const uint32_t t = *s1 + ((h >> 8) & 255u) + 1u;
+    *s2 = t < slots ? t : t - slots;
 }
 
 Status build_wide_enc_tables(const WideTree& t, WideEncTables& out);

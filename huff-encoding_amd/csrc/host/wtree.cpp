@@ -3,6 +3,7 @@
 // Same algorithm as tree.cpp (tree_inner.rs:281-320 over the Rust std heap,
 // rust_heap.hpp), with W-byte letters and an unbounded number of leaves.
 #include <algorithm>
+#include <cstring>
 
 #include "rust_heap.hpp"
 #include "wide.hpp"
@@ -199,76 +200,99 @@ Status build_wide_enc_tables(const WideTree& t, WideEncTables& out) {
     if (maxlen > kWideMaxEncodeLen)
         return Status::err(HUFF_E_CODE_TOO_LONG, "code longer than 56 bits: outside the GPU encoder's range");
     const uint32_t W = t.width();
-    const uint32_t KB = wide_key_bytes(W);
     out.width = W;
     out.maxlen = maxlen;
     out.distinct = codes.size();
-    // buckets of 2 slots, load <= 1/2; grow (at most 16x) until every key is
-    // placed. Keys of <= 8 bytes hash injectively, so they separate within
-    // that; 16-byte keys fold to 64 bits first, and letters whose folds
-    // collide never separate by growing: then re-seed the fold multiplier
-    uint32_t lgb0 = 5;
-    while ((2ull << lgb0) < 2 * codes.size()) ++lgb0;
-    struct Ent {
-        u128 key;
-        uint64_t val;
-        bool used;
+    out.long_codes = maxlen > kWideShortMax;
+    wide_slot_layout(W, out.long_codes, &out.val_off, &out.slot_bytes);
+    // shortest code (most frequent letter) first: it takes its first slot
+    std::stable_sort(codes.begin(), codes.end(), [](const WideLeaf& x, const WideLeaf& y) { return x.len < y.len; });
+    const size_t D = codes.size();
+    std::vector<uint32_t> hk(D), s1(D), s2(D);
+    std::vector<int32_t> occ;
+    // load <= 4/9 (two-choice cuckoo with single-slot buckets places every
+    // key below 1/2 with high probability); a failed build re-seeds the hash
+    // multipliers (and the fold of wide keys), every 8th failure grows the
+    // table by 1/8
+    uint64_t M = std::max<uint64_t>(512, (D * 9 + 3) / 4);
+    uint64_t seed = 0;
+    auto mix = [](uint64_t z) {  // splitmix64
+        z += 0x9E3779B97F4A7C15ull;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        return z ^ (z >> 31);
     };
-    std::vector<Ent> slot;
-    uint64_t rng = 0x9E3779B97F4A7C15ull;
-    uint64_t fold = kWideFold0, seed = 0;
-    const uint32_t lg_cap = std::min<uint32_t>(lgb0 + 4, 31);
-    uint32_t lgb = lgb0;
-    for (;; ++lgb) {
-        if (lgb > lg_cap) {
-            if (W <= 8 || ++seed > 64)
-                return Status::err(HUFF_E_INVALID_ARG, "letters do not separate in the encoder's hash table");
-            uint64_t z = (seed * 0x9E3779B97F4A7C15ull) ^ kWideFold0;  // splitmix64 of the seed
-            z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-            z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-            fold = (z ^ (z >> 31)) | 1u;
-            lgb = lgb0;
+    for (uint32_t attempt = 0;; ++attempt) {
+        if (attempt == 256 || M >= (1ull << 31))
+            return Status::err(HUFF_E_INVALID_ARG, "letters do not separate in the encoder's hash table");
+        if (attempt && attempt % 8 == 0) M += M / 8;
+        const uint64_t z = mix(++seed);
+        out.mul1 = static_cast<uint32_t>(z) | 1u;
+        out.fold = attempt == 0 ? kWideFold0 : (mix(seed ^ kWideFold0) | 1u);
+        out.slots = static_cast<uint32_t>(M);
+        for (size_t i = 0; i < D; ++i) {
+            hk[i] = wide_hkey(static_cast<uint64_t>(codes[i].letter), static_cast<uint64_t>(codes[i].letter >> 64), W,
+                              out.fold);
+            wide_slots(hk[i], out.mul1, out.slots, &s1[i], &s2[i]);
         }
-        slot.assign(size_t(2) << lgb, Ent{0, 0, false});
+        occ.assign(M, -1);
         bool ok = true;
-        for (const WideLeaf& c : codes) {
-            Ent cur{c.letter, (c.code << 8) | c.len, true};
-            bool placed = false;
-            for (int kick = 0; kick < 1000 && !placed; ++kick) {
-                uint32_t b[2];
-                wide_buckets(static_cast<uint64_t>(cur.key), static_cast<uint64_t>(cur.key >> 64), lgb, W, fold, &b[0],
-                             &b[1]);
-                for (int q = 0; q < 4 && !placed; ++q) {
-                    Ent& e = slot[2 * b[q >> 1] + (q & 1)];
-                    if (!e.used) {
-                        e = cur;
-                        placed = true;
-                    }
-                }
-                if (placed) break;
-                rng ^= rng << 13;
-                rng ^= rng >> 7;
-                rng ^= rng << 17;
-                std::swap(cur, slot[2 * b[rng & 1] + ((rng >> 1) & 1)]);  // evict, re-place the evicted
+        for (size_t i = 0; i < D && ok; ++i) {
+            if (occ[s1[i]] < 0) {
+                occ[s1[i]] = static_cast<int32_t>(i);
+                continue;
             }
-            if (!placed) {
-                ok = false;
-                break;
+            if (occ[s2[i]] < 0) {
+                occ[s2[i]] = static_cast<int32_t>(i);
+                continue;
+            }
+            // evict along the walk: the evicted key moves to its other slot
+            int32_t cur = static_cast<int32_t>(i);
+            uint32_t pos = s1[i];
+            ok = false;
+            for (int kick = 0; kick < 512; ++kick) {
+                std::swap(cur, occ[pos]);
+                const uint32_t alt = s1[cur] == pos ? s2[cur] : s1[cur];
+                if (occ[alt] < 0) {
+                    occ[alt] = cur;
+                    ok = true;
+                    break;
+                }
+                pos = alt;
             }
         }
         if (ok) break;
     }
-    out.log2_slots = lgb + 1;
-    out.fold = fold;
-    out.keys.assign(slot.size() * KB, 0);
-    out.vals.assign(slot.size(), 0);
-    for (size_t i = 0; i < slot.size(); ++i) {
-        if (!slot[i].used) continue;
-        store_letter(&out.keys[i * KB], W, slot[i].key);
-        out.vals[i] = slot[i].val;
+    out.table.assign((static_cast<size_t>(M) * out.slot_bytes + 15) / 16 * 16, 0);  // staged in 16-B pieces
+    // the empty slots' key: the smallest value that is no letter (keys of
+    // <= 2 bytes: 2^32 - 1, above every letter)
+    u128 empty = ~u128(0) >> (128 - 8 * wide_key_bytes(W));
+    if (W > 2) {
+        std::vector<u128> ls(D);
+        for (size_t i = 0; i < D; ++i) ls[i] = codes[i].letter;
+        std::sort(ls.begin(), ls.end());
+        empty = 0;
+        for (const u128& l : ls) {
+            if (l != empty) break;
+            ++empty;
+        }
     }
-    out.vals32.clear();
-    if (maxlen <= 24) out.vals32.assign(out.vals.begin(), out.vals.end());
+    for (uint64_t sl = 0; sl < M; ++sl) {
+        if (occ[sl] < 0) {
+            store_letter(&out.table[sl * out.slot_bytes], wide_key_bytes(W), empty);
+            continue;
+        }
+        const WideLeaf& c = codes[occ[sl]];
+        uint8_t* p = &out.table[sl * out.slot_bytes];
+        store_letter(p, W, c.letter);  // u32 keys: bytes W..3 stay zero
+        if (out.long_codes) {
+            const uint64_t v = (c.code << 6) | c.len;
+            std::memcpy(p + out.val_off, &v, 8);
+        } else {
+            const uint32_t v = static_cast<uint32_t>(c.code << (32 - c.len)) | c.len;
+            std::memcpy(p + out.val_off, &v, 4);
+        }
+    }
     return Status::ok();
 }
 

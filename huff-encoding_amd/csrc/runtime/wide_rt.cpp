@@ -56,7 +56,7 @@ Status huff_wenc::init(huff_ctx* c, uint32_t w, const uint8_t* d, uint64_t nlett
     width = w;
     d_in = d;
     n = nletters;
-    nchunks = static_cast<uint32_t>((n + huff::dev::kChunk - 1) / huff::dev::kChunk);
+    nchunks = static_cast<uint32_t>((n + huff::dev::kWideChunk - 1) / huff::dev::kWideChunk);
     HUFF_TRY(chunk_bits.ensure((nchunks + 1) * 8));
     HUFF_TRY(chunk_start.ensure((nchunks + 2) * 8));
     HUFF_TRY(tsum.ensure((nchunks / 1024 + 2) * 8));
@@ -65,34 +65,37 @@ Status huff_wenc::init(huff_ctx* c, uint32_t w, const uint8_t* d, uint64_t nlett
     return Status::ok();
 }
 
+huff::dev::WideArgs huff_wenc::enc_args(bool pack_pass) const {
+    huff::dev::WideArgs a{};
+    a.in = d_in;
+    a.n = n;
+    a.width = width;
+    a.table = table.p;
+    a.slots = et->slots;
+    a.slot_bytes = et->slot_bytes;
+    a.mul1 = et->mul1;
+    a.fold = et->fold;
+    a.long_codes = et->long_codes;
+    a.max_len = et->maxlen;
+    a.nchunks = nchunks;
+    a.cu_count = static_cast<uint32_t>(ctx->cu_count);
+    a.stage_words = huff::dev::wide_stage_words(width, et->maxlen);
+    a.table_in_lds = huff::dev::wide_lds_bytes(a, pack_pass, true) <= huff::dev::kWideLdsMax;
+    return a;
+}
+
 Status huff_wenc::bits(const huff_wtree* t, uint64_t* total, huff::u128* missing_letter) {
     HUFF_TRY(ctx->activate());
     HUFF_TRY(t->enc_tables(&et));
     if (et->width != width) return Status::err(HUFF_E_INVALID_ARG, "the tree's letter width differs from the job's");
     hipStream_t s = ctx->stream;
     if (enc_tree != t->id) {
-        HUFF_TRY(keys.ensure(et->keys.size()));
-        HUFF_TRY(vals.ensure(et->vals.size() * 8));
-        HIP_TRY(hipMemcpyAsync(keys.p, et->keys.data(), et->keys.size(), hipMemcpyHostToDevice, s));
-        if (!et->vals32.empty())
-            HIP_TRY(hipMemcpyAsync(vals.p, et->vals32.data(), et->vals32.size() * 4, hipMemcpyHostToDevice, s));
-        else
-            HIP_TRY(hipMemcpyAsync(vals.p, et->vals.data(), et->vals.size() * 8, hipMemcpyHostToDevice, s));
+        HUFF_TRY(table.ensure(et->table.size()));
+        HIP_TRY(hipMemcpyAsync(table.p, et->table.data(), et->table.size(), hipMemcpyHostToDevice, s));
         enc_tree = t->id;
     }
     HIP_TRY(hipMemsetAsync(missing.p, 0xFF, 8, s));
-    huff::dev::WideArgs a{};
-    a.in = d_in;
-    a.n = n;
-    a.width = width;
-    a.log2_slots = et->log2_slots;
-    a.fold = et->fold;
-    a.keys = static_cast<const uint8_t*>(keys.p);
-    a.vals = vals.p;
-    a.val32 = !et->vals32.empty();
-    a.table_in_lds = huff::dev::wide_table_lds_bytes(width, et->log2_slots, a.val32) <= kTableLdsMax;
-    a.nchunks = nchunks;
-    a.cu_count = static_cast<uint32_t>(ctx->cu_count);
+    huff::dev::WideArgs a = enc_args(false);
     a.chunk_bits = static_cast<uint64_t*>(chunk_bits.p);
     a.sub_bit = static_cast<uint32_t*>(sub_bit.p);
     a.first_missing = static_cast<unsigned long long*>(missing.p);
@@ -121,24 +124,11 @@ Status huff_wenc::bits(const huff_wtree* t, uint64_t* total, huff::u128* missing
 Status huff_wenc::pack(const huff_wtree* t, uint8_t* d_out, size_t out_cap, uint64_t* total) {
     if (bits_tree != t->id) HUFF_TRY(bits(t, nullptr, nullptr));
     if (total) *total = total_bits;
-    const uint64_t need = (total_bits + 31) / 32 * 4;
+    const uint64_t need = (total_bits + 7) / 8;
     if (out_cap < need) return Status::err(HUFF_E_BUFFER_TOO_SMALL, "output buffer too small");
-    if (reinterpret_cast<uintptr_t>(d_out) & 3) return Status::err(HUFF_E_INVALID_ARG, "output must be 4-byte aligned");
-    huff::dev::WideArgs a{};
-    a.in = d_in;
-    a.n = n;
-    a.width = width;
-    a.log2_slots = et->log2_slots;
-    a.fold = et->fold;
-    a.keys = static_cast<const uint8_t*>(keys.p);
-    a.vals = vals.p;
-    a.val32 = !et->vals32.empty();
-    a.table_in_lds = huff::dev::wide_table_lds_bytes(width, et->log2_slots, a.val32) <= kTableLdsMax;
-    a.nchunks = nchunks;
-    a.cu_count = static_cast<uint32_t>(ctx->cu_count);
+    huff::dev::WideArgs a = enc_args(true);
     a.chunk_start = static_cast<const uint64_t*>(chunk_start.p);
-    a.sub_bit = static_cast<uint32_t*>(sub_bit.p);
-    a.out = reinterpret_cast<uint32_t*>(d_out);
+    a.out = d_out;
     hipStream_t s = ctx->stream;
     return ctx->timed("wpack", [&] { return huff::dev::launch_wide_pack(a, s); });
 }

@@ -42,7 +42,7 @@ struct huff_wenc {
     uint32_t width = 1;
     uint32_t nchunks = 0;
     DevBuf chunk_bits, chunk_start, tsum, sub_bit, missing;
-    DevBuf keys, vals, lut, letters;  // device tables of the last trees used
+    DevBuf table, lut, letters;  // device tables of the last trees used
     uint64_t enc_tree = 0, dec_tree = 0;
     const huff::WideEncTables* et = nullptr;
     const huff::WideDecTables* dt = nullptr;
@@ -50,6 +50,7 @@ struct huff_wenc {
     uint64_t total_bits = 0;
 
     huff::Status init(huff_ctx* c, uint32_t w, const uint8_t* d, uint64_t nletters);
+    huff::dev::WideArgs enc_args(bool pack_pass) const;  // the table and job fields of a pass
     // pass A; a letter without a code -> HUFF_E_MISSING_LETTER, its value in *missing
     huff::Status bits(const huff_wtree* t, uint64_t* total, huff::u128* missing);
     huff::Status pack(const huff_wtree* t, uint8_t* d_out, size_t out_cap, uint64_t* total);

@@ -97,6 +97,8 @@ SIGNATURES = [
     ("huff_enc_compress", i, [vp, vp, sz, C.POINTER(vp), u64p]),
     ("huff_enc_decode", i, [vp, vp, vp, vp]),
     ("huff_dev_decompress", i, [vp, vp, vp, sz, C.c_uint8, vp, sz, szp]),
+    ("huff_batch_hist", i, [vp, vp, vp, C.c_uint32, vp]),
+    ("huff_batch_trees", i, [vp, vp, C.c_uint32, vp, sz, vp, vp, vp, vp]),
     ("huff_comm_unique_id", i, [vp]),
     ("huff_comm_init", i, [vp, vp, i, i, C.POINTER(vp)]),
     ("huff_comm_free", None, [vp]),

@@ -272,6 +272,28 @@ int huff_mgpu_pack_rows(huff_enc* e, const int64_t* rows, int world, int rank, u
 int huff_dev_decompress(huff_ctx* ctx, const huff_tree* t, const uint8_t* d_comp, size_t comp_bytes,
                         uint8_t padding, uint8_t* d_out, size_t out_cap, size_t* n_out);
 
+/* Many small byte streams at once (device pointers, one
+ * launch each, synchronous):
+ *  huff_batch_hist:  d_hist[s][256] = the byte weights (ByteWeights::from
+ *                    of the bytes, weights.rs:196-208) of stream s =
+ *                    d_in[d_offsets[s], d_offsets[s + 1]).
+ *  huff_batch_trees: HuffTree::from_weights of each d_hist[s] (tree_inner.rs:
+ *                    281-320, with the reference's exact BinaryHeap tie order)
+ *                    -> d_tree_bits + s * tree_stride: as_bin (tree_inner.rs:
+ *                    637-663), MSB first, d_tree_nbits[s] bits; d_codes[s][l] =
+ *                    code << 8 | len of letter l (0: no code); d_max_len[s];
+ *                    d_status[s] = HUFF_OK, HUFF_E_EMPTY_WEIGHTS (all weights
+ *                    zero: "provided empty weights") or HUFF_E_CODE_TOO_LONG (a
+ *                    code longer than 56 bits: its d_codes entry is 0; the
+ *                    tree bits are complete). tree_stride >=
+ *                    HUFF_TREE_BITS_MAX_BYTES; per-stream weights < 2^54. */
+#define HUFF_TREE_BITS_MAX_BYTES 322
+int huff_batch_hist(huff_ctx* ctx, const uint8_t* d_in, const uint64_t* d_offsets, uint32_t nstreams,
+                    uint64_t* d_hist);
+int huff_batch_trees(huff_ctx* ctx, const uint64_t* d_hist, uint32_t nstreams, uint8_t* d_tree_bits,
+                     size_t tree_stride, uint32_t* d_tree_nbits, uint64_t* d_codes, uint32_t* d_max_len,
+                     uint32_t* d_status);
+
 /* synthetic inputs generated on the device (not reference functions):
  * kind 0 = uniform bytes, 1 = Zipf(alpha) with cdf[256] (host), 2 = text.
  * Byte i of the stream depends only on (kind, seed, offset + i). */

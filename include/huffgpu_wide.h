@@ -91,7 +91,7 @@ int huff_wenc_create(huff_ctx* ctx, uint32_t width, const void* d_in, size_t n, 
 void huff_wenc_free(huff_wenc* e);
 /* pass A: code lengths, restart index; *total_bits */
 int huff_wenc_bits(huff_wenc* e, const huff_wtree* t, uint64_t* total_bits);
-/* pass B into d_out (4-byte aligned, out_cap >= 4 * ceil(bits / 32)) */
+/* pass B into d_out (any alignment, out_cap >= ceil(bits / 8)) */
 int huff_wenc_pack(huff_wenc* e, const huff_wtree* t, uint8_t* d_out, size_t out_cap, uint64_t* total_bits);
 /* restart-index decode of this job's pack output into d_out (n * width bytes) */
 int huff_wenc_decode(huff_wenc* e, const huff_wtree* t, const uint8_t* d_comp, uint8_t* d_out);

@@ -12,7 +12,9 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 
-LENGTHS = [1, 2, 7, 255, 256, 257, 4095, 65535, 65536, 65537, 65536 * 3 + 1001, 400_003]
+# around the encoder's wide chunk (16,384 letters, one wave) and the 256-run
+# decoder groups
+LENGTHS = [1, 2, 7, 255, 256, 257, 4095, 16383, 16384, 16385, 65535, 65536, 65537, 65536 * 3 + 1001, 400_003]
 
 
 @pytest.fixture(scope="module")
@@ -153,27 +155,74 @@ def test_single_letter_and_empty(W, ctx):
         W.compress_with_tree(np.zeros(0, np.int32), t, ctx)
 
 
-def test_long_codes(W, O, ctx):
-    """Fibonacci weights give codes up to 39 bits: the > 32-bit split in the
-    packer and the secondary tables in the decoder; the index-free decoder
-    refuses them (> 32 bits) with CODE_TOO_LONG"""
+@pytest.mark.parametrize("dtype", [np.uint8, np.uint16, np.int32, np.uint64])
+def test_long_codes(W, O, ctx, dtype):
+    """Fibonacci weights give codes up to 39 bits: u64 table values (the
+    > 32-bit split in the packer) and the secondary tables in the decoder;
+    the index-free decoder refuses them (> 32 bits) with CODE_TOO_LONG"""
     import huff_coding as H
 
     fib = [1, 1]
     while len(fib) < 40:
         fib.append(fib[-1] + fib[-2])
-    items = [(1000 + i, f) for i, f in enumerate(fib)]
-    t = W.WideTree.from_weights(items, np.uint16)
+    items = [(100 + i, f) for i, f in enumerate(fib)]
+    t = W.WideTree.from_weights(items, dtype)
     assert max(len(c) for c in t.read_codes().values()) == 39
     rng = np.random.default_rng(9)
-    letters = (1000 + rng.integers(0, 40, 300_000)).astype(np.uint16)
+    letters = (100 + rng.integers(0, 40, 300_000)).astype(dtype)
     cd = W.compress_with_tree(letters, t, ctx)
-    (ocomp, opad), _ = oracle_stream(O, letters, items, 16)
+    (ocomp, opad), _ = oracle_stream(O, letters, items, 8 * np.dtype(dtype).itemsize)
     assert cd.comp_bytes() == ocomp and cd.padding_bits() == opad
     assert np.array_equal(W.decompress(cd, ctx), letters)
     with pytest.raises(H.HuffError) as e:
-        W.decompress(W.WideCompressData.try_from_bytes(cd.to_bytes(), np.uint16), ctx)
+        W.decompress(W.WideCompressData.try_from_bytes(cd.to_bytes(), dtype), ctx)
     assert e.value.code == 7
+
+
+@pytest.mark.parametrize("dtype,k", [(np.uint32, 40_000), (np.uint16, 65536), (np.uint64, 20_000)])
+def test_large_alphabet_table_in_hbm(W, O, ctx, dtype, k):
+    """alphabets whose code table exceeds the LDS budget (kWideLdsMax):
+    the encoder reads the table from L2; every u16 letter present (the
+    table's empty slot key 0 is a real letter)"""
+    rng = np.random.default_rng(k)
+    if dtype == np.uint16:
+        letters = np.concatenate([np.arange(65536, dtype=np.uint16), rng.integers(0, 65536, 200_000, dtype=np.uint16)])
+        rng.shuffle(letters)
+    else:
+        letters = zipf_letters(rng, 300_001, dtype, k=k)
+        letters[:k // 4] = np.arange(k // 4, dtype=dtype)  # 0 and other small keys
+    wmap = W.build_weights_map(letters, ctx)
+    items = list(wmap.items())
+    t = W.WideTree.from_weights(items, dtype)
+    cd = W.compress_with_tree(letters, t, ctx)
+    (ocomp, opad), _ = oracle_stream(O, letters, items, 8 * np.dtype(dtype).itemsize)
+    assert cd.comp_bytes() == ocomp and cd.padding_bits() == opad
+    assert np.array_equal(W.decompress(cd, ctx), letters)
+
+
+@pytest.mark.parametrize("dtype", [np.uint8, np.uint16, np.int32, np.int64])
+def test_device_pack_any_alignment(W, O, ctx, dtype):
+    """pass 2 into an output at every offset mod 16: the bytes equal the
+    oracle's stream, and no byte outside [off, off + ceil(bits / 8)) changes"""
+    import torch
+
+    rng = np.random.default_rng(np.dtype(dtype).itemsize)
+    n = 3 * 16384 + 77
+    letters = zipf_letters(rng, n, dtype, k=200 if dtype == np.uint8 else 3000)
+    items = list(W.build_weights_map(letters, ctx).items())
+    t = W.WideTree.from_weights(items, dtype)
+    (ocomp, opad), _ = oracle_stream(O, letters, items, 8 * np.dtype(dtype).itemsize)
+    x = torch.from_numpy(letters.copy()).cuda()
+    job = W.WideEncodeJob(ctx, np.dtype(dtype).itemsize, x.data_ptr(), n)
+    bits = job.bits(t)
+    nb = (bits + 7) // 8
+    assert nb == len(ocomp)
+    for off in (0, 1, 3, 4, 8, 13, 15):
+        buf = torch.full((nb + 64,), 0xAB, dtype=torch.uint8, device="cuda")
+        assert job.pack(t, buf.data_ptr() + off, nb) == bits
+        got = buf.cpu().numpy()
+        assert got[off:off + nb].tobytes() == ocomp, off
+        assert (got[:off] == 0xAB).all() and (got[off + nb:] == 0xAB).all(), off
 
 
 def test_device_job_large(W, ctx):

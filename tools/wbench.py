@@ -85,10 +85,13 @@ def main():
         ms, c = ctx.kernel_time(kname)
         if c:
             avg = ms / c
+            gbps = b / (avg * 1e-3) / 1e9 if b else None
             res["kernels"][kname] = {"avg_ms": round(avg, 4), "algo_bytes": b,
-                                     "GBps": round(b / (avg * 1e-3) / 1e9, 1) if b else None}
+                                     "GBps": round(gbps, 1) if b else None,
+                                     "frac_of_8TBps": round(gbps / 8000, 4) if b else None}
     enc_ms = sum(res["kernels"][k]["avg_ms"] for k in ("wbits", "wscan", "wpack"))
     res["encode_GBps_input"] = round(nbytes / (enc_ms * 1e-3) / 1e9, 1)
+    res["encode_frac_input"] = round(nbytes / (enc_ms * 1e-3) / 1e9 / 8000, 4)
     res["decode_GBps_input"] = round(nbytes / (res["kernels"]["wdecode"]["avg_ms"] * 1e-3) / 1e9, 1)
     if args.indexless:
         pad = (8 - bits % 8) % 8
