@@ -230,6 +230,7 @@ struct WideArgs {
     // {key, value}; a letter's slots are wide_slots(wide_hkey(letter))
     const void* table;
     uint32_t slots, slot_bytes, mul1;
+    uint32_t hash_mode;           // host/wide.hpp WideHash (0 generic, 1 narrow, 2 direct)
     uint64_t fold;
     uint32_t long_codes;          // values u64 code << 6 | len, else u32 code << (32 - len) | len
     uint32_t max_len;
@@ -293,7 +294,7 @@ enum : uint32_t { kTreeOk = 0, kTreeEmpty = 2, kTreeDeep = 7 };  // = HUFF_OK, H
 struct TreeBatchArgs {
     const uint64_t* hist;   // [nstreams][256] byte weights
     uint32_t nstreams;
-    uint8_t* tree_bits;     // [nstreams][tree_stride]: as_bin (tree_inner.rs:637-663), MSB first
+    uint8_t* tree_bits;     // [nstreams][tree_stride]: as_bin (tree_inner.rs:632-663), MSB first
     uint32_t tree_stride;   // >= kTreeBitsMaxBytes
     uint32_t* tree_nbits;   // [nstreams]
     uint64_t* codes;        // [nstreams][256]: code << 8 | len; 0 = no code (or longer than kTreeCodeMax)

@@ -6,7 +6,7 @@
 // weight order (branch_heap.rs:18-83 over std's sift_up /
 // sift_down_to_bottom; host/rust_heap.hpp), two minima popped per merge
 // (tree_inner.rs:289-306), codes and as_bin in preorder (tree_inner.rs:313-
-// 320, 637-663).
+// 320, 632-663).
 //
 // The heap is inherently serial, so the parallelism is across streams: one
 // lane per stream, kTreeLanes streams per workgroup, each stream's heap,
@@ -141,21 +141,29 @@ __global__ __launch_bounds__(kTreeLanes) void k_tree_batch(TreeBatchArgs a) {
     uint64_t* codes = a.codes + static_cast<uint64_t>(s) * 256;
     for (uint32_t b = 0; b < 256; ++b) codes[b] = 0;
 
-    // leaves in ByteWeights::iter order (host/weights.cpp)
+    // leaves in ByteWeights::iter order (host/weights.cpp); the row is read
+    // 16 weights at a time (independent loads in flight, not one latency per bin)
     LaneHeap hp{heap, lane};
     uint32_t nl = 0;
     int last = -1;
-    for (uint32_t b = 0; b < 256; ++b) {
-        const uint64_t w = h[b];
-        if (w == 0) continue;
-        leaf[nl][lane] = static_cast<uint8_t>(b);
-        hp.push((w << kNodeBits) | nl);
-        ++nl;
-        last = static_cast<int>(b);
+    uint64_t w0 = 0;
+    for (uint32_t b0 = 0; b0 < 256; b0 += 16) {
+        uint64_t w[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) w[j] = h[b0 + j];
+        if (b0 == 0) w0 = w[0];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            if (w[j] == 0) continue;
+            leaf[nl][lane] = static_cast<uint8_t>(b0 + j);
+            hp.push((w[j] << kNodeBits) | nl);
+            ++nl;
+            last = static_cast<int>(b0 + j);
+        }
     }
-    if (h[0] != 0 && last != 255) {
+    if (w0 != 0 && last != 255) {
         leaf[nl][lane] = 0;
-        hp.push((h[0] << kNodeBits) | nl);
+        hp.push((w0 << kNodeBits) | nl);
         ++nl;
     }
     if (nl == 0) {  // tree_inner.rs:283-285

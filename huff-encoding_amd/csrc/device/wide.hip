@@ -111,20 +111,32 @@ __device__ __forceinline__ uint32_t hkey(KeyT<W> k, uint64_t fold) {
     }
 }
 
-// host/wide.hpp wide_slots: s1 = the high half of (x * mul) * slots; s2 =
-// s1 + 1 + bits 8..15 of x * mul, modulo slots (one quarter-rate multiply
-// pair per letter, the second slot from full-rate ops)
-__device__ __forceinline__ void wslots(uint32_t x, uint32_t mul, uint32_t slots, uint32_t& s1, uint32_t& s2) {
-    const uint32_t h = x * mul;
-    s1 = __umulhi(h, slots);
-    const uint32_t t = s1 + ((h >> 8) & 255u) + 1u;
-    s2 = min(t, t - slots);  // t < slots: t; else t - slots (t - slots wraps above t otherwise)
+// host/wide.hpp wide_slots. Generic: h = x * mul, s1 = high half of h *
+// slots (two quarter-rate multiplies). Narrow (keys < 2^16, slots < 65536):
+// h = x * mul on 24 bits, s1 = ((h >> 8) * (slots << 8)) >> 32, both full-rate
+// 24-bit multiplies. s2 = s1 ^ bits 8..15 of h (slots a multiple of 256).
+// Direct (keys < 2^16, slots = 65536): s1 = s2 = x.
+enum : uint32_t { kHashGeneric = 0, kHashNarrow = 1, kHashDirect = 2 };
+__device__ __forceinline__ void wslots(uint32_t x, uint32_t mul, uint32_t slots, uint32_t mode, uint32_t& s1,
+                                       uint32_t& s2) {
+    uint32_t h;
+    if (mode == kHashNarrow) {
+        h = __umul24(x, mul);
+        s1 = static_cast<uint32_t>((static_cast<uint64_t>(h >> 8) * ((slots << 8) & 0xFFFFFFu)) >> 32);
+    } else if (mode == kHashDirect) {
+        s1 = s2 = x;
+        return;
+    } else {
+        h = x * mul;
+        s1 = __umulhi(h, slots);
+    }
+    s2 = s1 ^ ((h >> 8) & 255u);
 }
 
 template <uint32_t W, typename V>
 struct Tab {
     const Slot<KeyT<W>, V>* s;
-    uint32_t slots, mul1;
+    uint32_t slots, mul1, mode;
     uint64_t fold;
 };
 
@@ -140,7 +152,7 @@ __device__ __forceinline__ void lookup_group(const Tab<W, V>& t, const KeyT<W>* 
     using S = Slot<KeyT<W>, V>;
     uint32_t s1[B], s2[B];
 #pragma unroll
-    for (int k = 0; k < B; ++k) wslots(hkey<W>(key[k], t.fold), t.mul1, t.slots, s1[k], s2[k]);
+    for (int k = 0; k < B; ++k) wslots(hkey<W>(key[k], t.fold), t.mul1, t.slots, t.mode, s1[k], s2[k]);
     S e1[B];
 #pragma unroll
     for (int k = 0; k < B; ++k) e1[k] = t.s[s1[k]];
@@ -157,7 +169,7 @@ __device__ __forceinline__ void lookup_group(const Tab<W, V>& t, const KeyT<W>* 
 #pragma unroll
     for (int k = 0; k < B; ++k) e2[k] = t.s[a2[k]];
 #pragma unroll
-    for (int k = 0; k < B; ++k) val[k] = keep_if(m1[k], e1[k].val) | keep_if(key_eq(e2[k].key, key[k]), e2[k].val);
+    for (int k = 0; k < B; ++k) val[k] = m1[k] ? e1[k].val : keep_if(key_eq(e2[k].key, key[k]), e2[k].val);
 }
 // in groups of <= 8 letters (4 with long values and small keys): the
 // slots of a group are in flight together
@@ -251,7 +263,10 @@ __host__ __device__ constexpr uint32_t table_lds_bytes(uint32_t slots, uint32_t 
 template <uint32_t W, typename V, bool LDS>
 __device__ __forceinline__ Tab<W, V> stage_table(const WideArgs& a, uint8_t* lds) {
     using S = Slot<KeyT<W>, V>;
-    Tab<W, V> t{nullptr, a.slots, a.mul1, a.fold};
+    // the hash form: compile-time for wide keys and for tables in LDS (those
+    // of 16-bit keys are always narrow), else the table's
+    const uint32_t mode = W > 2 ? kHashGeneric : (LDS ? kHashNarrow : a.hash_mode);
+    Tab<W, V> t{nullptr, a.slots, a.mul1, mode, a.fold};
     if constexpr (LDS) {
         const uint32_t q = table_lds_bytes(a.slots, a.slot_bytes) / 16;
         for (uint32_t i = threadIdx.x; i < q; i += blockDim.x)
@@ -310,14 +325,23 @@ __global__ __launch_bounds__(kEncWaves * 64) __attribute__((amdgpu_waves_per_eu(
 #pragma unroll
                 for (int k = 0; k < N; ++k) val[k] = l0 + k < cnt ? val[k] : V(1u << 31);  // length 0, not missing
             }
-            uint32_t bits = 0, nocode = 0;
+            // the code lengths (two per add3) and the smallest value: 0 = a
+            // letter without a code (rare: then its index is looked for)
+            uint32_t bits = 0;
+            V lowest = val[0];
 #pragma unroll
-            for (int k = 0; k < N; ++k) {
-                bits += len_of(val[k]);
-                nocode |= val[k] == 0 ? 1u << k : 0u;
+            for (int k = 0; k + 1 < N; k += 2) {
+                bits += len_of(val[k]) + len_of(val[k + 1]);
+                lowest = min(lowest, min(val[k], val[k + 1]));
             }
-            if (nocode) {  // a letter without a code (rare): the lane's first one
-                const uint64_t i = i0 + l0 + static_cast<uint32_t>(__builtin_ctz(nocode));
+            if constexpr (N & 1) {
+                bits += len_of(val[N - 1]);
+                lowest = min(lowest, val[N - 1]);
+            }
+            if (lowest == 0) {
+                uint32_t k = 0;
+                while (val[k] != 0) ++k;
+                const uint64_t i = i0 + l0 + k;
                 first_miss = i < first_miss ? i : first_miss;
             }
             const uint32_t incl = wave_scan_incl(bits);

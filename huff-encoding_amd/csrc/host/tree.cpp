@@ -158,7 +158,7 @@ uint32_t HuffTree::max_depth() const {
 }
 
 std::vector<uint8_t> HuffTree::as_bin() const {
-    // tree_inner.rs:637-663: preorder; joint -> 1, leaf -> 0 then the letter's
+    // tree_inner.rs:632-663: preorder; joint -> 1, leaf -> 0 then the letter's
     // big-endian bits (8 for u8).
     std::vector<uint8_t> bits;
     std::vector<int32_t> st{root_};

@@ -105,6 +105,7 @@ struct WideEncTables {
     uint32_t slot_bytes = 8;
     uint32_t val_off = 4;
     uint32_t mul1 = 0;            // odd hash multiplier (wide_slots)
+    uint32_t hash_mode = 0;       // WideHash
     uint64_t fold = kWideFold0;   // 8- and 16-byte keys: 64-bit fold multiplier (wide_hkey)
     bool long_codes = false;
     std::vector<uint8_t> table;   // slots * slot_bytes
@@ -137,13 +138,26 @@ inline uint32_t wide_hkey(uint64_t lo, uint64_t hi, uint32_t width, uint64_t fol
     const uint64_t k = width == 16 ? lo ^ (hi * fold) : lo;
     return static_cast<uint32_t>((k * fold) >> 32);
 }
-// The two slots of a hash key: s1 = the high half of (x * mul) * slots;
-// s2 = s1 + 1 + bits 8..15 of x * mul, modulo slots (slots > 256)
-inline void wide_slots(uint32_t x, uint32_t mul, uint32_t slots, uint32_t* s1, uint32_t* s2) {
-    const uint32_t h = x * mul;
-    *s1 = static_cast<uint32_t>((static_cast<uint64_t>(h) * slots) >> 32);
-    const uint32_t t = *s1 + ((h >> 8) & 255u) + 1u;
-    *s2 = t < slots ? t : t - slots;
+// The two slots of a hash key (= device/wide.hip wslots). Generic: h = x *
+// mul, s1 = the high half of h * slots. Narrow (keys of <= 2 bytes, slots <
+// 65536): h = (x * mul) on 24 bits, s1 = ((h >> 8) * (slots << 8)) >> 32 (the
+// GPU's full-rate 24-bit multiplies). s2 = s1 ^ bits 8..15 of h (slots a
+// multiple of 256; s2 = s1 leaves the key one slot). Direct (keys of <= 2
+// bytes, slots = 65536): s1 = s2 = x.
+enum WideHash : uint32_t { kWideHashGeneric = 0, kWideHashNarrow = 1, kWideHashDirect = 2 };
+inline void wide_slots(uint32_t x, uint32_t mul, uint32_t slots, uint32_t mode, uint32_t* s1, uint32_t* s2) {
+    uint32_t h;
+    if (mode == kWideHashNarrow) {
+        h = static_cast<uint32_t>(static_cast<uint64_t>(x & 0xFFFFFFu) * (mul & 0xFFFFFFu));
+        *s1 = static_cast<uint32_t>((static_cast<uint64_t>(h >> 8) * ((slots << 8) & 0xFFFFFFu)) >> 32);
+    } else if (mode == kWideHashDirect) {
+        *s1 = *s2 = x;
+        return;
+    } else {
+        h = x * mul;
+        *s1 = static_cast<uint32_t>((static_cast<uint64_t>(h) * slots) >> 32);
+    }
+    *s2 = *s1 ^ ((h >> 8) & 255u);
 }
 
 Status build_wide_enc_tables(const WideTree& t, WideEncTables& out);

@@ -93,7 +93,7 @@ Status WideTree::try_from_bin(uint32_t width, const std::vector<uint8_t>& bits, 
 }
 
 std::vector<uint8_t> WideTree::as_bin() const {
-    // tree_inner.rs:637-663: preorder; joint -> 1, leaf -> 0 + as_be_bytes bits
+    // tree_inner.rs:632-663: preorder; joint -> 1, leaf -> 0 + as_be_bytes bits
     const uint32_t lb = 8 * width_;
     std::vector<uint8_t> bits;
     std::vector<int32_t> st{root_};
@@ -214,7 +214,14 @@ Status build_wide_enc_tables(const WideTree& t, WideEncTables& out) {
     // key below 1/2 with high probability); a failed build re-seeds the hash
     // multipliers (and the fold of wide keys), every 8th failure grows the
     // table by 1/8
-    uint64_t M = std::max<uint64_t>(512, (D * 9 + 3) / 4);
+    // slots: a multiple of 256 (wide_slots' s2), >= 9/4 D; 16-bit keys use
+    // the narrow hash below 65,536 slots and a direct table (slot = letter)
+    // from there
+    auto round256 = [](uint64_t m) { return (m + 255) / 256 * 256; };
+    uint64_t M = round256(std::max<uint64_t>(512, (D * 9 + 3) / 4));
+    out.hash_mode = kWideHashGeneric;
+    if (W <= 2) out.hash_mode = M < 65536 ? kWideHashNarrow : kWideHashDirect;
+    if (out.hash_mode == kWideHashDirect) M = 65536;
     uint64_t seed = 0;
     auto mix = [](uint64_t z) {  // splitmix64
         z += 0x9E3779B97F4A7C15ull;
@@ -225,7 +232,13 @@ Status build_wide_enc_tables(const WideTree& t, WideEncTables& out) {
     for (uint32_t attempt = 0;; ++attempt) {
         if (attempt == 256 || M >= (1ull << 31))
             return Status::err(HUFF_E_INVALID_ARG, "letters do not separate in the encoder's hash table");
-        if (attempt && attempt % 8 == 0) M += M / 8;
+        if (attempt && attempt % 8 == 0 && out.hash_mode != kWideHashDirect) {
+            M = round256(M + M / 8);
+            if (out.hash_mode == kWideHashNarrow && M >= 65536) {
+                out.hash_mode = kWideHashDirect;
+                M = 65536;
+            }
+        }
         const uint64_t z = mix(++seed);
         out.mul1 = static_cast<uint32_t>(z) | 1u;
         out.fold = attempt == 0 ? kWideFold0 : (mix(seed ^ kWideFold0) | 1u);
@@ -233,7 +246,7 @@ Status build_wide_enc_tables(const WideTree& t, WideEncTables& out) {
         for (size_t i = 0; i < D; ++i) {
             hk[i] = wide_hkey(static_cast<uint64_t>(codes[i].letter), static_cast<uint64_t>(codes[i].letter >> 64), W,
                               out.fold);
-            wide_slots(hk[i], out.mul1, out.slots, &s1[i], &s2[i]);
+            wide_slots(hk[i], out.mul1, out.slots, out.hash_mode, &s1[i], &s2[i]);
         }
         occ.assign(M, -1);
         bool ok = true;

@@ -74,6 +74,7 @@ huff::dev::WideArgs huff_wenc::enc_args(bool pack_pass) const {
     a.slots = et->slots;
     a.slot_bytes = et->slot_bytes;
     a.mul1 = et->mul1;
+    a.hash_mode = et->hash_mode;
     a.fold = et->fold;
     a.long_codes = et->long_codes;
     a.max_len = et->maxlen;

@@ -274,13 +274,13 @@ int huff_dev_decompress(huff_ctx* ctx, const huff_tree* t, const uint8_t* d_comp
 
 /* Many small byte streams at once (device pointers, one
  * launch each, synchronous):
- *  huff_batch_hist:  d_hist[s][256] = the byte weights (ByteWeights::from
- *                    of the bytes, weights.rs:196-208) of stream s =
+ *  huff_batch_hist:  d_hist[s][256] = the byte weights (ByteWeights::
+ *                    from_bytes, weights.rs:265-279) of stream s =
  *                    d_in[d_offsets[s], d_offsets[s + 1]).
  *  huff_batch_trees: HuffTree::from_weights of each d_hist[s] (tree_inner.rs:
  *                    281-320, with the reference's exact BinaryHeap tie order)
  *                    -> d_tree_bits + s * tree_stride: as_bin (tree_inner.rs:
- *                    637-663), MSB first, d_tree_nbits[s] bits; d_codes[s][l] =
+ *                    632-663), MSB first, d_tree_nbits[s] bits; d_codes[s][l] =
  *                    code << 8 | len of letter l (0: no code); d_max_len[s];
  *                    d_status[s] = HUFF_OK, HUFF_E_EMPTY_WEIGHTS (all weights
  *                    zero: "provided empty weights") or HUFF_E_CODE_TOO_LONG (a

@@ -1,7 +1,7 @@
 """GPU parity of the batched small-stream API (device-side
 tree build, include/huffgpu.h huff_batch_hist / huff_batch_trees): for
 >= 1,000 independent streams in one launch, the weights equal np.bincount
-and every stream's tree bits (as_bin, tree_inner.rs:637-663) and codes equal
+and every stream's tree bits (as_bin, tree_inner.rs:632-663) and codes equal
 the oracle's HuffTree::from_weights (tree_inner.rs:281-320 with the exact
 BinaryHeap tie order, oracle/huff_oracle.c)."""
 import numpy as np
