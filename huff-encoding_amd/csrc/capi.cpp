@@ -470,7 +470,8 @@ int huff_batch_trees(huff_ctx* ctx, const uint64_t* d_hist, uint32_t nstreams, u
     if (tree_stride < HUFF_TREE_BITS_MAX_BYTES || tree_stride > 0xFFFFFFFFu)
         return fail(HUFF_E_INVALID_ARG, "tree_stride < HUFF_TREE_BITS_MAX_BYTES");
     static_assert(HUFF_TREE_BITS_MAX_BYTES == huff::dev::kTreeBitsMaxBytes, "as_bin of 257 leaves");
-    static_assert(huff::dev::kTreeEmpty == HUFF_E_EMPTY_WEIGHTS && huff::dev::kTreeDeep == HUFF_E_CODE_TOO_LONG,
+    static_assert(static_cast<int>(huff::dev::kTreeEmpty) == static_cast<int>(HUFF_E_EMPTY_WEIGHTS) &&
+                      static_cast<int>(huff::dev::kTreeDeep) == static_cast<int>(HUFF_E_CODE_TOO_LONG),
                   "the kernel writes the C ABI's status codes");
     return guarded([&]() -> huff::Status {
         HUFF_TRY(ctx->activate());

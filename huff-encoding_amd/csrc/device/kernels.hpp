@@ -219,9 +219,11 @@ hipError_t launch_index_expand(uint64_t n, const uint64_t* task_base, const uint
                                const uint64_t* chunk_start, uint32_t* sub_bit, hipStream_t s);
 
 // wider letters (wide.hip): W-byte keys, hash-table code lookup. The
-// encoder's chunk is kWideChunk letters (one wave: 64 runs of kSub), its
-// restart index chunk_start per chunk + u32 sub_bit per run.
-constexpr uint32_t kWideChunk = 64 * kSub;
+// encoder's chunk is kWideChunk letters (one wave), its restart index
+// chunk_start per chunk + u32 sub_bit per run of kWideRun letters (relative
+// to the chunk start; sub_abs entries of index-free streams likewise per run).
+constexpr uint32_t kWideRun = 64;
+constexpr uint32_t kWideChunk = 256 * kWideRun;
 struct WideArgs {
     const uint8_t* in;            // n letters of `width` bytes, native layout, 16-B aligned
     uint64_t n;
@@ -240,7 +242,7 @@ struct WideArgs {
     uint32_t stage_words;         // pack: LDS staging words per wave (wide_stage_words)
     uint64_t* chunk_bits;         // [nchunks]            (bits pass)
     const uint64_t* chunk_start;  // [nchunks + 1]        (pack pass)
-    uint32_t* sub_bit;            // [ceil(n / kSub)] run start - chunk start
+    uint32_t* sub_bit;            // [ceil(n / kWideRun)] run start - chunk start
     unsigned long long* first_missing;  // min index of a letter without a code
     uint8_t* out;                 // any alignment: ceil(bits / 8) bytes
 };
@@ -254,21 +256,27 @@ struct WideDecArgs {
     uint64_t comp_bytes;
     const uint32_t* lut;          // leaf = (len << 24) | leaf, ptr = kLutPtr | offset
     uint32_t lut_bits;
+    const void* stab;             // wdecode.hip: the two-level table (host/wide.hpp WideDecTables::stab)
+    uint32_t stab_bits;           // its level-1 index bits
+    uint32_t stab_bytes;
     const uint8_t* letters;       // [leaves * width]
     uint32_t nleaves;
     uint32_t width;
-    const uint64_t* chunk_start;
-    const uint32_t* sub_bit;
-    const uint64_t* sub_abs;      // non-null: index-free restart points
+    const uint64_t* chunk_start;  // per wide chunk
+    const uint32_t* sub_bit;      // per run of kWideRun letters
+    const uint64_t* sub_abs;      // non-null: index-free restart points, per run of kWideRun letters
+    uint64_t end_bit;             // the stream's last bit + 1 (wdecode.hip: the last task's end)
     uint32_t nchunks;
     uint32_t cu_count;
-    uint32_t max_len;             // longest code (<= 32: the 64-byte-unit decoder)
+    uint32_t max_len;             // longest code (<= 32: wdecode.hip)
+    uint32_t stage_bytes;         // wdecode.hip: LDS stage per wave (a multiple of 16)
     uint64_t n;
     uint8_t* out;                 // n * width bytes
 };
 hipError_t launch_wide_bits(const WideArgs& a, hipStream_t s);
 hipError_t launch_wide_pack(const WideArgs& a, hipStream_t s);
-hipError_t launch_wide_decode(const WideDecArgs& a, hipStream_t s);
+hipError_t launch_wide_decode(const WideDecArgs& a, hipStream_t s);       // codes > 32 bits (wide.hip)
+hipError_t launch_wide_decode_task(const WideDecArgs& a, hipStream_t s);  // codes <= 32 bits (wdecode.hip)
 // build_weights_map on the device (wweights.hip). width <= 2: counts = the
 // 2^(8 width) bins (zeroed). width >= 4: an HBM table of `slots`
 // (wcount_slots) keys_lo (all ones), counts (zero), width 16 also keys_hi and

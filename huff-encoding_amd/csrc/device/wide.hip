@@ -19,10 +19,10 @@
 //            broadcast address): the second read costs only the misses'
 //            bank conflicts. The host inserts letters shortest code first,
 //            so frequent letters sit in their first slot.
-//  k_wbits   pass 1: per-lane code-length sums, a wave scan per round, and
-//            the run totals (a run = kSub letters = 16 / 8W lanes) gathered
-//            lane j <- run j; at the chunk end one more wave scan gives
-//            sub_bit (run start - chunk start) and chunk_bits. The first
+//  k_wbits   pass 1: per-lane code-length sums and a wave scan per round;
+//            the first lane of every run of kWideRun = 64 letters stores the
+//            run's start (sub_bit, relative to the chunk start), the round
+//            total carries into the next; chunk_bits at the end. The first
 //            letter with no code (input order) goes to first_missing
 //            (CompressError, comp.rs:426-432).
 //  k_wpack   pass 2 (pack.hip's scheme, pack_emit.hpp): a wave scan of the
@@ -34,9 +34,11 @@
 //            letters before it are recomputed from those letters, so no byte
 //            is written twice and the output needs no zero fill. Any output
 //            alignment: the image is aligned to the 16-byte granule below.
-//  k_wdecode one lane per 256-letter run from the restart index (or from the
-//            index-free decoder's sub_abs), primary table in LDS, secondary
-//            tables and the leaf letters in global memory.
+//  k_wdecode codes longer than 32 bits (or a task-decoder table over 4 Mi
+//            entries): one lane per 256-letter run from the restart index (or
+//            the index-free decoder's sub_abs), primary table in LDS,
+//            secondary tables and the leaf letters in global memory. Codes of
+//            <= 32 bits: the task decoder of wdecode.hip.
 //
 // Roofline: HBM-bound. Pass 1 reads n W bytes, pass 2 n W + writes C.
 #include <type_traits>
@@ -298,7 +300,7 @@ __global__ __launch_bounds__(kEncWaves * 64) __attribute__((amdgpu_waves_per_eu(
 #if WIDE_BITS_AHEAD > 1
         LaneIn<LB> v1 = load_round<LB>(rin, 1, lane);
 #endif
-        uint32_t runacc = 0;  // lane j: the code bits of run j
+        uint32_t round_base = 0;  // code bits of the chunk before this round
         for (uint32_t r = 0; r < nrounds; ++r) {
             const LaneIn<LB> v = v0;
 #if WIDE_BITS_AHEAD > 1
@@ -344,26 +346,16 @@ __global__ __launch_bounds__(kEncWaves * 64) __attribute__((amdgpu_waves_per_eu(
                 const uint64_t i = i0 + l0 + k;
                 first_miss = i < first_miss ? i : first_miss;
             }
+            // the restart index: every run of kWideRun letters starts at a
+            // lane (LPR lanes per run); the run's first lane stores its start
             const uint32_t incl = wave_scan_incl(bits);
-            if constexpr (RB / W >= kSub) {
-                constexpr uint32_t RPR = RB / W / kSub;  // runs per round
-                constexpr uint32_t LPR = 64 / RPR;       // lanes per run
-                uint32_t prev = 0;
-#pragma unroll
-                for (uint32_t q = 0; q < RPR; ++q) {
-                    const uint32_t e = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(incl), (q + 1) * LPR - 1));
-                    runacc = lane == r * RPR + q ? e - prev : runacc;
-                    prev = e;
-                }
-            } else {  // a run spans several rounds
-                constexpr uint32_t RPN = kSub * W / RB;
-                const uint32_t e = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(incl), 63));
-                runacc += lane == r / RPN ? e : 0u;
-            }
+            constexpr uint32_t LPR = kWideRun * W / LB;  // lanes per run
+            static_assert(LPR >= 1 && 64 % LPR == 0, "whole runs per round");
+            if (lane % LPR == 0 && l0 < cnt)
+                a.sub_bit[static_cast<uint64_t>(c) * (kWideChunk / kWideRun) + l0 / kWideRun] = round_base + incl - bits;
+            round_base += static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(incl), 63));
         }
-        const uint32_t incl = wave_scan_incl(runacc);
-        if (lane * kSub < cnt) a.sub_bit[static_cast<uint64_t>(c) * 64 + lane] = incl - runacc;
-        if (lane == 63) a.chunk_bits[c] = incl;
+        if (lane == 0) a.chunk_bits[c] = round_base;
     }
     if (first_miss != ~0ull) atomicMin(a.first_missing, first_miss);
 }
@@ -552,7 +544,7 @@ __device__ __forceinline__ void wdecode_chunk(const WideDecArgs& a, const uint32
     const uint32_t cnt = static_cast<uint32_t>(a.n - i0 < kSub ? a.n - i0 : kSub);
     const BitSrc src{reinterpret_cast<const uint32_t*>(a.comp), a.comp, a.comp_bytes};
     T* out = reinterpret_cast<T*>(a.out) + i0;
-    uint64_t pos = a.sub_abs ? a.sub_abs[run] : a.chunk_start[run >> 6] + a.sub_bit[run];
+    uint64_t pos = a.sub_abs ? a.sub_abs[run * 4] : a.chunk_start[run >> 6] + a.sub_bit[run * 4];
     // the lane's stream through a 4 x 16-byte register ring (48 bytes in
     // flight ahead of the dword being consumed), as decode.hip k_decode
     uint4 cur, n1, n2, n3;
@@ -657,127 +649,6 @@ __global__ __launch_bounds__(kThreads) void k_wdecode(WideDecArgs a) {
     }
 }
 
-// Codes <= 32 bits (the usual case): the lane's stream in 64-byte units, the
-// four 16-byte loads of the next unit issued before the current one is
-// decoded and consumed at static register positions (as decode.hip
-// k_decode_short), so no load result is waited for inside a branch. Letters
-// of <= 4 bytes gather in a lane-private LDS row of 16 dwords and leave as one
-// 64-byte piece; wider letters are stored one by one.
-constexpr uint32_t kRowStride = 17;  // dwords per lane row (+1: bank spread)
-
-template <typename T>
-__device__ __forceinline__ void wdecode_short_chunk(const WideDecArgs& a, const uint32_t* plut, const T* letters,
-                                                    uint32_t* rows, uint32_t chunk) {
-    constexpr uint32_t W = sizeof(T);
-    constexpr uint32_t per = W <= 4 ? 4 / W : 1;  // letters per dword (W <= 4)
-    const uint32_t K = a.lut_bits;
-    const uint32_t t = threadIdx.x;
-    const uint64_t run = static_cast<uint64_t>(chunk) * kThreads + t;
-    const uint64_t i0 = run * kSub;
-    if (i0 >= a.n) return;
-    const uint32_t cnt = static_cast<uint32_t>(a.n - i0 < kSub ? a.n - i0 : kSub);
-    T* out = reinterpret_cast<T*>(a.out) + i0;
-    uint32_t* row = rows + t * kRowStride;
-    const uint64_t pos = a.sub_abs ? a.sub_abs[run] : a.chunk_start[run >> 6] + a.sub_bit[run];
-    uint64_t unit = pos >> 9;
-    uint32_t drop = static_cast<uint32_t>(pos & 511);
-    uint4 A0 = load_vec(a.comp, unit * 64 + 0, a.comp_bytes);
-    uint4 A1 = load_vec(a.comp, unit * 64 + 16, a.comp_bytes);
-    uint4 A2 = load_vec(a.comp, unit * 64 + 32, a.comp_bytes);
-    uint4 A3 = load_vec(a.comp, unit * 64 + 48, a.comp_bytes);
-    uint64_t buf = 0;
-    uint32_t nb = 0, j = 0, acc = 0;
-    auto emit = [&](T v) {
-        if constexpr (W <= 4) {
-            acc |= static_cast<uint32_t>(v) << (8 * W * (j % per));
-            if (j % per == per - 1) {
-                row[(j / per) & 15] = acc;
-                acc = 0;
-                if ((j + 1) % (16 * per) == 0) {  // a whole row: letters [j + 1 - 16 per, j + 1)
-                    uint4* d4 = reinterpret_cast<uint4*>(out + (j + 1 - 16 * per));
-                    d4[0] = make_uint4(row[0], row[1], row[2], row[3]);
-                    d4[1] = make_uint4(row[4], row[5], row[6], row[7]);
-                    d4[2] = make_uint4(row[8], row[9], row[10], row[11]);
-                    d4[3] = make_uint4(row[12], row[13], row[14], row[15]);
-                }
-            }
-        } else {
-            out[j] = v;
-        }
-    };
-    auto dec_dword = [&](uint32_t dw) {
-        if (nb < 32) {
-            buf |= static_cast<uint64_t>(__builtin_bswap32(dw)) << (32 - nb);
-            nb += 32;
-        }
-        if (drop) {
-            const uint32_t k = drop < nb ? drop : nb;
-            buf <<= k;
-            nb -= k;
-            drop -= k;
-        }
-        while (nb >= 32 && j < cnt) {
-            uint32_t e = plut[buf >> (64 - K)];
-            if (e & kLutPtr) {  // codes <= 32 bits: the window holds the whole code
-                uint32_t d = K;
-                do {
-                    e = a.lut[(e & ~kLutPtr) + static_cast<uint32_t>((buf >> (56 - d)) & 0xFFu)];
-                    d += 8;
-                } while (e & kLutPtr);
-            }
-            const uint32_t len = (e >> 24) & 0x7Fu;
-            buf <<= len;
-            nb -= len;
-            emit(letters[e & 0xFFFFFFu]);
-            ++j;
-        }
-    };
-    while (j < cnt) {
-        ++unit;
-        const uint4 B0 = load_vec(a.comp, unit * 64 + 0, a.comp_bytes);
-        const uint4 B1 = load_vec(a.comp, unit * 64 + 16, a.comp_bytes);
-        const uint4 B2 = load_vec(a.comp, unit * 64 + 32, a.comp_bytes);
-        const uint4 B3 = load_vec(a.comp, unit * 64 + 48, a.comp_bytes);
-        dec_dword(A0.x); dec_dword(A0.y); dec_dword(A0.z); dec_dword(A0.w);
-        dec_dword(A1.x); dec_dword(A1.y); dec_dword(A1.z); dec_dword(A1.w);
-        dec_dword(A2.x); dec_dword(A2.y); dec_dword(A2.z); dec_dword(A2.w);
-        dec_dword(A3.x); dec_dword(A3.y); dec_dword(A3.z); dec_dword(A3.w);
-        A0 = B0;
-        A1 = B1;
-        A2 = B2;
-        A3 = B3;
-    }
-    if constexpr (W <= 4) {  // ragged end: letters [j rounded down to a row, j)
-        const uint32_t rl = 16 * per;
-        if (j % rl) {
-            if (j % per) row[(j / per) & 15] = acc;
-            for (uint32_t i = j - j % rl; i < j; ++i)
-                out[i] = static_cast<T>(row[(i / per) & 15] >> (8 * W * (i % per)));
-        }
-    }
-}
-
-template <typename T, bool LLDS>
-__global__ __launch_bounds__(kThreads) void k_wdecode_short(WideDecArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t plut[];
-    const uint32_t nprim = 1u << a.lut_bits;
-    for (uint32_t i = threadIdx.x; i < nprim; i += kThreads) plut[i] = a.lut[i];
-    const uint32_t lw = LLDS ? (a.nleaves * static_cast<uint32_t>(sizeof(T)) + 15) / 16 * 4 : 0;
-    uint32_t* rows = plut + nprim + lw;
-    if constexpr (LLDS) {
-        uint32_t* ll = plut + nprim;
-        for (uint32_t i = threadIdx.x; i < lw; i += kThreads) ll[i] = reinterpret_cast<const uint32_t*>(a.letters)[i];
-        __syncthreads();
-        for (uint32_t c = blockIdx.x; c < dec_groups(a); c += gridDim.x)
-            wdecode_short_chunk<T>(a, plut, reinterpret_cast<const T*>(ll), rows, c);
-    } else {
-        __syncthreads();
-        for (uint32_t c = blockIdx.x; c < dec_groups(a); c += gridDim.x)
-            wdecode_short_chunk<T>(a, plut, reinterpret_cast<const T*>(a.letters), rows, c);
-    }
-}
-
-
 // persistent grid: as many 256-thread workgroups as fit on the chip at once
 // (LDS and the 8-workgroup-per-CU wave limit), at most one per group
 inline uint32_t grid_for(uint32_t ngroups, uint32_t cus, size_t lds) {
@@ -860,18 +731,7 @@ template <typename T>
 void decode_as(const WideDecArgs& a, hipStream_t s) {
     const size_t prim = (size_t(1) << a.lut_bits) * 4;
     const size_t lw = (static_cast<size_t>(a.nleaves) * sizeof(T) + 15) / 16 * 16;
-    const bool llds = lw <= kLetterLdsMax;
-    if (a.max_len <= 32) {
-        const size_t rows = sizeof(T) <= 4 ? size_t(kThreads) * kRowStride * 4 : 0;
-        const size_t lds = prim + (llds ? lw : 0) + rows;
-        const uint32_t g = grid_for(dec_groups_host(a), a.cu_count, lds);
-        if (llds)
-            hipLaunchKernelGGL((k_wdecode_short<T, true>), dim3(g), dim3(kThreads), lds, s, a);
-        else
-            hipLaunchKernelGGL((k_wdecode_short<T, false>), dim3(g), dim3(kThreads), lds, s, a);
-        return;
-    }
-    if (llds)
+    if (lw <= kLetterLdsMax)
         hipLaunchKernelGGL((k_wdecode<T, true>), dim3(grid_for(dec_groups_host(a), a.cu_count, prim + lw)), dim3(kThreads),
                            prim + lw, s, a);
     else

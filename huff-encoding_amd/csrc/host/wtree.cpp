@@ -309,16 +309,102 @@ Status build_wide_enc_tables(const WideTree& t, WideEncTables& out) {
     return Status::ok();
 }
 
+// The task decoder's two-level table (WideDecTables::stab): level 1 indexed
+// by the first K1 = sbits bits; a window whose first code is longer points to
+// a level-2 table of 2^s entries indexed by the next s bits, s = the deepest
+// leaf below that node minus K1 (exact depth: no further level). Left empty
+// for codes > 32 bits or more than 4 Mi entries (the long-code decoder).
+static void build_wide_stab(const WideTree& t, uint32_t W, const std::vector<int64_t>& leaf_of, WideDecTables& out) {
+    const auto& nodes = t.nodes();
+    const uint32_t eb = W == 4 ? 8 : 4;
+    std::vector<uint64_t> tab;
+    auto leaf_entry = [&](int32_t x, uint32_t len, uint32_t leaf) -> uint64_t {
+        if (W <= 2) return (static_cast<uint64_t>(nodes[x].letter) << 8) | len;
+        if (W == 4) return (static_cast<uint64_t>(static_cast<uint32_t>(nodes[x].letter)) << 32) | len;
+        return (static_cast<uint64_t>(leaf) << 8) | len;
+    };
+    if (t.root_is_leaf()) {  // every bit decodes the root letter (comp.rs:506-509)
+        out.sbits = 1;
+        const int32_t r = t.root();
+        tab = {leaf_entry(r, 1, static_cast<uint32_t>(leaf_of[r])), leaf_entry(r, 1, static_cast<uint32_t>(leaf_of[r]))};
+    } else {
+        const uint32_t K1 = out.sbits;
+        tab.assign(size_t(1) << K1, 0);
+        auto depth_below = [&](int32_t x) {
+            uint32_t m = 0;
+            std::vector<std::pair<int32_t, uint32_t>> st{{x, 0}};
+            while (!st.empty()) {
+                auto [y, d] = st.back();
+                st.pop_back();
+                if (nodes[y].is_leaf) {
+                    m = std::max(m, d);
+                } else {
+                    st.push_back({nodes[y].left, d + 1});
+                    st.push_back({nodes[y].right, d + 1});
+                }
+            }
+            return m;
+        };
+        // walk `bits` bits (MSB first) of index i from node x: the leaf and
+        // its depth, or the node reached at depth `bits`
+        auto walk = [&](int32_t x, uint32_t i, uint32_t bits, uint32_t* depth) {
+            for (uint32_t p = 0; p < bits; ++p) {
+                x = ((i >> (bits - 1 - p)) & 1u) ? nodes[x].right : nodes[x].left;
+                if (nodes[x].is_leaf) {
+                    *depth = p + 1;
+                    return x;
+                }
+            }
+            *depth = bits;
+            return x;
+        };
+        for (uint32_t i = 0; i < (1u << K1); ++i) {
+            uint32_t d;
+            const int32_t x = walk(t.root(), i, K1, &d);
+            if (nodes[x].is_leaf) {
+                tab[i] = leaf_entry(x, d, static_cast<uint32_t>(leaf_of[x]));
+                continue;
+            }
+            const uint32_t sw = depth_below(x);  // >= 1
+            if (K1 + sw > 32 || tab.size() + (size_t(1) << sw) > (size_t(1) << 22)) {
+                out.stab.clear();  // codes > 32 bits or a table > 4 Mi entries: the long-code decoder
+                return;
+            }
+            const uint64_t off = tab.size();
+            tab[i] = (off << 8) | 0x80u | sw;
+            tab.resize(tab.size() + (size_t(1) << sw));
+            for (uint32_t j = 0; j < (1u << sw); ++j) {
+                uint32_t r;
+                const int32_t y = walk(x, j, sw, &r);
+                tab[off + j] = leaf_entry(y, K1 + r, static_cast<uint32_t>(leaf_of[y]));
+            }
+        }
+    }
+    out.stab.assign((tab.size() * eb + 15) / 16 * 16, 0);
+    for (size_t i = 0; i < tab.size(); ++i) {
+        if (W == 4) {
+            // pointer entries keep the offset in bits 8..31 of the low half
+            std::memcpy(&out.stab[i * 8], &tab[i], 8);
+        } else {
+            const uint32_t v = static_cast<uint32_t>(tab[i]);
+            std::memcpy(&out.stab[i * 4], &v, 4);
+        }
+    }
+}
+
 Status build_wide_dec_tables(const WideTree& t, WideDecTables& out) {
     const uint32_t W = t.width();
     const auto& nodes = t.nodes();
     out.lut.clear();
     out.letters.clear();
-    // leaf index = order of appearance in the walk below
+    // leaf index = order of appearance in the walk below (leaf_of: a node's
+    // index, for the task decoder's table)
+    std::vector<int64_t> leaf_of(nodes.size(), -1);
     auto leaf_id = [&](int32_t x) {
         const uint32_t id = static_cast<uint32_t>(out.letters.size() / W);
         out.letters.resize(out.letters.size() + W);
         store_letter(&out.letters[id * W], W, nodes[x].letter);
+        leaf_of[x] = id;
         return id;
     };
     if (t.root_is_leaf()) {  // every bit decodes the root letter (comp.rs:506-509)
@@ -326,6 +412,8 @@ Status build_wide_dec_tables(const WideTree& t, WideDecTables& out) {
         out.maxdepth = 1;
         const uint32_t e = (1u << 24) | leaf_id(t.root());
         out.lut = {e, e};
+        out.sbits = 1;
+        build_wide_stab(t, W, leaf_of, out);
         return Status::ok();
     }
     const uint32_t maxd = t.max_depth();
@@ -368,6 +456,8 @@ Status build_wide_dec_tables(const WideTree& t, WideDecTables& out) {
             }
         }
     }
+    out.sbits = std::max<uint32_t>(1, std::min<uint32_t>(maxd, 10));
+    build_wide_stab(t, W, leaf_of, out);
     return Status::ok();
 }
 

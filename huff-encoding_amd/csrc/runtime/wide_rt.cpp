@@ -60,7 +60,7 @@ Status huff_wenc::init(huff_ctx* c, uint32_t w, const uint8_t* d, uint64_t nlett
     HUFF_TRY(chunk_bits.ensure((nchunks + 1) * 8));
     HUFF_TRY(chunk_start.ensure((nchunks + 2) * 8));
     HUFF_TRY(tsum.ensure((nchunks / 1024 + 2) * 8));
-    HUFF_TRY(sub_bit.ensure(((n + huff::dev::kSub - 1) / huff::dev::kSub + 1) * 4));
+    HUFF_TRY(sub_bit.ensure(((n + huff::dev::kWideRun - 1) / huff::dev::kWideRun + 1) * 4));
     HUFF_TRY(missing.ensure(8));
     return Status::ok();
 }
@@ -139,9 +139,11 @@ Status huff_wenc::upload_dec(const huff_wtree* t) {
     if (t->t.width() != width) return Status::err(HUFF_E_INVALID_ARG, "the tree's letter width differs from the job's");
     if (dec_tree == t->id) return Status::ok();
     HUFF_TRY(lut.ensure(dt->lut.size() * 4));
-    HUFF_TRY(letters.ensure(dt->letters.size() + 16));
+    HUFF_TRY(letters.ensure((dt->letters.size() + 31) / 16 * 16));  // staged in 16-B pieces
+    HUFF_TRY(stab.ensure(dt->stab.size()));
     HIP_TRY(hipMemcpyAsync(lut.p, dt->lut.data(), dt->lut.size() * 4, hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(hipMemcpyAsync(letters.p, dt->letters.data(), dt->letters.size(), hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(stab.p, dt->stab.data(), dt->stab.size(), hipMemcpyHostToDevice, ctx->stream));
     dec_tree = t->id;
     return Status::ok();
 }
@@ -156,6 +158,9 @@ Status huff_wenc::decode(const huff_wtree* t, const uint8_t* d_comp, uint64_t co
     a.comp_bytes = comp_bytes;
     a.lut = static_cast<const uint32_t*>(lut.p);
     a.lut_bits = dt->bits;
+    a.stab = stab.p;
+    a.stab_bits = dt->sbits;
+    a.stab_bytes = static_cast<uint32_t>(dt->stab.size());
     a.letters = static_cast<const uint8_t*>(letters.p);
     a.nleaves = static_cast<uint32_t>(dt->letters.size() / width);
     a.max_len = dt->maxdepth;
@@ -167,14 +172,25 @@ Status huff_wenc::decode(const huff_wtree* t, const uint8_t* d_comp, uint64_t co
     a.cu_count = static_cast<uint32_t>(ctx->cu_count);
     a.n = n;
     a.out = d_out;
+    a.end_bit = comp_bytes * 8;  // bounds the last task's staged range
     hipStream_t s = ctx->stream;
+    if (!dt->stab.empty()) {
+        // the task decoder's LDS stage per wave: the task's mean compressed
+        // bytes with a quarter of headroom (tasks beyond it decode from
+        // global memory), 2..16 KiB
+        const double bits_per = n ? static_cast<double>(comp_bytes) * 8.0 / static_cast<double>(n) : 8.0;
+        const double want = 1.25 * bits_per * huff::dev::kWideRun * 64 / 8 + 96;
+        uint32_t sb = static_cast<uint32_t>(want < 2048 ? 2048 : (want > 16384 ? 16384 : want));
+        a.stage_bytes = (sb + 15) & ~15u;
+        return ctx->timed("wdecode", [&] { return huff::dev::launch_wide_decode_task(a, s); });
+    }
     return ctx->timed("wdecode", [&] { return huff::dev::launch_wide_decode(a, s); });
 }
 
 Status huff_wenc::download_index(huff_index_host& idx) {
     idx.n = n;
     idx.chunk_start.resize(nchunks + 1);
-    idx.sub_bit.resize((n + huff::dev::kSub - 1) / huff::dev::kSub);
+    idx.sub_bit.resize((n + huff::dev::kWideRun - 1) / huff::dev::kWideRun);
     HIP_TRY(hipMemcpyAsync(idx.chunk_start.data(), chunk_start.p, idx.chunk_start.size() * 8, hipMemcpyDeviceToHost,
                            ctx->stream));
     if (!idx.sub_bit.empty())
@@ -337,7 +353,7 @@ Status wdecode_indexless_dev(huff_ctx* ctx, const huff_wtree* t, const uint8_t* 
     if (!dev::indexless_staged(st.a))
         return Status::err(HUFF_E_CODE_TOO_LONG, "index-free decode of letters wider than a byte needs codes <= 32 bits");
     DevBuf& sub_abs = ctx->idx_sub_abs;
-    HUFF_TRY(indexless_mark(ctx, st, sub_abs));
+    HUFF_TRY(indexless_mark(ctx, st, sub_abs, 6));  // every kWideRun-th letter
     HIP_TRY(hipEventRecord(ctx->lut_free, ctx->stream));
     huff_wenc e;
     HUFF_TRY(e.init(ctx, t->t.width(), nullptr, st.total));

@@ -42,7 +42,7 @@ struct huff_wenc {
     uint32_t width = 1;
     uint32_t nchunks = 0;
     DevBuf chunk_bits, chunk_start, tsum, sub_bit, missing;
-    DevBuf table, lut, letters;  // device tables of the last trees used
+    DevBuf table, lut, letters, stab;  // device tables of the last trees used
     uint64_t enc_tree = 0, dec_tree = 0;
     const huff::WideEncTables* et = nullptr;
     const huff::WideDecTables* dt = nullptr;

@@ -179,6 +179,28 @@ def test_long_codes(W, O, ctx, dtype):
     assert e.value.code == 7
 
 
+@pytest.mark.parametrize("dtype", [np.uint8, np.int16, np.uint32, np.int64])
+def test_codes_17_to_32_bits(W, O, ctx, dtype):
+    """Fibonacci weights over 25 letters: codes up to 24 bits, so the task
+    decoder refills before every code and takes level-2 entries (wdecode.hip);
+    restart-index and index-free decode"""
+    fib = [1, 1]
+    while len(fib) < 25:
+        fib.append(fib[-1] + fib[-2])
+    items = [(3 + 5 * i, f) for i, f in enumerate(fib)]
+    t = W.WideTree.from_weights(items, dtype)
+    assert max(len(c) for c in t.read_codes().values()) == 24
+    rng = np.random.default_rng(17)
+    p = np.array(fib, np.float64) ** 0.5  # flatter than the weights: long codes are frequent
+    letters = (3 + 5 * rng.choice(25, 300_001, p=p / p.sum())).astype(dtype)
+    cd = W.compress_with_tree(letters, t, ctx)
+    (ocomp, opad), _ = oracle_stream(O, letters, items, 8 * np.dtype(dtype).itemsize)
+    assert cd.comp_bytes() == ocomp and cd.padding_bits() == opad
+    assert np.array_equal(W.decompress(cd, ctx), letters)
+    back = W.decompress(W.WideCompressData.try_from_bytes(cd.to_bytes(), dtype), ctx)
+    assert np.array_equal(back, letters)
+
+
 @pytest.mark.parametrize("dtype,k", [(np.uint32, 40_000), (np.uint16, 65536), (np.uint64, 20_000)])
 def test_large_alphabet_table_in_hbm(W, O, ctx, dtype, k):
     """alphabets whose code table exceeds the LDS budget (kWideLdsMax):
@@ -223,6 +245,16 @@ def test_device_pack_any_alignment(W, O, ctx, dtype):
         got = buf.cpu().numpy()
         assert got[off:off + nb].tobytes() == ocomp, off
         assert (got[:off] == 0xAB).all() and (got[off + nb:] == 0xAB).all(), off
+    # the restart-index decoder into a misaligned destination
+    out = torch.empty(nb + 64, dtype=torch.uint8, device="cuda")
+    job.pack(t, out.data_ptr(), nb)
+    w = np.dtype(dtype).itemsize
+    for off in (w, 16 + w):
+        dec = torch.full((n * w + 64,), 0xCD, dtype=torch.uint8, device="cuda")
+        job.decode(t, out.data_ptr(), dec.data_ptr() + off)
+        got = dec.cpu().numpy()
+        assert got[off:off + n * w].tobytes() == letters.tobytes(), off
+        assert (got[:off] == 0xCD).all() and (got[off + n * w:] == 0xCD).all(), off
 
 
 def test_device_job_large(W, ctx):
