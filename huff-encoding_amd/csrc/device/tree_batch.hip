@@ -25,7 +25,7 @@ namespace huff::dev {
 
 namespace {
 
-constexpr int kTreeLanes = 32;      // streams per workgroup (one lane each)
+constexpr int kTreeLanes = 16;      // streams per workgroup (one lane each): 53 KB of LDS, 3 workgroups per CU
 constexpr int kHeapCap = 257;       // 256 letters + the byte-0 re-yield
 constexpr uint32_t kNodeBits = 10;  // heap key = weight << 10 | node (node < 2 * 257)
 
