@@ -61,7 +61,7 @@ void build_multi_table(const HuffTree& t, uint32_t mbits, DecTables& out);
 
 // HUFF_DISABLE_FIXED8=1 forces the general kernels even for all-8-bit codes
 bool fixed8_disabled();
-// HUFF_DEC_VARIANT=11|12|13 -> k_decode_fixed self-check mode 1|2|3 (else 0)
+// HUFF_DEC_VARIANT=11 -> k_decode_fixed's self-checking build (mode 1; else 0)
 uint32_t decode_check_mode();
 
 Status build_dec_tables(const HuffTree& t, DecTables& out);
