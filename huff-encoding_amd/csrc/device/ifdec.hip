@@ -47,6 +47,26 @@
 
 #include "bitreader.hpp"
 
+// Blocks are numbered by a dynamic ticket (one device-scope atomic per block),
+// so a block only ever waits on blocks that started before it. IFD_TICKET=0
+// numbers them by blockIdx instead (relies on in-order dispatch; a violation
+// ends in the spin limit and the host's fallback, not a hang): measured the
+// same on 1 GiB Zipf/text (3.31 vs 3.31 ms), so the ticket stays.
+#ifndef IFD_TICKET
+#define IFD_TICKET 1
+#endif
+// IFD_DBG builds (tools/build_variant.sh) write each block's phase timestamps
+// (s_memrealtime, 100 MHz) to a.dbg[8 b ...]: entry, staged, decoded, fixed,
+// aggregate published, offset known, written; [7] = CU id << 32 | slow lanes
+#ifndef IFD_DBG
+#define IFD_DBG 0
+#endif
+#if IFD_DBG
+#define IFD_T(k) do { if (t == 0 && a.dbg) a.dbg[8ull * b + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define IFD_T(k) do { } while (0)
+#endif
+
 namespace huff::dev {
 
 namespace {
@@ -59,7 +79,8 @@ constexpr uint32_t kPfCap = kIfdPrefixCap;
 // look-back word: status in bits [62, 64) (1 aggregate, 2 inclusive prefix),
 // kStBroken (this block's true exit is not the next block's anchor), value
 constexpr uint64_t kStAgg = 1ull << 62, kStIncl = 2ull << 62, kStBroken = 1ull << 61, kStVal = (1ull << 61) - 1;
-constexpr uint32_t kSpinLimit = 1u << 26;  // look-back polls before the kernel gives up (error flag)
+constexpr uint32_t kSpinLimit = 1u << 20;  // look-back polls (>= ~1 s) before the kernel gives up (flag 4: the host
+                                           // reruns the stream through the multi-kernel path)
 
 struct Lds {
     uint16_t* stab;
@@ -184,17 +205,29 @@ __global__ __launch_bounds__(kT) void k_ifd(IfdArgs a) {
     const Lds L = lds_layout(a, smem);
     const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const uint32_t K = a.stab_bits;
+#if IFD_DBG
+    const uint64_t t_entry = __builtin_amdgcn_s_memrealtime();
+#endif
 
     // ---- 1. ticket, table, stage -------------------------------------------
+#if IFD_TICKET
     if (t == 0) L.misc[0] = atomicAdd(a.ticket, 1u);
+#endif
     {
         const uint32_t tab_words = ((1u << K) + 1) / 2;
         uint32_t* tw = reinterpret_cast<uint32_t*>(L.stab);
         for (uint32_t i = t; i < tab_words; i += kT) tw[i] = reinterpret_cast<const uint32_t*>(a.stab)[i];
     }
     __syncthreads();
+#if IFD_TICKET
     const uint32_t b = __builtin_amdgcn_readfirstlane(L.misc[0]);
+#else
+    const uint32_t b = blockIdx.x;
+#endif
     if (b >= a.nblocks) return;  // never: the grid is nblocks workgroups
+#if IFD_DBG
+    if (t == 0 && a.dbg) a.dbg[8ull * b] = t_entry;
+#endif
     const uint64_t seg0 = static_cast<uint64_t>(b) * kBlockSegs;
     const uint64_t byte_lo = ((seg0 * a.seg_bits) >> 3) & ~15ull;
     const uint64_t bit_lo = byte_lo * 8;
@@ -217,6 +250,7 @@ __global__ __launch_bounds__(kT) void k_ifd(IfdArgs a) {
     }
     __syncthreads();
 
+    IFD_T(1);
     // ---- 2. speculative decode of 64 codes -----------------------------------
     const uint64_t k = seg0 + t;
     const bool live = k < a.nseg;
@@ -263,6 +297,7 @@ __global__ __launch_bounds__(kT) void k_ifd(IfdArgs a) {
     for (int r = 0; r < static_cast<int>(kQm / 2); ++r) reinterpret_cast<uint32_t*>(L.qm)[r * kT + t] = q[r];
     L.ex[t] = x_spec;
     __syncthreads();
+    IFD_T(2);
 
     // ---- 3. fix-up -----------------------------------------------------------
     const bool owned = live && (t > 0 || b == 0);
@@ -323,6 +358,13 @@ __global__ __launch_bounds__(kT) void k_ifd(IfdArgs a) {
         }
     };
     settle(owned && x_true != x_spec);
+    IFD_T(3);
+#if IFD_DBG
+    {
+        const int ns_slow = __syncthreads_count(slow);
+        if (t == 0 && a.dbg) a.dbg[8ull * b + 7] = (static_cast<uint64_t>(__smid()) << 32) | static_cast<uint32_t>(ns_slow);
+    }
+#endif
 
     // ---- 4. counts, anchors, look-back ---------------------------------------
     // The block's count assumes its anchor (lane 0's speculative exit) is
@@ -363,26 +405,54 @@ __global__ __launch_bounds__(kT) void k_ifd(IfdArgs a) {
             __builtin_amdgcn_s_sleep(1);
         }
     };
-    // Look-back (thread 0). The aggregate published first assumes this
+    // Look-back (wave 0, lane 0 publishes). The aggregate published first assumes this
     // block's anchor is true; a BROKEN bit on any record met on the way back
     // means some later block may be repairing itself, so the scan then waits
     // for the predecessor's inclusive record instead, whose BROKEN bit and
     // value are final (a record's BROKEN bit changes only in a block that
     // repairs, and only a BROKEN predecessor makes a block repair).
-    if (t == 0) {
+    if (wave == 0) {
         const uint64_t brk = L.misc[4] ? kStBroken : 0ull;
         uint64_t O = 0;
         uint32_t repair = 0;
         if (b > 0) {
-            __hip_atomic_store(a.status + b, kStAgg | brk | cb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (lane == 0)
+                __hip_atomic_store(a.status + b, kStAgg | brk | cb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            IFD_T(4);
+            // windows of 64 predecessors, nearest in lane 0: the window is
+            // used once every word up to its nearest inclusive prefix (or all
+            // 64 words) is published; the aggregates before that prefix, and
+            // the prefix, are summed (words before block 0 read as prefix 0)
             bool seen = false;
-            for (int64_t v = static_cast<int64_t>(b) - 1;; --v) {
-                const uint64_t s = spin_load(static_cast<uint64_t>(v));
-                seen |= (s & kStBroken) != 0;
-                O += s & kStVal;
-                if ((s >> 62) == 2 || v == 0) break;
+            int64_t top = static_cast<int64_t>(b) - 1;
+            for (uint32_t spins = 0;;) {
+                const int64_t v = top - static_cast<int64_t>(lane);
+                const uint64_t s = v >= 0 ? __hip_atomic_load(a.status + v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                          : kStIncl;
+                const uint64_t incl = __ballot((s >> 62) == 2);
+                const uint64_t ready = __ballot((s >> 62) != 0);
+                const uint32_t fi = incl ? static_cast<uint32_t>(__builtin_ctzll(incl)) : 64u;
+                const uint64_t need = fi >= 63 ? ~0ull : ((2ull << fi) - 1);
+                if ((ready & need) != need) {
+                    if (++spins > kSpinLimit) {
+                        if (lane == 0) atomicOr(a.flags, 4u);  // a predecessor never published: report, do not hang
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;
+                }
+                const uint32_t av = lane < fi ? static_cast<uint32_t>(s & kStVal) : 0u;
+                O += __builtin_amdgcn_readlane(static_cast<int>(wave_scan_incl(av)), 63) & 0xFFFFFFFFull;
+                seen |= __ballot(lane <= fi && (s & kStBroken) != 0) != 0;
+                if (fi < 64) {
+                    const uint64_t iv = s & kStVal;
+                    O += (static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(iv >> 32), static_cast<int>(fi)))) << 32) |
+                         static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(iv), static_cast<int>(fi)));
+                    break;
+                }
+                top -= 64;
             }
-            if (seen) {
+            if (lane == 0 && seen) {
                 uint64_t r = spin_load(b - 1);
                 for (uint32_t spins = 0; (r >> 62) != 2; ++spins) {
                     if (spins > kSpinLimit) {
@@ -403,11 +473,14 @@ __global__ __launch_bounds__(kT) void k_ifd(IfdArgs a) {
                 }
             }
         }
-        L.misc[1] = static_cast<uint32_t>(O);
-        L.misc[2] = static_cast<uint32_t>(O >> 32);
-        L.misc[6] = repair;
+        if (lane == 0) {
+            L.misc[1] = static_cast<uint32_t>(O);
+            L.misc[2] = static_cast<uint32_t>(O >> 32);
+            L.misc[6] = repair;
+        }
     }
     __syncthreads();
+    IFD_T(5);
     if (L.misc[6]) {  // repair: lane 0's exit is the previous block's true exit
         if (t == 0) x_true = L.misc[5];
         settle(t == 0);
@@ -494,6 +567,7 @@ __global__ __launch_bounds__(kT) void k_ifd(IfdArgs a) {
                 if (i >= img0 && i < end) a.out[gbase + i] = L.out[i];
         }
     }
+    IFD_T(6);
 }
 
 }  // namespace

@@ -184,6 +184,7 @@ struct IfdArgs {
     unsigned int* flags;          // zeroed; 2: out_cap too small, 4: the look-back gave up
     unsigned long long* total;    // letters
     unsigned long long* end_bit;  // may be null: the bit after the last complete code
+    unsigned long long* dbg;      // [nblocks][8] phase timestamps (builds with IFD_DBG only; else unused)
     // LDS layout (ifd_layout)
     uint32_t stage_off, stage_bytes, qm_off, pf_off, ex_off, cnt_off, misc_off, out_off, out_img;
 };

@@ -1173,7 +1173,25 @@ static Status decode_indexless_single(huff_ctx* ctx, const uint8_t* d_comp, uint
         a.out = dst;
         a.out_cap = cap;
         HIP_TRY(hipMemsetAsync(st.ifd.p, 0, scratch, strm));
+        // HUFF_IFD_DBG=<file>: per-block phase timestamps of an IFD_DBG build
+        const char* dbg_path = std::getenv("HUFF_IFD_DBG");
+        DevBuf dbg;
+        if (dbg_path) {
+            HUFF_TRY(dbg.ensure(64 * static_cast<size_t>(a.nblocks)));
+            HIP_TRY(hipMemsetAsync(dbg.p, 0, 64 * static_cast<size_t>(a.nblocks), strm));
+            a.dbg = static_cast<unsigned long long*>(dbg.p);
+        }
         HUFF_TRY(ctx->timed("indexless_decode", [&] { return dev::launch_ifd(a, strm); }));
+        if (dbg_path) {
+            std::vector<uint64_t> h(8 * static_cast<size_t>(a.nblocks));
+            HIP_TRY(hipMemcpyAsync(h.data(), dbg.p, 64 * static_cast<size_t>(a.nblocks), hipMemcpyDeviceToHost, strm));
+            HUFF_TRY(ctx->sync());
+            if (FILE* f = std::fopen(dbg_path, "wb")) {
+                std::fwrite(h.data(), 8, h.size(), f);
+                std::fclose(f);
+            }
+            a.dbg = nullptr;
+        }
         HIP_TRY(hipMemcpyAsync(res, st.ifd.p, 144, hipMemcpyDeviceToHost, strm));
         HUFF_TRY(ctx->sync());
         const uint32_t flags = static_cast<uint32_t>(res[0]);
@@ -1189,8 +1207,9 @@ static Status decode_indexless_single(huff_ctx* ctx, const uint8_t* d_comp, uint
                          double(res[10]), double(res[11]), double(res[12]), double(res[13]), double(res[14]),
                          double(res[15]));
         }
-        if (flags & 4u) return Status::err(HUFF_E_HIP, "index-free decode: the look-back did not complete");
-        if (flags & 1u) return Status::ok();  // not self-synchronising here: the multi-kernel path
+        // 1: not self-synchronising here; 4: a look-back gave up waiting (never
+        // seen; it would mean blocks ran out of index order): the multi-kernel path
+        if (flags & 5u) return Status::ok();
         *nsym = res[17];
         if (!(flags & 2u)) break;
         if (d_user) return Status::err(HUFF_E_BUFFER_TOO_SMALL, "output buffer too small");
