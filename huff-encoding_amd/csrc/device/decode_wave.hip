@@ -242,6 +242,9 @@ __device__ __forceinline__ void decode_fixed64(const Words& src, uint32_t rel, u
         X -= e;                                                                               \
     } while (0)
 
+#ifdef HUFF_SKIP_EXPERIMENT  // timing only (wrong letters): 1 = no skip codes, 2 = the wave's max for all lanes
+    if constexpr (SKIP) skip = HUFF_SKIP_EXPERIMENT == 1 ? 0u : __reduce_max_sync(~0ull, skip);
+#endif
     if constexpr (SKIP) {  // codes before this lane's first letter: decoded, not kept
         for (uint32_t j = skip; j >= 2; j -= 2) {
             FX_REFILL();

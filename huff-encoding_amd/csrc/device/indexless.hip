@@ -236,7 +236,8 @@ Seg make_seg(const IndexlessArgs& a) {
 
 struct Staged {
     const uint32_t* w;
-    uint64_t base;  // bit position of w[0]'s most significant bit
+    uint64_t base;       // bit position of w[0]'s most significant bit
+    const uint32_t* l2;  // the level-2 length table in LDS (null: the global multi-level table)
 };
 
 // The block's range from its 16-B granule, 8 loads of 16 B per lane in
@@ -264,7 +265,7 @@ __device__ Staged stage_block(const IndexlessArgs& a, uint32_t* w) {
         for (int k = 0; k < 8; ++k)
             if (p0 + k * kThreads < np) w4[p0 + k * kThreads] = v[k];
     }
-    return Staged{w, byte_lo * 8};
+    return Staged{w, byte_lo * 8, nullptr};
 }
 
 struct LaneBits {
@@ -309,10 +310,12 @@ constexpr int kChunkSteps = 8;
 // every two codes (the next dword is read one refill ahead)
 struct Cursor {
     const uint32_t* w;
+    const uint32_t* l2;
     uint64_t buf;
     uint32_t X, rp, nextw;
     __device__ __forceinline__ void init(const Staged& st, uint64_t p) {
         w = st.w;
+        l2 = st.l2;
         const uint64_t rel = p - st.base;
         rp = static_cast<uint32_t>(rel >> 5);
         const uint32_t sh = static_cast<uint32_t>(rel & 31);
@@ -328,10 +331,23 @@ struct Cursor {
         nextw = __builtin_bswap32(w[rp]);
     }
     // the length of the next code, consumed; codes longer than the table's
-    // index (kSsSlow) through the global multi-level table
+    // index (kSsSlow) through the level-2 length table in LDS (descriptor
+    // index in the entry's bits [0, 7) and [8, 16)), else the global
+    // multi-level table
     template <bool SLOW>
     __device__ __forceinline__ uint32_t step(const uint16_t* stab, uint32_t K, const uint32_t* glut, uint32_t Kg) {
         uint32_t e = stab[static_cast<uint32_t>(buf >> 32) >> (32 - K)];
+        if (SLOW && (e & kSsSlow) && l2) {
+            refill();  // >= 32 valid bits: the whole code (<= 32 bits)
+            const uint32_t d = l2[(e & 0x7Fu) | ((e >> 8) << 7)];
+            const uint32_t E = d & 31u;
+            const uint32_t j = (static_cast<uint32_t>(buf >> 32) << K) >> (32 - E);
+            const uint32_t l1 = reinterpret_cast<const uint8_t*>(l2)[(d >> 5) + j];
+            buf <<= l1;
+            X -= l1;
+            refill();
+            return l1;
+        }
         if (SLOW && (e & kSsSlow)) {
             refill();
             uint32_t e1 = glut[static_cast<uint32_t>(buf >> (64 - Kg))];
@@ -386,19 +402,54 @@ struct Cursor {
     }
 };
 
+// A sample word (segments of < 1024 bits): bits [0, 10) = offset of a
+// boundary of the speculative path from the segment start, [10, 20) = its
+// spec-local code index, [20, 27) / [27, 32) = how far back (bits / codes)
+// the chunk end before it lies, a second boundary between two samples (0
+// codes: none). k_mark_lite starts a mark from the nearest of both, so the
+// fixed-count decoder's lanes skip ~half as many codes; ~0u: no sample.
+#ifndef HUFF_HALF_SAMPLES
+#define HUFF_HALF_SAMPLES 1
+#endif
+__device__ __forceinline__ uint32_t samp_off(uint32_t v) { return v & 1023u; }
+__device__ __forceinline__ uint32_t samp_idx(uint32_t v) { return (v >> 10) & 1023u; }
+// the nearest boundary at or before spec-local code u among a segment's
+// samples (main and half): (code index, bit offset); (0, 0) = the segment start
+__device__ __forceinline__ void samp_pick(const uint32_t (&sv)[kSampMax], uint32_t u, uint32_t& idx, uint32_t& rel) {
+    idx = 0;
+    rel = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kSampMax; ++k) {  // ascending: half_k < main_k < half_k+1
+        const uint32_t v = sv[k];
+        const bool valid = v != ~0u;
+        const uint32_t mi = samp_idx(v), mo = samp_off(v), dc = v >> 27, db = (v >> 20) & 127u;
+        const bool okh = valid && dc != 0 && mi - dc <= u;
+        idx = okh ? mi - dc : idx;
+        rel = okh ? mo - db : rel;
+        const bool ok = valid && mi <= u;
+        idx = ok ? mi : idx;
+        rel = ok ? mo : rel;
+    }
+}
+
 // LDS: [single-symbol table][walk table (if any)][staged input]
 __device__ __forceinline__ uint32_t stab_words(const IndexlessArgs& a) {
     return ((((1u << a.stab_bits) + 1) / 2) + 3) & ~3u;
 }
 __device__ __forceinline__ uint32_t tables_words(const IndexlessArgs& a) {
-    return stab_words(a);
+    return stab_words(a) + a.l2_words;
 }
 __device__ __forceinline__ const uint16_t* load_stab(const IndexlessArgs& a, uint32_t* lds) {
     // the walk table when there is one (its low bits are stab's lengths), else stab
     const uint32_t words = ((1u << a.stab_bits) + 1) / 2;
     const uint32_t* src = reinterpret_cast<const uint32_t*>(a.wtab ? a.wtab : a.stab);
     for (uint32_t i = threadIdx.x; i < words; i += blockDim.x) lds[i] = src[i];
+    for (uint32_t i = threadIdx.x; i < a.l2_words; i += blockDim.x) lds[stab_words(a) + i] = a.l2[i];
     return reinterpret_cast<const uint16_t*>(lds);
+}
+__device__ __forceinline__ Staged with_l2(Staged st, const IndexlessArgs& a, const uint32_t* lds) {
+    st.l2 = a.l2_words ? lds + stab_words(a) : nullptr;
+    return st;
 }
 
 template <bool SLOW>
@@ -406,7 +457,7 @@ __global__ __launch_bounds__(kThreads) void k_spec_lds(IndexlessArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const uint16_t* stab = load_stab(a, lds);
     const uint16_t* wtab = a.wtab ? stab : nullptr;  // one table serves single and multi-code steps
-    const Staged st = stage_block(a, lds + tables_words(a));
+    const Staged st = with_l2(stage_block(a, lds + tables_words(a)), a, lds);
     __syncthreads();
     const uint64_t i0 = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
     const bool live = i0 < a.nseg;  // no early return: the fix-up below has a barrier
@@ -425,15 +476,22 @@ __global__ __launch_bounds__(kThreads) void k_spec_lds(IndexlessArgs a) {
     uint64_t next_bit = (a.nsamp && live) ? start + kSampBits : ~0ull;
     uint64_t sp1 = ~0ull;  // the first sample (position, spec-local index)
     uint32_t si1 = 0;
+    uint64_t pc = start, pcn = 0, last_main = start;  // the previous chunk end, the last sample
     auto note_sample = [&]() {
         if (cur >= next_bit) {
-            smp[next_k - 1] = (static_cast<uint32_t>(cnt) << 16) | static_cast<uint32_t>(cur - start);
+            const uint64_t db = cur - pc, dc = cnt - pcn;
+            const bool half = HUFF_HALF_SAMPLES && pc > last_main && db <= 127 && dc <= 31;
+            smp[next_k - 1] = static_cast<uint32_t>(cur - start) | (static_cast<uint32_t>(cnt) << 10) |
+                              (half ? static_cast<uint32_t>((db << 20) | (dc << 27)) : 0u);
             if (next_k == 1) {  // kept for the fix-up below
                 sp1 = cur;
                 si1 = static_cast<uint32_t>(cnt);
             }
+            last_main = cur;
             next_bit = ++next_k <= a.nsamp ? next_bit + kSampBits : ~0ull;
         }
+        pc = cur;
+        pcn = cnt;
     };
     if (wtab) {
         // multi-code chunks while the chunk's last boundary stays below `end`
@@ -533,8 +591,8 @@ __global__ __launch_bounds__(kThreads) void k_spec_lds(IndexlessArgs a) {
             while (pa > pk) {  // passed the sample without landing on it: the next one
                 const uint32_t sv = k < a.nsamp ? smp[k] : ~0u;
                 ++k;
-                pk = sv == ~0u ? ~0ull : start + (sv & 0xFFFFu);
-                ik = sv >> 16;
+                pk = sv == ~0u ? ~0ull : start + samp_off(sv);
+                ik = samp_idx(sv);
             }
         }
         s_out = ns;
@@ -578,7 +636,7 @@ __global__ __launch_bounds__(kThreads) void k_mark_lds(IndexlessArgs a, const ui
                                                        uint64_t* __restrict__ sub_abs, uint32_t shift) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const uint16_t* stab = load_stab(a, lds);
-    const Staged st = stage_block(a, lds + tables_words(a));
+    const Staged st = with_l2(stage_block(a, lds + tables_words(a)), a, lds);
     __syncthreads();
     const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
     if (i >= a.nseg) return;
@@ -604,13 +662,8 @@ __global__ __launch_bounds__(kThreads) void k_mark_lds(IndexlessArgs a, const ui
             pos = walk<SLOW>(st, s_true, static_cast<uint32_t>(t), stab, K, a.lut, Kg);
         } else {
             const uint32_t u = static_cast<uint32_t>(static_cast<int64_t>(t) - dl);
-            uint32_t idx = 0, rel = 0;
-#pragma unroll
-            for (uint32_t k = 0; k < kSampMax; ++k) {  // samples ascend; ~0u never qualifies
-                const bool ok = (sv[k] >> 16) <= u;
-                idx = ok ? sv[k] >> 16 : idx;
-                rel = ok ? sv[k] & 0xFFFFu : rel;
-            }
+            uint32_t idx, rel;
+            samp_pick(sv, u, idx, rel);
             pos = walk<SLOW>(st, s_spec + rel, u - idx, stab, K, a.lut, Kg);
         }
         sub_abs[m >> shift] = pos;
@@ -645,13 +698,8 @@ __global__ __launch_bounds__(kThreads) void k_mark_lite(IndexlessArgs a, const u
             skip = t;
         } else {
             const uint32_t u = static_cast<uint32_t>(static_cast<int64_t>(t) - dl);
-            uint32_t idx = 0, rel = 0;
-#pragma unroll
-            for (uint32_t k = 0; k < kSampMax; ++k) {  // samples ascend; ~0u never qualifies
-                const bool ok = (sv[k] >> 16) <= u;
-                idx = ok ? sv[k] >> 16 : idx;
-                rel = ok ? sv[k] & 0xFFFFu : rel;
-            }
+            uint32_t idx, rel;
+            samp_pick(sv, u, idx, rel);
             pos = s_spec + rel;
             skip = u - idx;
         }
@@ -670,12 +718,13 @@ hipError_t launch_indexless_mark_lite(const IndexlessArgs& a, const uint64_t* of
 }
 
 static size_t lds_staged_bytes(const IndexlessArgs& a) {
-    return static_cast<size_t>(((((1u << a.stab_bits) + 1) / 2) + 3) & ~3u) * 4 +
+    return static_cast<size_t>((((((1u << a.stab_bits) + 1) / 2) + 3) & ~3u) + a.l2_words) * 4 +
            ((kThreads * a.seg_bits + 7) / 8 + 128 + 15) / 16 * 16;
 }
 
 static bool use_staged(const IndexlessArgs& a) {
-    return a.stab && a.stab_bits && a.max_len <= 32 && lds_staged_bytes(a) <= 160 * 1024;
+    // (the sample words hold 10-bit offsets and counts: segments < 1024 bits)
+    return a.stab && a.stab_bits && a.max_len <= 32 && a.seg_bits < 1024 && lds_staged_bytes(a) <= 160 * 1024;
 }
 
 hipError_t launch_indexless_mark(const IndexlessArgs& a, const uint64_t* off, uint64_t* sub_abs, uint32_t shift,

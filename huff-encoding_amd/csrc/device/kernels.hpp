@@ -26,7 +26,6 @@ constexpr uint32_t kLongMaxLen = 57;    // u64 table entries: code << 6 | len
 constexpr uint32_t kHistCopies = 8;     // XCD-group copies of the global weights
 constexpr uint32_t kLutMaxBits = 12;    // primary decode table index bits
 constexpr uint32_t kLutPtr = 0x80000000u;
-constexpr uint32_t kPackWaveRound = 1024;  // bytes per wave round in pack (64 lanes x 16 B: ~80 VGPRs, 6 waves per SIMD)
 #ifndef HUFF_PACK_WAVES
 #define HUFF_PACK_WAVES 8
 #endif
@@ -159,6 +158,11 @@ struct IndexlessArgs {
     // bits of all the window's complete codes, [12, 16) = their count
     // (null: single steps from stab only)
     const uint16_t* wtab;
+    // level-2 length table (DecTables::l2off: descriptors, then u8 lengths),
+    // staged in LDS after the single-symbol table; null: the slow steps read
+    // the global multi-level table `lut`
+    const uint32_t* l2;
+    uint32_t l2_words;
 };
 // single-pass index-free decode (ifdec.hip)
 constexpr uint32_t kIfdPrefixCap = 32;  // letters a lane's fix-up walk keeps before it gives up (slow lane)
@@ -349,6 +353,7 @@ hipError_t launch_decode_deep(const DecodeArgs& a, hipStream_t s);  // lut, lut_
 hipError_t launch_decode_deep_serial(const DeepSerialArgs& a, hipStream_t s);
 
 size_t pack_lds_bytes(bool long_codes, uint32_t max_len, uint32_t stage_words);
+uint32_t pack_round_bytes();  // input bytes per wave round of k_pack (its LDS stage holds one round's bits)
 uint32_t pack_waves_per_group(bool long_codes);
 size_t decode_lds_bytes(uint32_t lut_bits);
 // HUFF_DEC_VARIANT: 10 = k_decode_fixed (the default for codes <= 32 bits),

@@ -42,8 +42,19 @@ namespace {
 // 64 KiB table)
 template <bool LONG>
 constexpr int pack_waves() { return LONG ? 4 : static_cast<int>(kPackWaves); }
-constexpr uint32_t kBPL = kPackWaveRound / 64;  // consecutive input bytes per lane per round
+// consecutive input bytes per lane per round (HUFF_PACK_BPL) and rounds of
+// loads in flight ahead of the encoder (HUFF_PACK_AHEAD)
+#ifndef HUFF_PACK_BPL
+#define HUFF_PACK_BPL 16
+#endif
+#ifndef HUFF_PACK_AHEAD
+#define HUFF_PACK_AHEAD 2
+#endif
+constexpr uint32_t kBPL = HUFF_PACK_BPL;
+constexpr uint32_t kRoundB = 64 * kBPL;  // bytes per wave round
+constexpr int kAhead = HUFF_PACK_AHEAD;
 static_assert(kBPL % 16 == 0, "lanes load whole 16-byte pieces");
+static_assert(kBPL <= kIdx && kTaskSym % kRoundB == 0, "an index entry starts a lane; a task is whole rounds");
 constexpr int kPieces = kBPL / 16;
 
 struct LaneIn {
@@ -55,7 +66,10 @@ struct LaneIn {
 // (64 copies, so that letter b's address is one v_perm ((b << 8) | 4 lane)
 // instead of bfe + lshl_or, measured slower: the 64 KiB table leaves 4 waves
 // per SIMD instead of 6 — Zipf 0.481 vs 0.446 ms, text 0.440 vs 0.417)
-constexpr int kCopies = 32;
+#ifndef HUFF_PACK_COPIES
+#define HUFF_PACK_COPIES 32
+#endif
+constexpr int kCopies = HUFF_PACK_COPIES;
 template <bool LONG>
 constexpr uint32_t table_words() { return 256u * kCopies * (LONG ? 2u : 1u); }
 
@@ -64,7 +78,8 @@ __global__ __launch_bounds__(pack_waves<LONG>() * 64) void k_pack(PackArgs a) {
     constexpr int kWaves = pack_waves<LONG>();
     constexpr int kThreads = kWaves * 64;
     constexpr int C = kCopies;
-    constexpr int LOGC = 5;
+    constexpr int LOGC = C == 32 ? 5 : C == 16 ? 4 : C == 8 ? 3 : -1;
+    static_assert(LOGC > 0, "8, 16 or 32 table copies");
     using E = Entry<LONG>;
     using T = typename E::T;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -91,7 +106,7 @@ __global__ __launch_bounds__(pack_waves<LONG>() * 64) void k_pack(PackArgs a) {
         uint64_t stage_bit0 = (cs >> 7) << 7;  // global bit of stage word 0's MSB (16-B aligned)
         const uint64_t own_lo = cs >> 3;
         const uint64_t own_hi = (c + 1 == a.nchunks) ? (ce + 7) >> 3 : ce >> 3;
-        const uint32_t nrounds = static_cast<uint32_t>((nsym + kPackWaveRound - 1) / kPackWaveRound);
+        const uint32_t nrounds = static_cast<uint32_t>((nsym + kRoundB - 1) / kRoundB);
         // the chunk's bytes through a buffer resource (rounded up to the 16-B
         // granule of its end: bytes past n are masked by nvalid): loads past
         // it, and whole rounds past the chunk, read zeros, so the loads run
@@ -101,14 +116,12 @@ __global__ __launch_bounds__(pack_waves<LONG>() * 64) void k_pack(PackArgs a) {
         auto load_round = [&](uint32_t r) {
             LaneIn x;
 #pragma unroll
-            for (int q = 0; q < kPieces; ++q) x.v[q] = buf_ld16(rin, r * kPackWaveRound + lane * kBPL + 16 * q);
+            for (int q = 0; q < kPieces; ++q) x.v[q] = buf_ld16(rin, r * kRoundB + lane * kBPL + 16 * q);
             return x;
         };
-        LaneIn v0 = load_round(0);
-        LaneIn v1 = load_round(1);
-#if HUFF_PACK_AHEAD3
-        LaneIn v2 = load_round(2);
-#endif
+        LaneIn vq[kAhead];
+#pragma unroll
+        for (int i = 0; i < kAhead; ++i) vq[i] = load_round(i);
 
         // bits of the shared first byte that belong to the symbols before this chunk
         if (lane == 0 && (cs & 7)) {
@@ -140,18 +153,14 @@ __global__ __launch_bounds__(pack_waves<LONG>() * 64) void k_pack(PackArgs a) {
         wave_sync();
 
         uint64_t round_bit = cs, task_bit0 = cs;
-        static_assert(kTaskSym == 4 * kPackWaveRound, "a decode task is 4 pack rounds");
+        constexpr uint32_t kRoundsPerTask = kTaskSym / kRoundB;
         for (uint32_t r = 0; r < nrounds; ++r) {
-            const LaneIn v = v0;
-            v0 = v1;
-#if HUFF_PACK_AHEAD3
-            v1 = v2;
-            v2 = load_round(r + 3);
-#else
-            v1 = load_round(r + 2);
-#endif
+            const LaneIn v = vq[0];
+#pragma unroll
+            for (int i = 0; i + 1 < kAhead; ++i) vq[i] = vq[i + 1];
+            vq[kAhead - 1] = load_round(r + kAhead);
             // 32-bit: a chunk holds at most 65536 symbols
-            const uint32_t s_in_chunk = r * kPackWaveRound + lane * kBPL;
+            const uint32_t s_in_chunk = r * kRoundB + lane * kBPL;
             const uint32_t nsym32 = static_cast<uint32_t>(nsym);
             const int nvalid = s_in_chunk >= nsym32 ? 0
                                                     : static_cast<int>(nsym32 - s_in_chunk < kBPL ? nsym32 - s_in_chunk : kBPL);
@@ -167,7 +176,7 @@ __global__ __launch_bounds__(pack_waves<LONG>() * 64) void k_pack(PackArgs a) {
             }
             T ent[kBPL];
             auto lookup = [&](int k) -> T { return tab[(((wv[k >> 2] >> (8 * (k & 3))) & 0xFFu) << LOGC) | copy]; };
-            if ((r + 1ull) * kPackWaveRound <= nsym) {  // whole round (wave-uniform): no per-letter masks
+            if ((r + 1ull) * kRoundB <= nsym) {  // whole round (wave-uniform): no per-letter masks
 #pragma unroll
                 for (int k = 0; k < static_cast<int>(kBPL); ++k) ent[k] = lookup(k);
             } else {
@@ -191,9 +200,9 @@ __global__ __launch_bounds__(pack_waves<LONG>() * 64) void k_pack(PackArgs a) {
             const uint32_t excl = incl - bits;
 
             if (a.sub16) {  // compact index: a u64 base per task of 4 rounds, u16 offsets
-                if ((r & 3u) == 0) {
+                if ((r % kRoundsPerTask) == 0) {
                     task_bit0 = round_bit;
-                    if (lane == 0) a.task_base[(sym0 + r * kPackWaveRound) / kTaskSym] = round_bit;
+                    if (lane == 0) a.task_base[(sym0 + r * kRoundB) / kTaskSym] = round_bit;
                 }
                 if (nvalid > 0 && (s_in_chunk & (kIdx - 1)) == 0)
                     a.sub16[(sym0 + s_in_chunk) / kIdx] = static_cast<uint16_t>(round_bit - task_bit0 + excl);
@@ -244,6 +253,8 @@ size_t pack_lds_bytes(bool long_codes, uint32_t max_len, uint32_t stage_words) {
     const uint32_t waves = long_codes ? pack_waves<true>() : pack_waves<false>();
     return static_cast<size_t>(table + waves * stage_words) * 4;
 }
+
+uint32_t pack_round_bytes() { return kRoundB; }
 
 uint32_t pack_waves_per_group(bool long_codes) { return long_codes ? pack_waves<true>() : pack_waves<false>(); }
 

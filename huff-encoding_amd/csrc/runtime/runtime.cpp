@@ -225,6 +225,78 @@ static void build_walk_table(const HuffTree& t, uint32_t sbits, DecTables& out) 
     }
 }
 
+// The sync kernels' level-2 length table (DecTables::l2off): for every
+// sbits-bit window whose first code is longer, the lengths of the codes below
+// that node, indexed by exactly the E bits its deepest leaf needs; the slow
+// entries of the single-symbol and walk tables get the descriptor index. Only
+// the code lengths matter to the speculative pass and the marks, so a window
+// that once took two dependent global reads (the 8-bit secondary tables) takes
+// two LDS reads. Skipped past kL2MaxBytes (the LDS beside the stage) or for
+// codes > 32 bits.
+static void build_len_l2(const HuffTree& t, DecTables& out) {
+    constexpr size_t kL2MaxBytes = 24 * 1024;
+    constexpr uint32_t kMaxDesc = 1u << 15;
+    const uint32_t K = out.sbits;
+    if (t.root_is_leaf() || out.maxdepth <= K || out.maxdepth > 32) return;
+    const auto& nodes = t.nodes();
+    std::vector<uint32_t> desc;
+    std::vector<uint8_t> lens;
+    std::vector<std::pair<uint32_t, uint32_t>> slow;  // (window, descriptor)
+    for (uint32_t i = 0; i < (1u << K); ++i) {
+        int32_t x = t.root();
+        bool leaf = false;
+        for (uint32_t p = 0; p < K && !leaf; ++p) {
+            x = ((i >> (K - 1 - p)) & 1u) ? nodes[x].right : nodes[x].left;
+            leaf = nodes[x].is_leaf;
+        }
+        if (leaf) continue;
+        uint32_t E = 0;  // the deepest leaf below x, relative to x
+        std::vector<std::pair<int32_t, uint32_t>> st{{x, 0}};
+        while (!st.empty()) {
+            auto [y, d] = st.back();
+            st.pop_back();
+            if (nodes[y].is_leaf) {
+                E = std::max(E, d);
+            } else {
+                st.push_back({nodes[y].left, d + 1});
+                st.push_back({nodes[y].right, d + 1});
+            }
+        }
+        if (desc.size() >= kMaxDesc || K + E > 32) return;
+        desc.push_back(static_cast<uint32_t>((lens.size() << 5) | E));  // byte offset fixed below
+        slow.push_back({i, static_cast<uint32_t>(desc.size() - 1)});
+        for (uint32_t j = 0; j < (1u << E); ++j) {
+            int32_t y = x;
+            uint32_t r = E;
+            for (uint32_t p = 0; p < E; ++p) {
+                y = ((j >> (E - 1 - p)) & 1u) ? nodes[y].right : nodes[y].left;
+                if (nodes[y].is_leaf) {
+                    r = p + 1;
+                    break;
+                }
+            }
+            lens.push_back(static_cast<uint8_t>(K + r));
+        }
+        if (desc.size() * 4 + lens.size() > kL2MaxBytes) return;
+    }
+    if (desc.empty()) return;
+    const uint32_t base = static_cast<uint32_t>(desc.size() * 4);
+    for (uint32_t& d : desc) d = (((d >> 5) + base) << 5) | (d & 31u);
+    out.l2off = static_cast<uint32_t>(out.lut.size());
+    out.l2words = static_cast<uint32_t>((desc.size() * 4 + lens.size() + 15) / 16 * 4);
+    out.lut.resize(out.lut.size() + out.l2words, 0);
+    uint8_t* b = reinterpret_cast<uint8_t*>(out.lut.data() + out.l2off);
+    std::memcpy(b, desc.data(), desc.size() * 4);
+    std::memcpy(b + base, lens.data(), lens.size());
+    uint16_t* s = reinterpret_cast<uint16_t*>(out.lut.data() + out.soff);
+    uint16_t* w = reinterpret_cast<uint16_t*>(out.lut.data() + out.woff);
+    for (auto [i, d] : slow) {
+        const uint16_t e = static_cast<uint16_t>(dev::kSsSlow | (d & 0x7Fu) | ((d >> 7) << 8));
+        s[i] = e;
+        w[i] = e;
+    }
+}
+
 Status build_dec_tables(const HuffTree& t, DecTables& out) {
     const auto& nodes = t.nodes();
     out.lut.clear();
@@ -286,6 +358,7 @@ Status build_dec_tables(const HuffTree& t, DecTables& out) {
     build_multi_table(t, ms_bits(), out);
     build_single_table(t, std::min<uint32_t>(maxd, dev::kSsMaxBits), out);
     build_walk_table(t, out.sbits, out);
+    build_len_l2(t, out);
     return Status::ok();
 }
 
@@ -646,9 +719,9 @@ huff::Status huff_enc::pack(const huff_tree* t, uint64_t base, const uint8_t* pr
         a.sub_bit = nullptr;
     }
     a.prev_tail_len = static_cast<uint32_t>(prev_tail_len);
-    // one wave round: <= kPackWaveRound*maxlen bits + a < 128-bit carry (+ the
+    // one wave round: <= round bytes * maxlen bits + a < 128-bit carry (+ the
     // 128-bit window past the last unit, which the OR emit may touch with zero)
-    a.stage_words = (huff::dev::kPackWaveRound / 32 * std::max<uint32_t>(et.maxlen, 1) + 12 + 3) & ~3u;
+    a.stage_words = (huff::dev::pack_round_bytes() / 32 * std::max<uint32_t>(et.maxlen, 1) + 12 + 3) & ~3u;
     a.max_len = et.maxlen;
     const size_t lds = huff::dev::pack_lds_bytes(long_codes, et.maxlen, a.stage_words);
     const uint32_t per_cu = std::max<uint32_t>(1, std::min<uint32_t>(8, static_cast<uint32_t>((160 * 1024) / lds)));
@@ -1006,6 +1079,8 @@ Status indexless_sync(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_bytes,
             S = static_cast<uint64_t>(g) * k;
             break;
         }
+    // the staged kernels' sample words hold 10-bit offsets (indexless.hip)
+    if (dt->maxdepth <= 32 && S >= 1024) S = static_cast<uint64_t>(g) * (1023 / g);
     const uint64_t nseg = (valid_bits + S - 1) / S;
     if (nseg > 0xFFFFFFFFull) return Status::err(HUFF_E_INVALID_ARG, "stream too long for one decode");
     HUFF_TRY(st.s.ensure(nseg * 8));
@@ -1033,6 +1108,10 @@ Status indexless_sync(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_bytes,
     a.stab = reinterpret_cast<const uint16_t*>(static_cast<const uint32_t*>(ctx->d_lut.p) + dt->soff);
     a.stab_bits = dt->sbits;
     a.wtab = reinterpret_cast<const uint16_t*>(static_cast<const uint32_t*>(ctx->d_lut.p) + dt->woff);
+    if (dt->l2words && !std::getenv("HUFF_NO_L2")) {  // HUFF_NO_L2=1: the global secondary tables (A/B)
+        a.l2 = static_cast<const uint32_t*>(ctx->d_lut.p) + dt->l2off;
+        a.l2_words = dt->l2words;
+    }
     a.tm = static_cast<uint32_t*>(st.tm.p);
     a.dl = static_cast<int32_t*>(st.dl.p);
     a.flags = static_cast<unsigned int*>(st.flag.p);

@@ -54,6 +54,12 @@ struct DecTables {
     // multi-code walk table (indexless.hip's speculative pass): [1 << sbits]
     // u16 entries at word `woff`: first length | kSsSlow | used << 8 | count << 12
     uint32_t woff = 0;
+    // level-2 length table for the sync kernels (codes longer than sbits,
+    // <= 32 bits): `l2words` words at word `l2off` = nd u32 descriptors
+    // (byte offset of the prefix's entries in this block << 5 | its index
+    // bits E) then u8 code lengths; the slow entries of stab and the walk
+    // table carry their descriptor index in bits [0, 7) and [8, 16). 0: none
+    uint32_t l2off = 0, l2words = 0;
 };
 
 // append the multi-symbol table (decode.hip k_decode_ms) to out.lut
@@ -125,6 +131,8 @@ struct IndexlessSync;
 struct FileWs;
 }
 
+struct huff_wenc;
+
 struct huff_ctx {
     int device = 0;
     int cu_count = 256;
@@ -149,6 +157,9 @@ struct huff_ctx {
     // the .hff file path's pinned pieces and device buffers (filepath.cpp),
     // kept across calls: pinning ~0.5 GB per call costs more than the copies
     std::shared_ptr<huff::FileWs> file_ws;
+    // the task decoder of index-free wide-letter decodes (wide_rt.cpp), kept
+    // so repeated decodes reuse its buffers and uploaded tables
+    std::shared_ptr<huff_wenc> wdec_ws;
     uint64_t lut_tree_id = 0;
 
     // kernel timing

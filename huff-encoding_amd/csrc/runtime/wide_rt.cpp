@@ -355,7 +355,10 @@ Status wdecode_indexless_dev(huff_ctx* ctx, const huff_wtree* t, const uint8_t* 
     DevBuf& sub_abs = ctx->idx_sub_abs;
     HUFF_TRY(indexless_mark(ctx, st, sub_abs, 6));  // every kWideRun-th letter
     HIP_TRY(hipEventRecord(ctx->lut_free, ctx->stream));
-    huff_wenc e;
+    // one task decoder per context: its buffers only grow and its tables
+    // upload once per tree (a fresh one per call allocated and freed ~40 MB)
+    if (!ctx->wdec_ws) ctx->wdec_ws = std::make_shared<huff_wenc>();
+    huff_wenc& e = *ctx->wdec_ws;
     HUFF_TRY(e.init(ctx, t->t.width(), nullptr, st.total));
     HUFF_TRY(e.decode(t, d_comp, comp_bytes, d_out, static_cast<const uint64_t*>(sub_abs.p)));
     return ctx->sync();

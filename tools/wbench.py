@@ -96,14 +96,19 @@ def main():
     if args.indexless:
         pad = (8 - bits % 8) % 8
         ctx.reset_timing()
-        torch.cuda.synchronize()
-        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        ev0.record()
-        cnt = W.decompress_dev(ctx, t, out.data_ptr(), comp, pad, dec.data_ptr(), n)
-        ev1.record()
-        torch.cuda.synchronize()
-        assert cnt == n and torch.equal(dec, x)
-        res["indexless_decode_ms"] = round(ev0.elapsed_time(ev1), 3)
+        times = []
+        for _ in range(3):  # the first call builds the shape's tables and workspaces
+            dec.zero_()
+            torch.cuda.synchronize()
+            ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            ev0.record()
+            cnt = W.decompress_dev(ctx, t, out.data_ptr(), comp, pad, dec.data_ptr(), n)
+            ev1.record()
+            torch.cuda.synchronize()
+            assert cnt == n and torch.equal(dec, x)
+            times.append(ev0.elapsed_time(ev1))
+        res["indexless_decode_ms_cold"] = round(times[0], 3)
+        res["indexless_decode_ms"] = round(min(times[1:]), 3)
     print(json.dumps(res), flush=True)
 
 
