@@ -271,6 +271,38 @@ def test_dev_decompress_foreign_streams(H, O, ctx):
             assert out[:got].cpu().numpy().tobytes() == want
 
 
+@pytest.mark.parametrize("l2", [True, False], ids=["l2-lds", "l2-global"])
+def test_dev_decompress_codes_past_table(H, O, ctx, l2, monkeypatch):
+    """index-free decode of streams whose codes pass the 12-bit table (13-30
+    bits): the sync kernels' level-2 length table in LDS, and with
+    HUFF_NO_L2=1 the global secondary tables; both byte-exact vs the oracle"""
+    import torch
+    from huff_coding import device as D
+
+    if not l2:
+        monkeypatch.setenv("HUFF_NO_L2", "1")
+    rng = np.random.default_rng(29)
+    cases = [np.minimum(rng.geometric(p, n), 255).astype(np.uint8).tobytes()
+             for p, n in ((0.08, 2_000_000), (0.2, 700_001), (0.35, 65536 * 5 + 3))]
+    # 24 letters with Fibonacci-like counts: codes up to 23 bits
+    fib = [1, 1]
+    while len(fib) < 24:
+        fib.append(fib[-1] + fib[-2])
+    letters = np.repeat(np.arange(24, dtype=np.uint8), np.array(fib) * 3)
+    cases.append(rng.permutation(letters).tobytes())
+    for data in cases:
+        t = O.Tree.from_weights(O.weights_from_bytes(data))
+        comp, pad = O.compress_with_tree(data, t)
+        want = O.decompress(comp, pad, t)
+        tree = H.HuffTree.try_from_bin(t.as_bin())
+        dc = torch.zeros(len(comp) + 64, dtype=torch.uint8, device="cuda")
+        dc[: len(comp)] = torch.frombuffer(bytearray(comp), dtype=torch.uint8).cuda()
+        out = torch.empty(len(want) + 64, dtype=torch.uint8, device="cuda")
+        got = D.decompress_dev(ctx, tree, dc.data_ptr(), len(comp), pad, out.data_ptr(), len(want))
+        torch.cuda.synchronize()
+        assert got == len(want) and out[:got].cpu().numpy().tobytes() == want
+
+
 def _device_gen(H, ctx, kind, seed, n):
     import torch
     from huff_coding import device as D
