@@ -270,6 +270,8 @@ struct WideDecArgs {
     const uint64_t* chunk_start;  // per wide chunk
     const uint32_t* sub_bit;      // per run of kWideRun letters
     const uint64_t* sub_abs;      // non-null: index-free restart points, per run of kWideRun letters
+    uint32_t skip_packed;         // wdecode.hip: sub_abs entries as k_mark_lite writes them (a boundary at
+                                  // or before the run in bits [0, 48), the codes to skip from it above)
     uint64_t end_bit;             // the stream's last bit + 1 (wdecode.hip: the last task's end)
     uint32_t nchunks;
     uint32_t cu_count;

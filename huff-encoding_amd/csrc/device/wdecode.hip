@@ -83,6 +83,16 @@ __device__ __forceinline__ void leaf_letter(const uint8_t* letters, uint32_t lea
 // 64-bit buf, valid-bit count in the low 6 bits of X (the rest don't-care),
 // refilled unconditionally (decode_wave.hip FX_REFILL): every two codes when
 // codes have <= 16 bits, before every code otherwise (R1).
+// the window shifted left by len (1..32 bits, the entries' code lengths) as
+// two 32-bit halves: no 64-bit shift by a VGPR amount, which the gfx950 shift
+// hazard makes depend on the register allocation
+__device__ __forceinline__ uint64_t shl_window(uint64_t buf, uint32_t len) {
+    const uint32_t hi = static_cast<uint32_t>(buf >> 32), lo = static_cast<uint32_t>(buf);
+    const uint32_t nhi = __builtin_amdgcn_alignbit(hi, lo, 32u - len);
+    const uint32_t nlo = len >= 32 ? 0u : lo << len;
+    return (static_cast<uint64_t>(nhi) << 32) | nlo;
+}
+
 template <uint32_t W>
 struct Lane {
     uint64_t buf;
@@ -117,7 +127,10 @@ __device__ __forceinline__ void decode_part(Lane<W>& s, const Words& src, uint32
             e = ptr ? e2 : e;
         }
         const uint32_t len = static_cast<uint32_t>(e) & 63u;
-        s.buf <<= len;
+        // (8- and 16-byte letters: the split shift keeps the build clear of
+        // the shift hazard since the skip loop was added; others unchanged)
+        if constexpr (W >= 8) s.buf = shl_window(s.buf, len);
+        else s.buf <<= len;
         s.X -= len;
         const uint32_t v = payload<W>(e);
         if constexpr (W == 1) {
@@ -147,6 +160,29 @@ __device__ __forceinline__ void lane_init(Lane<W>& s, const Words& src, uint32_t
     s.nextw = src(s.rp);
 }
 
+// n codes consumed without their letters (index-free marks: the codes between
+// the boundary k_mark_lite names and the run's first letter); a refill before
+// every code, so any length <= 32 fits
+template <uint32_t W, bool TWO, class Words>
+__device__ __forceinline__ void lane_skip(Lane<W>& s, const Words& src, const EntryT<W>* __restrict__ tab, uint32_t K1,
+                                          uint32_t n) {
+    for (uint32_t j = 0; j < n; ++j) {
+        s.buf |= (static_cast<uint64_t>(s.nextw) << 32) >> (s.X & 63);
+        s.rp += (s.X & 32) ? 0u : 1u;
+        s.X |= 32;
+        s.nextw = src(s.rp);
+        const uint32_t top = static_cast<uint32_t>(s.buf >> 32);
+        EntryT<W> e = tab[top >> (32 - K1)];
+        if constexpr (TWO) {
+            const uint32_t lo = static_cast<uint32_t>(e);
+            if (lo & kSlowFlag) e = tab[(lo >> 8) + ((top << K1) >> (32 - (lo & 63u)))];
+        }
+        const uint32_t len = static_cast<uint32_t>(e) & 63u;
+        s.buf = shl_window(s.buf, len);
+        s.X -= len;
+    }
+}
+
 // letters per part: 64 bytes of output (16 registers; 128-byte parts held
 // 135 registers for 2-byte letters)
 template <uint32_t W>
@@ -165,12 +201,13 @@ __device__ __forceinline__ uint32_t row_piece(uint32_t r, uint32_t q) { return r
 template <uint32_t W, bool TWO, bool R1, class Words>
 __device__ __forceinline__ void lane_full(const Words& src, uint32_t rel, uint8_t* dst, const EntryT<W>* tab,
                                           uint32_t K1, const uint8_t* letters, bool aligned, uint8_t* rows,
-                                          uint8_t* task_out, uint32_t lane) {
+                                          uint8_t* task_out, uint32_t lane, uint32_t skip) {
     constexpr uint32_t PL = part_letters<W>();
     constexpr uint32_t ND = PL * W / 4;
     static_assert(ND == 16, "64-B parts");
     Lane<W> s;
     lane_init<W>(s, src, rel);
+    lane_skip<W, TWO>(s, src, tab, K1, skip);
     for (uint32_t p = 0; p < kWideRun / PL; ++p) {
         uint32_t o[ND];
         decode_part<W, PL, TWO, R1>(s, src, o, tab, K1, letters);
@@ -206,9 +243,10 @@ __device__ __forceinline__ void lane_full(const Words& src, uint32_t rel, uint8_
 // the stream's last lane (fewer than 64 letters): one letter at a time
 template <uint32_t W, bool TWO, bool R1, class Words>
 __device__ __forceinline__ void lane_tail(const Words& src, uint32_t rel, uint32_t cnt, uint8_t* dst,
-                                          const EntryT<W>* tab, uint32_t K1, const uint8_t* letters) {
+                                          const EntryT<W>* tab, uint32_t K1, const uint8_t* letters, uint32_t skip) {
     Lane<W> s;
     lane_init<W>(s, src, rel);
+    lane_skip<W, TWO>(s, src, tab, K1, skip);
     for (uint32_t j = 0; j < cnt; j += 2) {
         uint32_t o[2 * W / 4 > 0 ? 2 * W / 4 : 1];
         decode_part<W, 2, TWO, R1>(s, src, o, tab, K1, letters);
@@ -250,14 +288,21 @@ __global__ __launch_bounds__(max_waves<W>() * 64) void k_wdec_task(WideDecArgs a
         const uint64_t run = task * 64 + lane;
         const uint64_t l0 = run * kWideRun;
         const uint32_t cnt = l0 >= a.n ? 0u : static_cast<uint32_t>(a.n - l0 < kWideRun ? a.n - l0 : kWideRun);
-        const uint64_t lane_bit = !cnt ? 0 : (a.sub_abs ? a.sub_abs[run] : a.chunk_start[run >> 8] + a.sub_bit[run]);
+        uint64_t lane_bit = !cnt ? 0 : (a.sub_abs ? a.sub_abs[run] : a.chunk_start[run >> 8] + a.sub_bit[run]);
+        uint32_t skip = 0;
+        if (a.skip_packed) {
+            skip = static_cast<uint32_t>(lane_bit >> 48);
+            lane_bit &= kSkipPosMask;
+        }
         // the task's range: lane 0's start to the next task's start
         const uint32_t f_lo = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(lane_bit)));
         const uint32_t f_hi = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(lane_bit >> 32)));
         const uint64_t first = (static_cast<uint64_t>(f_hi) << 32) | f_lo;
         const uint64_t nrun = (task + 1) * 64;
-        const uint64_t end = nrun < nruns ? (a.sub_abs ? a.sub_abs[nrun] : a.chunk_start[nrun >> 8] + a.sub_bit[nrun])
-                                          : a.end_bit;
+        uint64_t end = nrun < nruns ? (a.sub_abs ? a.sub_abs[nrun] : a.chunk_start[nrun >> 8] + a.sub_bit[nrun])
+                                    : a.end_bit;
+        if (a.skip_packed && nrun < nruns)  // the next task's first letter lies within its skipped codes
+            end = (end & kSkipPosMask) + (end >> 48) * a.max_len;
         const uint64_t b0 = (first >> 3) & ~15ull;
         const uint64_t b1 = ((((end + 7) >> 3) + 32) + 15) & ~15ull;  // + the window's lookahead
         const uint32_t np = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(
@@ -283,17 +328,17 @@ __global__ __launch_bounds__(max_waves<W>() * 64) void k_wdec_task(WideDecArgs a
             const StageWords src{stage};
             const uint32_t rel = static_cast<uint32_t>(lane_bit - b0 * 8);
             if (cnt == kWideRun)
-                lane_full<W, TWO, R1>(src, rel, dst, tab, K1, letters, aligned, trows, task_out, lane);
+                lane_full<W, TWO, R1>(src, rel, dst, tab, K1, letters, aligned, trows, task_out, lane, skip);
             else if (cnt)
-                lane_tail<W, TWO, R1>(src, rel, cnt, dst, tab, K1, letters);
+                lane_tail<W, TWO, R1>(src, rel, cnt, dst, tab, K1, letters, skip);
             wave_sync();  // the stage is reused by the next task
         } else {  // longer than the stage: straight from global memory
             const GlobalWords src{a.comp, a.comp_bytes, (lane_bit >> 5)};
             const uint32_t grel = static_cast<uint32_t>(lane_bit & 31);
             if (cnt == kWideRun)
-                lane_full<W, TWO, R1>(src, grel, dst, tab, K1, letters, aligned, trows, task_out, lane);
+                lane_full<W, TWO, R1>(src, grel, dst, tab, K1, letters, aligned, trows, task_out, lane, skip);
             else if (cnt)
-                lane_tail<W, TWO, R1>(src, grel, cnt, dst, tab, K1, letters);
+                lane_tail<W, TWO, R1>(src, grel, cnt, dst, tab, K1, letters, skip);
         }
     }
 }

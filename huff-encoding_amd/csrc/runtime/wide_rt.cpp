@@ -149,7 +149,7 @@ Status huff_wenc::upload_dec(const huff_wtree* t) {
 }
 
 Status huff_wenc::decode(const huff_wtree* t, const uint8_t* d_comp, uint64_t comp_bytes, uint8_t* d_out,
-                         const uint64_t* sub_abs) {
+                         const uint64_t* sub_abs, bool skip_packed) {
     HUFF_TRY(ctx->activate());
     if (reinterpret_cast<uintptr_t>(d_comp) & 3) return Status::err(HUFF_E_INVALID_ARG, "stream must be 4-byte aligned");
     HUFF_TRY(upload_dec(t));
@@ -168,6 +168,7 @@ Status huff_wenc::decode(const huff_wtree* t, const uint8_t* d_comp, uint64_t co
     a.chunk_start = static_cast<const uint64_t*>(chunk_start.p);
     a.sub_bit = static_cast<const uint32_t*>(sub_bit.p);
     a.sub_abs = sub_abs;
+    a.skip_packed = skip_packed ? 1u : 0u;
     a.nchunks = nchunks;
     a.cu_count = static_cast<uint32_t>(ctx->cu_count);
     a.n = n;
@@ -184,6 +185,7 @@ Status huff_wenc::decode(const huff_wtree* t, const uint8_t* d_comp, uint64_t co
         a.stage_bytes = (sb + 15) & ~15u;
         return ctx->timed("wdecode", [&] { return huff::dev::launch_wide_decode_task(a, s); });
     }
+    if (skip_packed) return Status::err(HUFF_E_INVALID_ARG, "skip marks need the task decoder (codes <= 32 bits)");
     return ctx->timed("wdecode", [&] { return huff::dev::launch_wide_decode(a, s); });
 }
 
@@ -353,14 +355,27 @@ Status wdecode_indexless_dev(huff_ctx* ctx, const huff_wtree* t, const uint8_t* 
     if (!dev::indexless_staged(st.a))
         return Status::err(HUFF_E_CODE_TOO_LONG, "index-free decode of letters wider than a byte needs codes <= 32 bits");
     DevBuf& sub_abs = ctx->idx_sub_abs;
-    HUFF_TRY(indexless_mark(ctx, st, sub_abs, 6));  // every kWideRun-th letter
+    // every kWideRun-th letter: the task decoder (the tree's two-level table)
+    // takes k_mark_lite's marks (a boundary and the codes to skip from it, as
+    // the byte path's skip build); HUFF_WIDE_MARK_WALK=1 or the long-code
+    // decoder: exact points walked by k_mark_lds
+    const WideDecTables* wdt = nullptr;
+    HUFF_TRY(t->dec_tables(&wdt));
+    const bool skip = !wdt->stab.empty() && !std::getenv("HUFF_WIDE_MARK_WALK");
+    if (skip) {
+        HUFF_TRY(sub_abs.ensure(((st.total + 63) >> 6) * 8 + 8));
+        HIP_TRY(dev::launch_indexless_mark_lite(st.a, static_cast<const uint64_t*>(st.off.p),
+                                                static_cast<uint64_t*>(sub_abs.p), ctx->stream));
+    } else {
+        HUFF_TRY(indexless_mark(ctx, st, sub_abs, 6));
+    }
     HIP_TRY(hipEventRecord(ctx->lut_free, ctx->stream));
     // one task decoder per context: its buffers only grow and its tables
     // upload once per tree (a fresh one per call allocated and freed ~40 MB)
     if (!ctx->wdec_ws) ctx->wdec_ws = std::make_shared<huff_wenc>();
     huff_wenc& e = *ctx->wdec_ws;
     HUFF_TRY(e.init(ctx, t->t.width(), nullptr, st.total));
-    HUFF_TRY(e.decode(t, d_comp, comp_bytes, d_out, static_cast<const uint64_t*>(sub_abs.p)));
+    HUFF_TRY(e.decode(t, d_comp, comp_bytes, d_out, static_cast<const uint64_t*>(sub_abs.p), skip));
     return ctx->sync();
 }
 

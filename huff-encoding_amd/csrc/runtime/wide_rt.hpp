@@ -55,7 +55,7 @@ struct huff_wenc {
     huff::Status bits(const huff_wtree* t, uint64_t* total, huff::u128* missing);
     huff::Status pack(const huff_wtree* t, uint8_t* d_out, size_t out_cap, uint64_t* total);
     huff::Status decode(const huff_wtree* t, const uint8_t* d_comp, uint64_t comp_bytes, uint8_t* d_out,
-                        const uint64_t* sub_abs = nullptr);
+                        const uint64_t* sub_abs = nullptr, bool skip_packed = false);
     huff::Status upload_dec(const huff_wtree* t);
     huff::Status download_index(huff_index_host& idx);
     huff::Status upload_index(const huff_index_host& idx);

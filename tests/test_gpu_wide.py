@@ -61,10 +61,15 @@ def test_compress_with_tree_matches_oracle(W, O, ctx, dtype):
         assert back.dtype == np.dtype(dtype) and np.array_equal(back, letters), (dtype, n)
 
 
+@pytest.mark.parametrize("marks", ["skip", "walk"])
 @pytest.mark.parametrize("dtype", [np.int16, np.uint32, np.int64])
-def test_index_free_decode(W, O, ctx, dtype):
+def test_index_free_decode(W, O, ctx, dtype, marks, monkeypatch):
     """a container from to_bytes has no restart index: the self-synchronising
-    decoder (run on the tree's shape) + the wide decoder from its restart points"""
+    decoder (run on the tree's shape) + the wide decoder from its restart
+    points (k_mark_lite's boundary + codes to skip, or k_mark_lds's walked
+    exact points with HUFF_WIDE_MARK_WALK=1)"""
+    if marks == "walk":
+        monkeypatch.setenv("HUFF_WIDE_MARK_WALK", "1")
     rng = np.random.default_rng(11)
     for n in (1, 300, 65536 + 77, 250_001):
         letters = zipf_letters(rng, n, dtype)
