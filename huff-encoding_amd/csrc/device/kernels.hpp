@@ -267,6 +267,7 @@ struct WideDecArgs {
     const uint8_t* letters;       // [leaves * width]
     uint32_t nleaves;
     uint32_t width;
+    uint32_t w4_leaf;             // W = 4: the table names leaves (letters >= 2^24), else letters
     const uint64_t* chunk_start;  // per wide chunk
     const uint32_t* sub_bit;      // per run of kWideRun letters
     const uint64_t* sub_abs;      // non-null: index-free restart points, per run of kWideRun letters

@@ -40,14 +40,15 @@ struct U128 {
     uint64_t lo, hi;
 };
 
-// entry type by letter width: the letter (<= 4 bytes) or the leaf (wider)
+// u32 entries: the letter (<= 2 bytes; 4 bytes below 2^24) or the leaf
+// (wider, and 4-byte alphabets with larger letters: WideDecArgs::w4_leaf)
 template <uint32_t W>
-using EntryT = std::conditional_t<W == 4, uint64_t, uint32_t>;
+using EntryT = uint32_t;
 template <uint32_t W>
-__device__ __forceinline__ uint32_t payload(EntryT<W> e) {
-    if constexpr (W == 4) return static_cast<uint32_t>(e >> 32);
-    else return static_cast<uint32_t>(e >> 8);
-}
+__device__ __forceinline__ uint32_t payload(EntryT<W> e) { return e >> 8; }
+// letters in LDS beside the table: wide letters, and 4-byte leaves
+template <uint32_t W>
+__host__ __device__ __forceinline__ bool leaf_letters(const WideDecArgs& a) { return W >= 8 || (W == 4 && a.w4_leaf); }
 
 // dword sources (stream order, most significant byte first)
 struct StageWords {
@@ -106,7 +107,7 @@ struct Lane {
 template <uint32_t W, uint32_t PL, bool TWO, bool R1, class Words>
 __device__ __forceinline__ void decode_part(Lane<W>& s, const Words& src, uint32_t (&o)[PL * W / 4 > 0 ? PL * W / 4 : 1],
                                             const EntryT<W>* __restrict__ tab, uint32_t K1,
-                                            const uint8_t* __restrict__ letters) {
+                                            const uint8_t* __restrict__ letters, bool leaf4) {
     auto refill = [&]() {
         s.buf |= (static_cast<uint64_t>(s.nextw) << 32) >> (s.X & 63);
         s.rp += (s.X & 32) ? 0u : 1u;
@@ -140,7 +141,7 @@ __device__ __forceinline__ void decode_part(Lane<W>& s, const Words& src, uint32
             if ((i & 1) == 0) o[i >> 1] = v;
             else o[i >> 1] |= v << 16;
         } else if constexpr (W == 4) {
-            o[i] = v;
+            o[i] = leaf4 ? reinterpret_cast<const uint32_t*>(letters)[v] : v;
         } else {
             uint32_t d[W / 4];
             leaf_letter<W>(letters, v, d);
@@ -201,7 +202,7 @@ __device__ __forceinline__ uint32_t row_piece(uint32_t r, uint32_t q) { return r
 template <uint32_t W, bool TWO, bool R1, class Words>
 __device__ __forceinline__ void lane_full(const Words& src, uint32_t rel, uint8_t* dst, const EntryT<W>* tab,
                                           uint32_t K1, const uint8_t* letters, bool aligned, uint8_t* rows,
-                                          uint8_t* task_out, uint32_t lane, uint32_t skip) {
+                                          uint8_t* task_out, uint32_t lane, uint32_t skip, bool leaf4) {
     constexpr uint32_t PL = part_letters<W>();
     constexpr uint32_t ND = PL * W / 4;
     static_assert(ND == 16, "64-B parts");
@@ -210,7 +211,7 @@ __device__ __forceinline__ void lane_full(const Words& src, uint32_t rel, uint8_
     lane_skip<W, TWO>(s, src, tab, K1, skip);
     for (uint32_t p = 0; p < kWideRun / PL; ++p) {
         uint32_t o[ND];
-        decode_part<W, PL, TWO, R1>(s, src, o, tab, K1, letters);
+        decode_part<W, PL, TWO, R1>(s, src, o, tab, K1, letters, leaf4);
         if (rows) {
             wave_order();  // the previous part's row reads were issued first
 #pragma unroll
@@ -243,13 +244,14 @@ __device__ __forceinline__ void lane_full(const Words& src, uint32_t rel, uint8_
 // the stream's last lane (fewer than 64 letters): one letter at a time
 template <uint32_t W, bool TWO, bool R1, class Words>
 __device__ __forceinline__ void lane_tail(const Words& src, uint32_t rel, uint32_t cnt, uint8_t* dst,
-                                          const EntryT<W>* tab, uint32_t K1, const uint8_t* letters, uint32_t skip) {
+                                          const EntryT<W>* tab, uint32_t K1, const uint8_t* letters, uint32_t skip,
+                                          bool leaf4) {
     Lane<W> s;
     lane_init<W>(s, src, rel);
     lane_skip<W, TWO>(s, src, tab, K1, skip);
     for (uint32_t j = 0; j < cnt; j += 2) {
         uint32_t o[2 * W / 4 > 0 ? 2 * W / 4 : 1];
-        decode_part<W, 2, TWO, R1>(s, src, o, tab, K1, letters);
+        decode_part<W, 2, TWO, R1>(s, src, o, tab, K1, letters, leaf4);
         // bytes [0, 2 W) of o: the pair's letters (the second one past cnt is dropped)
 #pragma unroll
         for (uint32_t b = 0; b < 2 * W; ++b)
@@ -264,7 +266,7 @@ __global__ __launch_bounds__(max_waves<W>() * 64) void k_wdec_task(WideDecArgs a
     const uint32_t t = threadIdx.x, lane = t & 63, wave = wave_index();
     // LDS: [the table][leaf letters (W >= 8)] when LDS, then the waves' stages
     const uint32_t tab_bytes = LDS ? a.stab_bytes : 0u;
-    const uint32_t let_bytes = LDS && W >= 8 ? (a.nleaves * W + 15) & ~15u : 0u;
+    const uint32_t let_bytes = LDS && leaf_letters<W>(a) ? (a.nleaves * W + 15) & ~15u : 0u;
     if constexpr (LDS) {
         for (uint32_t i = t; i < tab_bytes / 16; i += blockDim.x)
             reinterpret_cast<uint4*>(lds)[i] = reinterpret_cast<const uint4*>(a.stab)[i];
@@ -274,7 +276,8 @@ __global__ __launch_bounds__(max_waves<W>() * 64) void k_wdec_task(WideDecArgs a
     __syncthreads();
     // one pointer origin per instantiation (ds_read or global_load, never flat)
     const EntryT<W>* tab = LDS ? reinterpret_cast<const EntryT<W>*>(lds) : static_cast<const EntryT<W>*>(a.stab);
-    const uint8_t* letters = LDS && W >= 8 ? lds + tab_bytes : a.letters;
+    const uint8_t* letters = LDS && leaf_letters<W>(a) ? lds + tab_bytes : a.letters;
+    const bool leaf4 = W == 4 && a.w4_leaf;
     uint8_t* wave_lds = lds + tab_bytes + let_bytes + wave * (a.stage_bytes + kRowBytes);
     uint32_t* stage = reinterpret_cast<uint32_t*>(wave_lds);
     uint8_t* rows = wave_lds + a.stage_bytes;
@@ -328,17 +331,17 @@ __global__ __launch_bounds__(max_waves<W>() * 64) void k_wdec_task(WideDecArgs a
             const StageWords src{stage};
             const uint32_t rel = static_cast<uint32_t>(lane_bit - b0 * 8);
             if (cnt == kWideRun)
-                lane_full<W, TWO, R1>(src, rel, dst, tab, K1, letters, aligned, trows, task_out, lane, skip);
+                lane_full<W, TWO, R1>(src, rel, dst, tab, K1, letters, aligned, trows, task_out, lane, skip, leaf4);
             else if (cnt)
-                lane_tail<W, TWO, R1>(src, rel, cnt, dst, tab, K1, letters, skip);
+                lane_tail<W, TWO, R1>(src, rel, cnt, dst, tab, K1, letters, skip, leaf4);
             wave_sync();  // the stage is reused by the next task
         } else {  // longer than the stage: straight from global memory
             const GlobalWords src{a.comp, a.comp_bytes, (lane_bit >> 5)};
             const uint32_t grel = static_cast<uint32_t>(lane_bit & 31);
             if (cnt == kWideRun)
-                lane_full<W, TWO, R1>(src, grel, dst, tab, K1, letters, aligned, trows, task_out, lane, skip);
+                lane_full<W, TWO, R1>(src, grel, dst, tab, K1, letters, aligned, trows, task_out, lane, skip, leaf4);
             else if (cnt)
-                lane_tail<W, TWO, R1>(src, grel, cnt, dst, tab, K1, letters, skip);
+                lane_tail<W, TWO, R1>(src, grel, cnt, dst, tab, K1, letters, skip, leaf4);
         }
     }
 }
@@ -373,7 +376,7 @@ template <uint32_t W>
 hipError_t by_place(const WideDecArgs& a, hipStream_t s) {
     constexpr size_t kLds = 160 * 1024;
     const size_t tab = a.stab_bytes;
-    const size_t let = W >= 8 ? (static_cast<size_t>(a.nleaves) * W + 15) & ~size_t(15) : 0;
+    const size_t let = leaf_letters<W>(a) ? (static_cast<size_t>(a.nleaves) * W + 15) & ~size_t(15) : 0;
     const size_t per_wave = a.stage_bytes + kRowBytes;
     if (tab + let <= 96 * 1024 && tab + let + 4 * per_wave <= kLds) {
         size_t waves = (kLds - tab - let) / per_wave;

@@ -118,12 +118,14 @@ struct WideDecTables {
     std::vector<uint8_t> letters;  // leaves * W
     // the task decoder's two-level table (device/wdecode.hip): level 1 of
     // 2^sbits entries, the first code of each window: its length in bits
-    // [0, 6) and the letter (W <= 2: u32 entries, letter << 8; W = 4: u64,
-    // letter << 32) or the leaf index (W >= 8: u32, leaf << 8); or 0x80 | s
-    // with the offset of a level-2 table of 2^s entries (indexed by the next s
-    // bits, lengths counted from the window start) in bits 8..31. Padded to 16 B.
+    // [0, 6) and, in bits 8..31, the letter (W <= 2, and W = 4 when every
+    // letter is below 2^24) or the leaf index (W >= 8, and W = 4 otherwise:
+    // w4_leaf); or 0x80 | s with the offset of a level-2 table of 2^s entries
+    // (indexed by the next s bits, lengths counted from the window start) in
+    // bits 8..31. u32 entries, padded to 16 B.
     std::vector<uint8_t> stab;
     uint32_t sbits = 0;
+    bool w4_leaf = false;
 };
 
 // Slot layout: the key at offset 0 (keys of <= 4 bytes as u32, native

@@ -316,11 +316,17 @@ Status build_wide_enc_tables(const WideTree& t, WideEncTables& out) {
 // for codes > 32 bits or more than 4 Mi entries (the long-code decoder).
 static void build_wide_stab(const WideTree& t, uint32_t W, const std::vector<int64_t>& leaf_of, WideDecTables& out) {
     const auto& nodes = t.nodes();
-    const uint32_t eb = W == 4 ? 8 : 4;
+    const uint32_t eb = 4;
+    // 4-byte letters sit in the entry when they all fit its 24 bits, else the
+    // entry names the leaf (the u64 entries this replaces doubled the table,
+    // which for a 4,096-letter alphabet no longer fitted the LDS)
+    out.w4_leaf = false;
+    if (W == 4)
+        for (const auto& nd : nodes)
+            if (nd.is_leaf && static_cast<uint64_t>(static_cast<uint32_t>(nd.letter)) >= (1u << 24)) out.w4_leaf = true;
     std::vector<uint64_t> tab;
     auto leaf_entry = [&](int32_t x, uint32_t len, uint32_t leaf) -> uint64_t {
-        if (W <= 2) return (static_cast<uint64_t>(nodes[x].letter) << 8) | len;
-        if (W == 4) return (static_cast<uint64_t>(static_cast<uint32_t>(nodes[x].letter)) << 32) | len;
+        if (W <= 2 || (W == 4 && !out.w4_leaf)) return (static_cast<uint64_t>(static_cast<uint32_t>(nodes[x].letter)) << 8) | len;
         return (static_cast<uint64_t>(leaf) << 8) | len;
     };
     if (t.root_is_leaf()) {  // every bit decodes the root letter (comp.rs:506-509)
@@ -382,13 +388,8 @@ static void build_wide_stab(const WideTree& t, uint32_t W, const std::vector<int
     }
     out.stab.assign((tab.size() * eb + 15) / 16 * 16, 0);
     for (size_t i = 0; i < tab.size(); ++i) {
-        if (W == 4) {
-            // pointer entries keep the offset in bits 8..31 of the low half
-            std::memcpy(&out.stab[i * 8], &tab[i], 8);
-        } else {
-            const uint32_t v = static_cast<uint32_t>(tab[i]);
-            std::memcpy(&out.stab[i * 4], &v, 4);
-        }
+        const uint32_t v = static_cast<uint32_t>(tab[i]);
+        std::memcpy(&out.stab[i * 4], &v, 4);
     }
 }
 

@@ -163,6 +163,7 @@ Status huff_wenc::decode(const huff_wtree* t, const uint8_t* d_comp, uint64_t co
     a.stab_bytes = static_cast<uint32_t>(dt->stab.size());
     a.letters = static_cast<const uint8_t*>(letters.p);
     a.nleaves = static_cast<uint32_t>(dt->letters.size() / width);
+    a.w4_leaf = dt->w4_leaf ? 1u : 0u;
     a.max_len = dt->maxdepth;
     a.width = width;
     a.chunk_start = static_cast<const uint64_t*>(chunk_start.p);

@@ -85,6 +85,22 @@ def test_index_free_decode(W, O, ctx, dtype, marks, monkeypatch):
         assert np.array_equal(got, letters), (dtype, n)
 
 
+@pytest.mark.parametrize("top", [1 << 20, 1 << 31], ids=["letters-in-entries", "leaf-entries"])
+def test_u32_table_forms(W, O, ctx, top):
+    """4-byte letters: the task decoder's entries hold the letter when every
+    letter is below 2^24, else a leaf index into the letters in LDS; both
+    decode the indexed and the index-free container byte-exactly"""
+    rng = np.random.default_rng(top % 1000 + 3)
+    alphabet = np.unique(rng.integers(0, top, 3000, dtype=np.uint32))
+    p = 1.0 / np.arange(1, alphabet.size + 1) ** 1.1
+    letters = alphabet[rng.choice(alphabet.size, 400_003, p=p / p.sum())]
+    cd = W.compress(letters, ctx)
+    assert np.array_equal(W.decompress(cd, ctx), letters)
+    back_cd = W.WideCompressData.try_from_bytes(cd.to_bytes(), np.uint32)
+    assert not back_cd.has_index()
+    assert np.array_equal(W.decompress(back_cd, ctx), letters)
+
+
 def test_u128_letters(W, O, ctx):
     rng = np.random.default_rng(5)
     base = [(1 << 127) | (int(x) << 40) | 17 for x in rng.integers(0, 1 << 60, 500)] + [0, 1, (1 << 128) - 1]
