@@ -63,3 +63,20 @@ def test_host_cpp_tests():
     r = subprocess.run([os.path.join(pkg, "build", "test_host")], capture_output=True, text=True)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "ALL OK" in r.stdout
+
+
+def test_host_cpp_tests_under_sanitizers():
+    """the same host tests built with AddressSanitizer + UBSan (host code only:
+    GPU sanitizers are not available on the pool): no leak, overflow or UB
+    report, every check passing"""
+    import shutil
+    import subprocess
+
+    if shutil.which("g++") is None:
+        pytest.skip("no g++")
+    pkg = os.path.join(ROOT, "huff-encoding_amd")
+    subprocess.run(["make", "-s", "-C", pkg, "asan"], check=True)
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1:verify_asan_link_order=0", UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1")
+    r = subprocess.run([os.path.join(pkg, "build", "test_host_asan")], capture_output=True, text=True, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "ALL OK" in r.stdout and "runtime error" not in r.stderr
