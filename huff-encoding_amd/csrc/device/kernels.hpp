@@ -414,6 +414,13 @@ hipError_t launch_indexless_mark(const IndexlessArgs& a, const uint64_t* off, ui
                                  hipStream_t s);
 bool indexless_staged(const IndexlessArgs& a);  // k_spec/k_mark LDS variants apply
 hipError_t launch_bytemap(const BytemapArgs& a, hipStream_t s);
+// letter checksums of the decode check build (checksum.hip): per task of
+// kTaskSym letters, sum and position-weighted sum (u64 = s2 << 32 | s1);
+// the check counts differing tasks in err[0], the first one in err[1] (set
+// err[1] to ~0u before)
+hipError_t launch_task_sums(const uint8_t* x, uint64_t n, uint64_t* sums, hipStream_t s);
+hipError_t launch_task_sums_check(const uint8_t* x, uint64_t n, const uint64_t* sums, unsigned int* err,
+                                  hipStream_t s);
 hipError_t launch_find_first(const uint8_t* in, uint64_t n, const uint8_t* missing_mask, unsigned long long* pos,
                              hipStream_t s);
 hipError_t launch_generate(int kind, uint64_t seed, uint64_t offset, const uint64_t* cdf, uint8_t* out, uint64_t n,

@@ -496,7 +496,7 @@ huff::Status huff_enc::init(huff_ctx* c, const uint8_t* d, uint64_t nbytes) {
     d_in = d;
     n = nbytes;
     nchunks = static_cast<uint32_t>((n + huff::dev::kChunk - 1) / huff::dev::kChunk);
-    have_hist = packed = false;
+    have_hist = packed = sums_valid = false;
     const size_t nc = std::max<uint32_t>(nchunks, 1);
     HUFF_TRY(chunk_hist.ensure(nc * 256 * 4));
     HUFF_TRY(gw.ensure(huff::dev::kHistCopies * 256 * 8));
@@ -568,7 +568,7 @@ huff::Status huff_enc::hist_known(const uint64_t counts[256]) {
 huff::Status huff_enc::hist_row(long long* d_row) {
     HUFF_TRY(ctx->activate());
     hipStream_t s = ctx->stream;
-    have_hist = packed = false;
+    have_hist = packed = sums_valid = false;
     if (nchunks == 0) {
         HIP_TRY(hipMemsetAsync(d_row, 0, 258 * 8, s));
         return huff::Status::ok();
@@ -612,6 +612,24 @@ huff::Status huff_enc::bits(const huff_tree* t, uint64_t* total) {
     return huff::Status::ok();
 }
 
+// the check build's letter checksums of the decoded job (checksum.hip): a
+// wrong letter whose code has the right length keeps the stream in step, so
+// only this sees it
+huff::Status huff_enc::check_sums(const uint8_t* d_out) {
+    if (!sums_valid || !huff::decode_check_mode()) return huff::Status::ok();
+    HUFF_TRY(ctx->d_err.ensure(32));
+    unsigned int* err = static_cast<unsigned int*>(ctx->d_err.p);
+    const unsigned int init[2] = {0u, ~0u};
+    HIP_TRY(hipMemcpyAsync(err, init, 8, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(huff::dev::launch_task_sums_check(d_out, n, static_cast<const uint64_t*>(task_sums.p), err, ctx->stream));
+    unsigned int e[2] = {};
+    HIP_TRY(hipMemcpyAsync(e, err, 8, hipMemcpyDeviceToHost, ctx->stream));
+    HUFF_TRY(ctx->sync());
+    if (e[0] == 0) return huff::Status::ok();
+    return huff::Status::err(HUFF_E_CORRUPT, "decode self-check: letter checksums differ in " + std::to_string(e[0]) +
+                                                 " task(s) of 4096 letters; first: task " + std::to_string(e[1]));
+}
+
 huff::Status huff_enc::pack(const huff_tree* t, uint64_t base, const uint8_t* prev_tail, size_t prev_tail_len,
                             uint8_t* d_out, size_t out_cap, uint64_t* total) {
     uint64_t tb = 0;
@@ -623,6 +641,13 @@ huff::Status huff_enc::pack(const huff_tree* t, uint64_t base, const uint8_t* pr
     if (prev_tail_len > 8) return huff::Status::err(HUFF_E_INVALID_ARG, "prev_tail holds at most 8 bytes");
     HUFF_TRY(ctx->activate());
     hipStream_t s = ctx->stream;
+    // the check build records the input's letter checksums for decode (checksum.hip)
+    sums_valid = false;
+    if (huff::decode_check_mode() && n) {
+        HUFF_TRY(task_sums.ensure(((n + huff::dev::kTaskSym - 1) / huff::dev::kTaskSym) * 8));
+        HIP_TRY(huff::dev::launch_task_sums(d_in, n, static_cast<uint64_t*>(task_sums.p), s));
+        sums_valid = true;
+    }
     const huff::EncTables& et = t->enc_tables();
     const bool long_codes = et.maxlen > huff::dev::kShortMaxLen;
     if ((base & 7) == 0 && et.maxlen == 8 && !huff::fixed8_disabled()) {
@@ -776,7 +801,7 @@ huff::Status huff_enc::decode(const huff_tree* t, const uint8_t* d_comp, uint64_
         m.n = n;
         for (int b = 0; b < 256; ++b) m.map[b] = static_cast<uint8_t>(dt->lut[b]);  // entries (8 << 8) | letter
         HUFF_TRY(ctx->timed("decode", [&] { return huff::dev::launch_bytemap(m, ctx->stream); }));
-        return huff::Status::ok();
+        return check_sums(d_out);
     }
     HUFF_TRY(ensure_index());
     huff::dev::DecodeArgs a{};
@@ -834,6 +859,7 @@ huff::Status huff_enc::decode(const huff_tree* t, const uint8_t* d_comp, uint64_
     a.out = dst;
     if (a.check_mode) {
         HUFF_TRY(huff::run_checked_decode(ctx, a, [&] { return huff::dev::launch_decode(a, ctx->stream); }));
+        HUFF_TRY(check_sums(dst));
     } else {
         HUFF_TRY(ctx->timed("decode", [&] { return huff::dev::launch_decode(a, ctx->stream); }));
     }
@@ -860,6 +886,7 @@ huff::Status huff_enc::download_index(huff_index_host& idx) {
 huff::Status huff_enc::upload_index(const huff_index_host& idx) {
     if (idx.n != n || idx.chunk_start.size() != nchunks + 1u)
         return huff::Status::err(HUFF_E_INVALID_ARG, "restart index does not match the job");
+    sums_valid = false;  // no encode of this job's letters behind the index
     HUFF_TRY(ctx->activate());
     HIP_TRY(hipMemcpyAsync(chunk_start.p, idx.chunk_start.data(), idx.chunk_start.size() * 8, hipMemcpyHostToDevice,
                            ctx->stream));

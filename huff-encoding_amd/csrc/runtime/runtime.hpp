@@ -191,6 +191,11 @@ struct huff_enc {
     // expanded into sub_bit for the consumers that read that
     DevBuf task_base, sub16;
     bool compact_index = false;
+    // decode check build (HUFF_DEC_VARIANT=11): the input's letter checksums
+    // per decode task, recorded by pack (checksum.hip)
+    DevBuf task_sums;
+    bool sums_valid = false;
+    huff::Status check_sums(const uint8_t* d_out);
     huff::Status expand_index();
     uint64_t w[256] = {};
     bool have_hist = false;

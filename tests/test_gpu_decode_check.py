@@ -3,7 +3,9 @@
 The checked build runs the production decoder body with a per-lane check
 that every lane's letters end exactly at the next lane's restart entry
 (decode_wave.hip fx_check); a mismatch makes the runtime return
-HUFF_E_CORRUPT with the task and lane. Every decode is also compared
+HUFF_E_CORRUPT with the task and lane. A wrong letter whose code has the
+right length keeps every lane in step, so the check build also compares
+per-task letter checksums recorded at encode (checksum.hip). Every decode is also compared
 byte-for-byte with the input, and one test shows that the check fires on a
 damaged stream.
 
@@ -130,6 +132,35 @@ def test_check_fires_on_damaged_stream(H, ctx, monkeypatch):
     with pytest.raises(H.HuffError) as ei:
         job.decode(tree, out.data_ptr(), dec.data_ptr())
     assert ei.value.code == 19 and "self-check" in str(ei.value)
+
+
+def test_checksum_sees_wrong_letter_of_right_length(H, ctx, monkeypatch):
+    """16 letters of equal weight: every code has 4 bits, so one flipped bit
+    of the stream turns one letter into another and leaves every lane in
+    step (the end-bit check passes). The check build's letter checksums
+    (checksum.hip: per 4,096-letter task, sum and position-weighted sum of
+    the input, recorded by pack) see it and name the task."""
+    import torch
+
+    monkeypatch.setenv("HUFF_DEC_VARIANT", "11")
+    monkeypatch.setenv("HUFF_DISABLE_FIXED8", "1")
+    rng = np.random.default_rng(5)
+    # equal counts of letters 1..16: a full tree of depth 4 (letter 0 would
+    # add the reference's re-yielded byte-0 leaf, weights.rs:396-441)
+    n = (1 << 21) + 336
+    host = rng.permutation(np.tile(np.arange(1, 17, dtype=np.uint8), n // 16))
+    x = torch.from_numpy(np.concatenate([host, np.zeros(64, np.uint8)])).cuda()
+    job, tree, out, bits = _encode(H, x, n, ctx)
+    _, ln = tree.code_table()
+    assert set(ln[1:17].tolist()) == {4} and ln[17:].max() == 0
+    _decode_equal(job, tree, out, x, n)  # intact: both checks pass
+    byte = 3 * 2048 + 5  # letters 12,298-12,299: task 3
+    out[byte] ^= 0x10
+    dec = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
+    with pytest.raises(H.HuffError) as ei:
+        job.decode(tree, out.data_ptr(), dec.data_ptr())
+    assert ei.value.code == 19 and "letter checksums differ in 1 task" in str(ei.value)
+    assert "first: task 3" in str(ei.value)
 
 
 def test_decode_refuses_other_tree(H, ctx):
