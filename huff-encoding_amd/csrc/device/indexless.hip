@@ -268,35 +268,6 @@ __device__ Staged stage_block(const IndexlessArgs& a, uint32_t* w) {
     return Staged{w, byte_lo * 8, nullptr};
 }
 
-struct LaneBits {
-    const uint32_t* w;
-    uint64_t buf;
-    uint32_t nb, rp;
-    uint64_t pos;
-    __device__ __forceinline__ void init(const Staged& st, uint64_t p) {
-        w = st.w;
-        pos = p;
-        const uint64_t off = p - st.base;
-        rp = static_cast<uint32_t>(off >> 5);
-        const uint32_t sh = static_cast<uint32_t>(off & 31);
-        buf = (static_cast<uint64_t>(__builtin_bswap32(w[rp])) << 32) | __builtin_bswap32(w[rp + 1]);
-        buf <<= sh;
-        nb = 64 - sh;
-        rp += 2;
-    }
-    __device__ __forceinline__ void refill() {
-        if (nb < 32) {
-            buf |= static_cast<uint64_t>(__builtin_bswap32(w[rp++])) << (32 - nb);
-            nb += 32;
-        }
-    }
-    __device__ __forceinline__ void consume(uint32_t len) {
-        buf <<= len;
-        nb -= len;
-        pos += len;
-    }
-};
-
 // The staged kernels walk the stream one code per lookup in unrolled chunks
 // of 8 (u16 single-symbol table in LDS, as k_decode_fixed; no branch inside a
 // chunk), then settle where the walk should have stopped from the chunk's 8
