@@ -2,6 +2,9 @@
 //
 // Each entry point converts huff::Status into an int code plus the
 // thread-local last-error message; nothing throws across the ABI.
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <algorithm>
 #include <cstring>
 #include <exception>
@@ -415,11 +418,23 @@ int huff_enc_compress(huff_enc* e, uint8_t* d_out, size_t out_cap, huff_tree** t
     if (reinterpret_cast<uintptr_t>(d_out) & 15) return fail(HUFF_E_INVALID_ARG, "d_out must be 16-byte aligned");
     *tree_out = nullptr;
     return guarded([&]() -> huff::Status {
+        // HUFF_HOST_TRACE=1: host time of each phase (pass 1 + weights read-back,
+        // tree, pass 2 with its tables and launch), one stderr line per call
+        static const bool trace = std::getenv("HUFF_HOST_TRACE") != nullptr;
+        const auto t0 = std::chrono::steady_clock::now();
         HUFF_TRY(e->hist());
+        const auto t1 = std::chrono::steady_clock::now();
         auto t = std::make_unique<huff_tree>();
         HUFF_TRY(huff::HuffTree::from_weights(huff::ByteWeights::from_counts(e->w), t->t));
+        const auto t2 = std::chrono::steady_clock::now();
         uint64_t bits = 0;
         huff::Status st = e->pack(t.get(), 0, nullptr, 0, d_out, out_cap, &bits);
+        if (trace) {
+            const auto t3 = std::chrono::steady_clock::now();
+            auto us = [](auto a, auto b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
+            std::fprintf(stderr, "huff_enc_compress host us: hist %.1f tree %.1f pack %.1f\n", us(t0, t1), us(t1, t2),
+                         us(t2, t3));
+        }
         if (bits_out) *bits_out = bits;
         HUFF_TRY(st);
         *tree_out = t.release();
