@@ -246,6 +246,11 @@ def test_dev_decompress_foreign_streams(H, O, ctx):
         for hi in (1, 3, 40, 256):
             cases.append(rng.integers(0, hi, n, dtype=np.uint8).tobytes())
     cases.append(np.minimum(rng.geometric(0.2, 300_000), 255).astype(np.uint8).tobytes())
+    # equal counts of 8 / 64 letters: every code 3 / 6 bits, so the segment
+    # length (a multiple of the lengths' gcd near 992 bits) is clamped below
+    # the sample words' 1024-bit limit (indexless_sync)
+    for k in (8, 64):
+        cases.append(rng.permutation(np.tile(np.arange(1, k + 1, dtype=np.uint8), 400_000 // k)).tobytes())
     for data in cases:
         t = O.Tree.from_weights(O.weights_from_bytes(data))
         comp, pad = O.compress_with_tree(data, t)
