@@ -18,6 +18,11 @@ namespace {
 
 constexpr int kThreads = 256;
 constexpr int kCopies = 32;
+// log2 of the one-shot histogram's LDS copies (k_hist1): 32 copies (32 KiB,
+// conflict-free on any data, 5 workgroups per CU) by default
+#ifndef HUFF_HIST_LOGC
+#define HUFF_HIST_LOGC 5
+#endif
 
 
 template <int LOGC = 5>
@@ -349,7 +354,7 @@ hipError_t launch_hist(const uint8_t* base, uint64_t lo, uint64_t hi, uint32_t n
     if (chunk_hist) {  // per-chunk rows wanted: one-shot grid, then the row sum
         // 32 copies: 16 measured equal on uniform bytes and 20 % slower on
         // Zipf (same-address conflicts between lanes l and l + 16)
-        hipLaunchKernelGGL(k_hist1<5>, dim3(nchunks), dim3(kThreads), 0, s, base, lo, hi, chunk_hist, gw);
+        hipLaunchKernelGGL(k_hist1<HUFF_HIST_LOGC>, dim3(nchunks), dim3(kThreads), 0, s, base, lo, hi, chunk_hist, gw);
         const uint32_t g = nchunks < 512 ? nchunks : 512;
         hipLaunchKernelGGL(k_rows_sum, dim3(g), dim3(256), 0, s, chunk_hist, nchunks, gw);
         if (done.host) hipLaunchKernelGGL(k_hist_publish, dim3(1), dim3(256), 0, s, gw, done.host, done.tag);
