@@ -80,3 +80,54 @@ def test_random_trees_both_decoders(H, O, ctx, case):
     got = D.decompress_dev(ctx, tree, dc.data_ptr(), len(comp), pad, dec.data_ptr(), n + 64)
     torch.cuda.synchronize()
     assert got == n and torch.equal(dec[:n], x[:n]), (case, kind, got, n)
+
+
+WIDE_DTYPES = [np.int16, np.uint16, np.int32, np.uint32, np.int64, np.uint64]
+
+
+@pytest.mark.parametrize("case", range(48))
+def test_random_wide_alphabets(O, ctx, case):
+    """wide letters: a random dtype, alphabet (1 ... 6,000 letters, small or
+    full-range values), law (Zipf, equal, Fibonacci depths) and length;
+    compress_with_tree byte-equal to the oracle's stream, and both the indexed
+    container and its to_bytes form (no index: the sync kernels on the tree's
+    shape + skip marks) decode to the input"""
+    import huff_coding.wide as W
+
+    rng = np.random.default_rng(5000 + case)
+    dtype = WIDE_DTYPES[case % len(WIDE_DTYPES)]
+    info = np.iinfo(dtype)
+    k = int(rng.integers(1, 6000))
+    if rng.random() < 0.5:
+        alphabet = np.unique(rng.integers(info.min, info.max, k, dtype=dtype, endpoint=True))
+    else:  # small values (4-byte letters then sit in the decoder's table entries)
+        alphabet = np.unique(rng.integers(0, min(int(info.max), 1 << 20), k).astype(dtype))
+    k = alphabet.size
+    law = rng.integers(0, 3)
+    if law == 0:
+        p = 1.0 / np.arange(1, k + 1) ** rng.uniform(0.7, 1.5)
+    elif law == 1:
+        p = np.ones(k)
+    else:
+        m = min(k, 28)
+        f = [1.0, 1.0]
+        while len(f) < m:
+            f.append(f[-1] + f[-2])
+        p = np.zeros(k)
+        p[:m] = f[:m]
+    n = int(rng.choice([1, 3, 64, 4097, 65537, 250_001]))
+    letters = alphabet[rng.choice(k, n, p=p / p.sum())]
+    wmap = W.build_weights_map(letters, ctx)
+    items = list(wmap.items())
+    rng.shuffle(items)  # any HashMap iteration order
+    t = W.WideTree.from_weights(items, dtype)
+    cd = W.compress_with_tree(letters, t, ctx)
+    lbits = 8 * np.dtype(dtype).itemsize
+    mask = (1 << lbits) - 1
+    ot = O.Tree.from_leaves([int(a) & mask for a, _ in items], [int(v) for _, v in items])
+    u = letters.astype(np.int64).view(np.uint64) & np.uint64(mask) if lbits < 64 else letters.view(np.uint64)
+    ocomp, opad = O.wcompress_with_tree(u, ot)
+    assert cd.comp_bytes() == ocomp and cd.padding_bits() == opad, (case, dtype, k, n)
+    assert np.array_equal(W.decompress(cd, ctx), letters), (case, dtype, k, n)
+    back = W.WideCompressData.try_from_bytes(cd.to_bytes(), dtype)
+    assert np.array_equal(W.decompress(back, ctx), letters), (case, dtype, k, n)
