@@ -127,6 +127,27 @@ PHASE_KERNELS = {  # bench phase -> device kernels (names as in tools/summarize_
 }
 
 
+# the index-free decode pipeline of the general path: its
+# kernels' HBM bytes per launch from profiles/traffic_<kind>_indexfree.json
+# (tools/make_traffic.py over a kbench --phase indexless PMC run)
+INDEXFREE_KERNELS = ["k_spec_lds", "k_fix_list", "k_scan_tiles", "k_scan_tsum", "k_scan_fix", "k_mark_lite",
+                     "k_decode_fixed_skip"]
+
+
+def indexfree_traffic(kind, fixed8):
+    """HBM bytes of one index-free decode of the 1 GiB job: the byte map's
+    for all-8-bit codes, else the sum over the pipeline's kernels"""
+    if fixed8:
+        return dominant_traffic(kind, "decode", True, None)
+    path = os.path.join(ROOT, "profiles", f"traffic_{kind}_indexfree.json")
+    if not os.path.exists(path):
+        return None, None
+    t = json.load(open(path))
+    if not all(k in t for k in INDEXFREE_KERNELS):
+        return None, None
+    return int(sum(t[k]["hbm_bytes"] for k in INDEXFREE_KERNELS)), os.path.relpath(path, ROOT)
+
+
 def dominant_traffic(kind, phase, fixed8, dec_kernel):
     """HBM bytes per launch of the dominant phase from the committed PMC
     summary of this workload (profiles/traffic_<kind>.json, written by
@@ -348,6 +369,15 @@ def run_workload(s: Setup, kind: str, n: int, with_cpu: bool):
     if s.ceil is None:  # measured HBM ceilings of this GPU, same run (huff_dev_calibrate)
         s.ceil = D.calibrate(ctx, x.data_ptr(), dec.data_ptr(), n & ~15, 5)
     read_ceil, copy_ceil = s.ceil
+    # the index-free decode against the roofline: C + N algorithmic bytes over
+    # its wall time per call (the host read of the letter count included), and
+    # the pipeline's PMC bytes when a summary exists for this workload at 1 GiB
+    idx_ach = (comp_bytes + n) / (t_idx / args.steps) / 1e9
+    idx_traffic, idx_src = indexfree_traffic(kind, fixed8) if n == 1 << 30 else (None, None)
+    indexfree_roofline = {"algo_bytes": comp_bytes + n, "achieved": round(idx_ach, 1), "unit": "GB/s",
+                          "frac": round(idx_ach / HBM_PEAK_GBPS, 4), "traffic": idx_traffic,
+                          "traffic_x_algo": round(idx_traffic / (comp_bytes + n), 3) if idx_traffic else None,
+                          "traffic_source": idx_src}
     collective = None
     if world > 1:
         how = ("huff_mgpu_compress (library RCCL communicator)" if s.comm is not None
@@ -384,6 +414,7 @@ def run_workload(s: Setup, kind: str, n: int, with_cpu: bool):
                 "encode_ms": round(t_enc * 1e3 / args.steps, 4), "decode_ms": round(t_dec * 1e3 / args.steps, 4),
                 "indexfree_decode_GBps": round(world * n / (t_idx / args.steps) / 1e9, 1),
                 "indexfree_decode_ms": round(t_idx * 1e3 / args.steps, 4),
+                "indexfree_roofline": indexfree_roofline,
                 "note": "encode = pass 1 + host tree + pass 2 (+ the collective at N>1); decode = restart-index "
                         "decode; indexfree = huff_dev_decompress of the bare stream (spec/fix/scan/mark/decode, "
                         "one host read of the symbol count)"},
