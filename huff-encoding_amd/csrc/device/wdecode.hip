@@ -79,11 +79,6 @@ __device__ __forceinline__ void leaf_letter(const uint8_t* letters, uint32_t lea
     }
 }
 
-// One lane's letters [from, from + PL) of its 64, decoded into o (PL * W
-// bytes, PL * W / 4 dwords), window state carried between parts. Window:
-// 64-bit buf, valid-bit count in the low 6 bits of X (the rest don't-care),
-// refilled unconditionally (decode_wave.hip FX_REFILL): every two codes when
-// codes have <= 16 bits, before every code otherwise (R1).
 // the window shifted left by len (1..32 bits, the entries' code lengths) as
 // two 32-bit halves: no 64-bit shift by a VGPR amount, which the gfx950 shift
 // hazard makes depend on the register allocation
@@ -94,6 +89,11 @@ __device__ __forceinline__ uint64_t shl_window(uint64_t buf, uint32_t len) {
     return (static_cast<uint64_t>(nhi) << 32) | nlo;
 }
 
+// One lane's letters [from, from + PL) of its 64, decoded into o (PL * W
+// bytes, PL * W / 4 dwords), window state carried between parts. Window:
+// 64-bit buf, valid-bit count in the low 6 bits of X (the rest don't-care),
+// refilled unconditionally (decode_wave.hip FX_REFILL): every two codes when
+// codes have <= 16 bits, before every code otherwise (R1).
 template <uint32_t W>
 struct Lane {
     uint64_t buf;
@@ -264,7 +264,7 @@ __global__ __launch_bounds__(max_waves<W>() * 64) void k_wdec_task(WideDecArgs a
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const uint32_t K1 = a.stab_bits;
     const uint32_t t = threadIdx.x, lane = t & 63, wave = wave_index();
-    // LDS: [the table][leaf letters (W >= 8)] when LDS, then the waves' stages
+    // LDS: [the table][leaf letters (W >= 8, 4-byte leaves)] when LDS, then the waves' stages
     const uint32_t tab_bytes = LDS ? a.stab_bytes : 0u;
     const uint32_t let_bytes = LDS && leaf_letters<W>(a) ? (a.nleaves * W + 15) & ~15u : 0u;
     if constexpr (LDS) {
