@@ -32,7 +32,7 @@
 // incomplete final code (comp.rs:493-516).
 #include <algorithm>
 
-#include "bitreader.hpp"
+#include "segwalk.hpp"
 
 namespace huff::dev {
 
@@ -226,152 +226,7 @@ Seg make_seg(const IndexlessArgs& a) {
     return Seg{a.comp, a.comp_bytes, a.valid_bits, a.seg_bits, a.nseg, a.lut, a.lut_bits};
 }
 
-// ---- LDS-staged variants (every code <= 32 bits) ---------------------------
-// A workgroup's 256 consecutive segments are one contiguous bit range: it is
-// staged in LDS once with coalesced dword loads (plus 32 bytes of lookahead
-// for the code that crosses the last segment end), and each lane then reads
-// its bits from LDS: a 64-bit window refilled 32 bits at a time, multi-symbol
-// lookups (top 12 bits -> up to 3 letters) while the whole entry stays inside
-// the lane's range, single codes otherwise.
-
-struct Staged {
-    const uint32_t* w;
-    uint64_t base;       // bit position of w[0]'s most significant bit
-    const uint32_t* l2;  // the level-2 length table in LDS (null: the global multi-level table)
-};
-
-// The block's range from its 16-B granule, 8 loads of 16 B per lane in
-// flight per batch through a buffer resource over the range rounded up to
-// its last 16-B granule (pieces past it, incl. the two zero words the lanes'
-// lookahead may read, come back zero): the one-dword-at-a-time loop this
-// replaces waited out a memory latency per dword.
-__device__ Staged stage_block(const IndexlessArgs& a, uint32_t* w) {
-    const uint64_t seg0 = static_cast<uint64_t>(blockIdx.x) * kThreads;
-    const uint64_t bit_lo = seg0 * a.seg_bits;
-    const uint64_t seg_end = seg0 + kThreads < a.nseg ? seg0 + kThreads : a.nseg;
-    const uint64_t bit_hi = seg_end * a.seg_bits < a.valid_bits ? seg_end * a.seg_bits : a.valid_bits;
-    const uint64_t byte_lo = (bit_lo >> 3) & ~15ull;
-    uint64_t byte_hi = ((bit_hi + 7) >> 3) + 64;  // lookahead: a chunk's overshoot past the last end
-    if (byte_hi > a.comp_bytes) byte_hi = a.comp_bytes;
-    const uint32_t nbytes = static_cast<uint32_t>(byte_hi - byte_lo);
-    const uint32_t np = (nbytes + 8 + 15) / 16;  // + the two zero words
-    const auto rs = buf_rsrc(a.comp + byte_lo, (nbytes + 15) & ~15u);
-    uint4* w4 = reinterpret_cast<uint4*>(w);
-    for (uint32_t p0 = threadIdx.x; p0 < np; p0 += 8 * kThreads) {
-        uint4 v[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) v[k] = buf_ld16(rs, (p0 + k * kThreads) * 16);
-#pragma unroll
-        for (int k = 0; k < 8; ++k)
-            if (p0 + k * kThreads < np) w4[p0 + k * kThreads] = v[k];
-    }
-    return Staged{w, byte_lo * 8, nullptr};
-}
-
-// The staged kernels walk the stream one code per lookup in unrolled chunks
-// of 8 (u16 single-symbol table in LDS, as k_decode_fixed; no branch inside a
-// chunk), then settle where the walk should have stopped from the chunk's 8
-// code lengths kept in registers: a data-dependent loop per code (and a slow
-// path per lookup) cost ~40 VALU and ~40 SALU per step in the multi-symbol
-// form this replaces (PMC: 344 K VALU per SIMD per GiB).
-constexpr int kChunkSteps = 8;
-
-// lane cursor over the staged range: 64-bit window, valid bits in the low 6
-// bits of X (X -= entry borrows only above them), refilled unconditionally
-// every two codes (the next dword is read one refill ahead)
-struct Cursor {
-    const uint32_t* w;
-    const uint32_t* l2;
-    uint64_t buf;
-    uint32_t X, rp, nextw;
-    __device__ __forceinline__ void init(const Staged& st, uint64_t p) {
-        w = st.w;
-        l2 = st.l2;
-        const uint64_t rel = p - st.base;
-        rp = static_cast<uint32_t>(rel >> 5);
-        const uint32_t sh = static_cast<uint32_t>(rel & 31);
-        buf = static_cast<uint64_t>(__builtin_bswap32(w[rp]) << sh) << 32;
-        X = 32 - sh;
-        rp += 1;
-        nextw = __builtin_bswap32(w[rp]);
-    }
-    __device__ __forceinline__ void refill() {
-        buf |= (static_cast<uint64_t>(nextw) << 32) >> (X & 63);
-        rp += (X & 32) ? 0u : 1u;
-        X |= 32;
-        nextw = __builtin_bswap32(w[rp]);
-    }
-    // the length of the next code, consumed; codes longer than the table's
-    // index (kSsSlow) through the level-2 length table in LDS (descriptor
-    // index in the entry's bits [0, 7) and [8, 16)), else the global
-    // multi-level table
-    template <bool SLOW>
-    __device__ __forceinline__ uint32_t step(const uint16_t* stab, uint32_t K, const uint32_t* glut, uint32_t Kg) {
-        uint32_t e = stab[static_cast<uint32_t>(buf >> 32) >> (32 - K)];
-        if (SLOW && (e & kSsSlow) && l2) {
-            refill();  // >= 32 valid bits: the whole code (<= 32 bits)
-            const uint32_t d = l2[(e & 0x7Fu) | ((e >> 8) << 7)];
-            const uint32_t E = d & 31u;
-            const uint32_t j = (static_cast<uint32_t>(buf >> 32) << K) >> (32 - E);
-            const uint32_t l1 = reinterpret_cast<const uint8_t*>(l2)[(d >> 5) + j];
-            buf <<= l1;
-            X -= l1;
-            refill();
-            return l1;
-        }
-        if (SLOW && (e & kSsSlow)) {
-            refill();
-            uint32_t e1 = glut[static_cast<uint32_t>(buf >> (64 - Kg))];
-            uint32_t d = Kg;
-            while (e1 & kLutPtr) {
-                const uint32_t idx = static_cast<uint32_t>((buf >> (56 - d)) & 0xFFu);
-                e1 = glut[(e1 & ~kLutPtr) + idx];
-                d += 8;
-            }
-            const uint32_t l1 = (e1 >> 8) & 0xFFu;
-            buf <<= l1;
-            X -= l1;
-            refill();
-            return l1;
-        }
-        buf <<= (e & 63u);
-        X -= e;
-        return e & 63u;
-    }
-    template <bool SLOW>
-    __device__ __forceinline__ void chunk(uint32_t (&L)[kChunkSteps], const uint16_t* stab, uint32_t K,
-                                          const uint32_t* glut, uint32_t Kg) {
-#pragma unroll
-        for (int k = 0; k < kChunkSteps; ++k) {
-            if ((k & 1) == 0) refill();
-            L[k] = step<SLOW>(stab, K, glut, Kg);
-        }
-    }
-    // kChunkSteps windows, each consuming ALL its complete codes (walk table:
-    // bits used, count): U bits and N codes in total, ~2 codes per lookup on
-    // Zipf bytes. A window whose first code is longer than K takes that code.
-    template <bool SLOW>
-    __device__ __forceinline__ void multi_chunk(uint32_t& U, uint32_t& N, const uint16_t* wtab, const uint16_t* stab,
-                                                uint32_t K, const uint32_t* glut, uint32_t Kg) {
-        U = 0;
-        N = 0;
-#pragma unroll
-        for (int k = 0; k < kChunkSteps; ++k) {
-            if ((k & 1) == 0) refill();
-            const uint32_t e = wtab[static_cast<uint32_t>(buf >> 32) >> (32 - K)];
-            if (SLOW && (e & kSsSlow)) {
-                U += step<SLOW>(stab, K, glut, Kg);
-                N += 1;
-            } else {
-                const uint32_t u = (e >> 8) & 15u;
-                buf <<= u;
-                X -= u;
-                U += u;
-                N += e >> 12;
-            }
-        }
-    }
-};
+// ---- LDS-staged variants (every code <= 32 bits; segwalk.hpp) -------------
 
 // A sample word (segments of < 1024 bits): bits [0, 10) = offset of a
 // boundary of the speculative path from the segment start, [10, 20) = its
@@ -401,26 +256,6 @@ __device__ __forceinline__ void samp_pick(const uint32_t (&sv)[kSampMax], uint32
         idx = ok ? mi : idx;
         rel = ok ? mo : rel;
     }
-}
-
-// LDS: [single-symbol table][walk table (if any)][staged input]
-__device__ __forceinline__ uint32_t stab_words(const IndexlessArgs& a) {
-    return ((((1u << a.stab_bits) + 1) / 2) + 3) & ~3u;
-}
-__device__ __forceinline__ uint32_t tables_words(const IndexlessArgs& a) {
-    return stab_words(a) + a.l2_words;
-}
-__device__ __forceinline__ const uint16_t* load_stab(const IndexlessArgs& a, uint32_t* lds) {
-    // the walk table when there is one (its low bits are stab's lengths), else stab
-    const uint32_t words = ((1u << a.stab_bits) + 1) / 2;
-    const uint32_t* src = reinterpret_cast<const uint32_t*>(a.wtab ? a.wtab : a.stab);
-    for (uint32_t i = threadIdx.x; i < words; i += blockDim.x) lds[i] = src[i];
-    for (uint32_t i = threadIdx.x; i < a.l2_words; i += blockDim.x) lds[stab_words(a) + i] = a.l2[i];
-    return reinterpret_cast<const uint16_t*>(lds);
-}
-__device__ __forceinline__ Staged with_l2(Staged st, const IndexlessArgs& a, const uint32_t* lds) {
-    st.l2 = a.l2_words ? lds + stab_words(a) : nullptr;
-    return st;
 }
 
 template <bool SLOW>

@@ -164,6 +164,52 @@ struct IndexlessArgs {
     const uint32_t* l2;
     uint32_t l2_words;
 };
+// Index-free decode split at the scan (isplit.hip), codes <= 32 bits:
+//   k_sync   (A): speculative walk of every S-bit segment + in-workgroup
+//                 fix-up; writes, per LANE (a segment cut into R pieces at
+//                 the first boundaries at or past i S + q S / R), a record
+//                 {start - theta, letter count}, the segment's exit and the
+//                 letter totals of the output blocks (256 lanes each)
+//   k_fix_rec    : cross-workgroup fix-up of the records (rounds + sweep)
+//   scan of the block totals
+//   k_emit   (B): each lane decodes its letters from its settled start into
+//                 the block's LDS image; coalesced 16-B stores
+constexpr uint32_t kSplitRmax = 8;
+struct SplitArgs {
+    const uint8_t* comp;          // 16-B aligned
+    uint64_t comp_bytes;
+    uint64_t valid_bits;          // B
+    uint64_t seg_bits;            // S (< 1024, a multiple of the gcd of the code lengths)
+    uint64_t nseg;
+    uint32_t lg_r;                // R = 1 << lg_r lanes per segment (R <= kSplitRmax)
+    uint32_t nsamp;               // merge samples per segment (every kSampBits bits; <= kSampMax)
+    const uint32_t* lut;          // multi-level table (codes longer than stab_bits)
+    uint32_t lut_bits;
+    uint32_t max_len;             // <= 32
+    const uint16_t* stab;         // single-symbol table (letter, length)
+    uint32_t stab_bits;
+    const uint16_t* wtab;         // walk table (k_sync); k_emit reads stab
+    const uint32_t* l2;           // level-2 length table (k_sync's slow steps; null: lut)
+    uint32_t l2_words;
+    uint32_t* rec;                // [nseg << lg_r] (start - theta) | count << 10
+    uint8_t* xd;                  // [nseg] exit - segment end (< 32)
+    unsigned long long* btot;     // [nblk] letters per output block (256 lanes)
+    uint32_t* fixlist;            // segments k_sync left unsettled (besides every workgroup's first)
+    unsigned int* flags;          // [kFixRounds + 1] as IndexlessArgs::flags
+    // k_emit
+    const unsigned long long* boff;  // [nblk + 1] exclusive scan of btot
+    uint8_t* out;                 // 16-B aligned, boff[nblk] letters
+    uint32_t stage_bytes;         // LDS stage per workgroup (a multiple of 16)
+    uint32_t img_bytes;           // LDS output image per workgroup (a multiple of 16)
+    unsigned long long* end_bit;  // may be null: the bit after the last complete code
+};
+__host__ __device__ inline uint64_t split_blocks(uint64_t nseg, uint32_t lg_r) { return ((nseg << lg_r) + 255) / 256; }
+size_t split_sync_lds_bytes(const SplitArgs& a);
+size_t split_emit_lds_bytes(const SplitArgs& a);
+hipError_t launch_split_sync(const SplitArgs& a, hipStream_t s);
+hipError_t launch_split_fix(const SplitArgs& a, hipStream_t s);  // round 0 (list), rounds, sweep
+hipError_t launch_split_emit(const SplitArgs& a, hipStream_t s);
+
 // single-pass index-free decode (ifdec.hip)
 constexpr uint32_t kIfdPrefixCap = 32;  // letters a lane's fix-up walk keeps before it gives up (slow lane)
 constexpr uint32_t kIfdStageMax = 4 * 256 * 16;  // a block's staged bytes (4 pieces per thread in flight)
@@ -287,10 +333,13 @@ hipError_t launch_wide_decode(const WideDecArgs& a, hipStream_t s);       // cod
 hipError_t launch_wide_decode_task(const WideDecArgs& a, hipStream_t s);  // codes <= 32 bits (wdecode.hip)
 // build_weights_map on the device (wweights.hip). width <= 2: counts = the
 // 2^(8 width) bins (zeroed). width >= 4: an HBM table of `slots`
-// (wcount_slots) keys_lo (all ones), counts (zero), width 16 also keys_hi and
-// state (zero); the used slots are appended to out_lo / out_hi / out_c
-// (capacity min(n, slots)), their number to *nout (zero), the all-ones u64
-// letter's count to *sent (zero; width 8).
+// (wcount_slots of a guess of the distinct letters) keys_lo (all ones),
+// counts (zero), width 16 also keys_hi and state (zero); *used counts the
+// claimed slots and *overflow (zeroed) is set when the table is too full (the
+// host grows it and counts again; `unbounded`: the last size, no limits). Then
+// wextract_launch appends the used slots to out_lo / out_hi / out_c
+// (capacity *used), their number to *nout (zero); the all-ones u64 letter's
+// count goes to *sent (zero; width 8).
 struct WCountArgs {
     const uint8_t* in;  // n letters, 4-B aligned (width >= 4: width-aligned)
     uint64_t n;
@@ -299,14 +348,18 @@ struct WCountArgs {
     unsigned long long *keys_lo, *keys_hi, *counts, *sent;
     unsigned int* state;
     unsigned long long *out_lo, *out_hi, *out_c, *nout;
+    unsigned long long* used;
+    unsigned int* overflow;
+    uint32_t unbounded;
 };
-uint64_t wcount_slots(uint32_t width, uint64_t n);
+uint64_t wcount_slots(uint32_t width, uint64_t distinct);
 hipError_t wcount_launch(const WCountArgs& a, hipStream_t s);
+hipError_t wextract_launch(const WCountArgs& a, hipStream_t s);
 
 // HuffTree of many small byte streams in one launch (tree_batch.hip)
 constexpr uint32_t kTreeBitsMaxBytes = (2 * 257 - 1 + 8 * 257 + 7) / 8;  // as_bin of 257 leaves
 constexpr uint32_t kTreeCodeMax = 56;  // codes[] holds code << 8 | len
-enum : uint32_t { kTreeOk = 0, kTreeEmpty = 2, kTreeDeep = 7 };  // = HUFF_OK, HUFF_E_EMPTY_WEIGHTS, HUFF_E_CODE_TOO_LONG
+enum : uint32_t { kTreeOk = 0, kTreeHeavy = 1, kTreeEmpty = 2, kTreeDeep = 7 };  // = HUFF_OK, HUFF_E_INVALID_ARG (weights sum >= 2^54), HUFF_E_EMPTY_WEIGHTS, HUFF_E_CODE_TOO_LONG
 struct TreeBatchArgs {
     const uint64_t* hist;   // [nstreams][256] byte weights
     uint32_t nstreams;

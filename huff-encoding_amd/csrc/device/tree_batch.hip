@@ -30,30 +30,41 @@ constexpr int kHeapCap = 257;       // 256 letters + the byte-0 re-yield
 constexpr uint32_t kNodeBits = 10;  // heap key = weight << 10 | node (node < 2 * 257)
 
 // ---------------------------------------------------------------------------
+// A stream longer than 2^31 bytes is counted in pieces (a u32 LDS bin could
+// wrap within 2^32 bytes); each bin's piece counts add up in its thread's u64.
+// A stream with d_offsets[s + 1] < d_offsets[s] counts as empty.
+constexpr uint64_t kHistPiece = 1ull << 31;
 __global__ __launch_bounds__(256) void k_hist_batch(const uint8_t* __restrict__ in,
                                                     const uint64_t* __restrict__ off, uint64_t* __restrict__ hist) {
     __shared__ uint32_t bins[256];
     const uint32_t s = blockIdx.x, t = threadIdx.x;
-    bins[t] = 0;
-    __syncthreads();
-    const uint64_t lo = off[s], hi = off[s + 1];
-    // head bytes up to 4-B alignment, then dwords, then the tail
-    const uint64_t a0 = (lo + 3) & ~3ull;
-    const uint64_t mid_lo = a0 < hi ? a0 : hi;
-    const uint64_t mid_hi = mid_lo + ((hi - mid_lo) & ~3ull);
-    if (t < mid_lo - lo) atomicAdd(&bins[in[lo + t]], 1u);
-    const uint32_t* w = reinterpret_cast<const uint32_t*>(in + mid_lo);
-    const uint64_t nw = (mid_hi - mid_lo) / 4;
-    for (uint64_t i = t; i < nw; i += 256) {
-        const uint32_t v = w[i];
-        atomicAdd(&bins[v & 0xFF], 1u);
-        atomicAdd(&bins[(v >> 8) & 0xFF], 1u);
-        atomicAdd(&bins[(v >> 16) & 0xFF], 1u);
-        atomicAdd(&bins[v >> 24], 1u);
+    const uint64_t lo0 = off[s], hi0 = off[s + 1] > lo0 ? off[s + 1] : lo0;
+    uint64_t acc = 0;
+    for (uint64_t lo = lo0; lo < hi0 || lo == lo0; lo += kHistPiece) {
+        const uint64_t hi = hi0 - lo > kHistPiece ? lo + kHistPiece : hi0;
+        bins[t] = 0;
+        __syncthreads();
+        // head bytes up to 4-B alignment, then dwords, then the tail
+        const uint64_t a0 = (lo + 3) & ~3ull;
+        const uint64_t mid_lo = a0 < hi ? a0 : hi;
+        const uint64_t mid_hi = mid_lo + ((hi - mid_lo) & ~3ull);
+        if (t < mid_lo - lo) atomicAdd(&bins[in[lo + t]], 1u);
+        const uint32_t* w = reinterpret_cast<const uint32_t*>(in + mid_lo);
+        const uint64_t nw = (mid_hi - mid_lo) / 4;
+        for (uint64_t i = t; i < nw; i += 256) {
+            const uint32_t v = w[i];
+            atomicAdd(&bins[v & 0xFF], 1u);
+            atomicAdd(&bins[(v >> 8) & 0xFF], 1u);
+            atomicAdd(&bins[(v >> 16) & 0xFF], 1u);
+            atomicAdd(&bins[v >> 24], 1u);
+        }
+        if (t < hi - mid_hi) atomicAdd(&bins[in[mid_hi + t]], 1u);
+        __syncthreads();
+        acc += bins[t];
+        __syncthreads();
+        if (hi >= hi0) break;
     }
-    if (t < hi - mid_hi) atomicAdd(&bins[in[mid_hi + t]], 1u);
-    __syncthreads();
-    hist[static_cast<uint64_t>(s) * 256 + t] = bins[t];
+    hist[static_cast<uint64_t>(s) * 256 + t] = acc;
 }
 
 // ---------------------------------------------------------------------------
@@ -165,6 +176,23 @@ __global__ __launch_bounds__(kTreeLanes) void k_tree_batch(TreeBatchArgs a) {
         leaf[nl][lane] = 0;
         hp.push((w0 << kNodeBits) | nl);
         ++nl;
+    }
+    // the heap keys hold weight << kNodeBits: every joint's weight (at most
+    // the total) must stay below 2^54
+    {
+        uint64_t total = w0 != 0 && last != 255 ? w0 : 0;
+        bool heavy = (total >> 54) != 0;
+        for (uint32_t b = 0; b < 256; ++b) {
+            const uint64_t wb = h[b];
+            heavy |= (wb >> 54) != 0;
+            total += heavy ? 0 : wb;
+            heavy |= (total >> 54) != 0;
+        }
+        if (heavy) {
+            a.status[s] = kTreeHeavy;
+            a.tree_nbits[s] = 0;
+            return;
+        }
     }
     if (nl == 0) {  // tree_inner.rs:283-285
         a.status[s] = kTreeEmpty;

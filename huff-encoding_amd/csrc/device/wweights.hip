@@ -8,9 +8,12 @@
 //             workgroup's letters cannot overflow a u16), then adds its
 //             non-zero bins to the global u64 bins; the bins ARE the answer in
 //             ascending order.
-//  W = 4, 8   an open-addressing table in HBM (2^k slots >= 2 n, linear
-//             probing, key claimed by a 64-bit compare-and-swap, counts by
-//             64-bit atomic adds), fed through a per-workgroup LDS table of
+//  W = 4, 8   an open-addressing table in HBM (2^k slots, linear probing,
+//             key claimed by a 64-bit compare-and-swap, counts by 64-bit
+//             atomic adds; the host sizes it for a guess of the distinct
+//             letters and grows it when the kernel reports it too full: the
+//             claims past 3/4 of the slots or a probe run past its limit set
+//             the overflow word), fed through a per-workgroup LDS table of
 //             2,048 slots that absorbs the repeats of frequent letters (a
 //             letter whose LDS probe runs long goes straight to HBM). The
 //             all-ones u64 is the empty-slot marker; that letter (W = 8) is
@@ -21,6 +24,8 @@
 //             another lane of its own wave inside one branch.
 //  extract    the used slots are appended to (key, count) arrays; the host
 //             sorts them by key (distinct letters only).
+#include <algorithm>
+
 #include "kernels.hpp"
 
 namespace huff::dev {
@@ -83,28 +88,44 @@ __device__ __forceinline__ uint64_t key64(const uint8_t* in, uint64_t i) {
     else return *reinterpret_cast<const uint64_t*>(in + 8 * i);
 }
 
+// the table's bookkeeping: claimed slots, overflow flag (the host grows the
+// table and counts again), probe limit, the claims allowed
+struct HbmTab {
+    unsigned long long* used;
+    unsigned int* overflow;
+    uint64_t mask, max_probe, max_used;
+    __device__ __forceinline__ void claimed() const {
+        if (atomicAdd(used, 1ull) + 1 > max_used) atomicOr(overflow, 1u);
+    }
+};
+
 // one letter (count c) into the HBM table (W <= 8)
-__device__ __forceinline__ void hbm_add(unsigned long long* keys, unsigned long long* counts, uint64_t mask,
+__device__ __forceinline__ void hbm_add(unsigned long long* keys, unsigned long long* counts, const HbmTab& tab,
                                         unsigned long long* sent, uint64_t key, uint64_t c) {
     if (key == kEmpty) {
         atomicAdd(sent, static_cast<unsigned long long>(c));
         return;
     }
-    for (uint64_t s = mix64(key) & mask;; s = (s + 1) & mask) {
+    uint64_t s = mix64(key) & tab.mask;
+    for (uint64_t p = 0; p < tab.max_probe; ++p, s = (s + 1) & tab.mask) {
         unsigned long long k = __hip_atomic_load(keys + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (k == kEmpty) k = atomicCAS(keys + s, kEmpty, static_cast<unsigned long long>(key));
+        if (k == kEmpty) {
+            k = atomicCAS(keys + s, kEmpty, static_cast<unsigned long long>(key));
+            if (k == kEmpty) tab.claimed();
+        }
         if (k == kEmpty || k == key) {
             atomicAdd(counts + s, static_cast<unsigned long long>(c));
             return;
         }
     }
+    atomicOr(tab.overflow, 1u);  // a probe run this long: the table is too small
 }
 
 // W = 4 / 8: a grid-stride pass through an LDS table per workgroup
 template <uint32_t W>
 __global__ __launch_bounds__(kT) void k_wcount_hash(const uint8_t* __restrict__ in, uint64_t n,
                                                     unsigned long long* __restrict__ keys,
-                                                    unsigned long long* __restrict__ counts, uint64_t mask,
+                                                    unsigned long long* __restrict__ counts, HbmTab tab,
                                                     unsigned long long* __restrict__ sent) {
     __shared__ unsigned long long lk[kLdsSlots];
     __shared__ uint32_t lc[kLdsSlots];
@@ -129,11 +150,11 @@ __global__ __launch_bounds__(kT) void k_wcount_hash(const uint8_t* __restrict__ 
                 }
             }
         }
-        if (!done) hbm_add(keys, counts, mask, sent, key, 1);
+        if (!done) hbm_add(keys, counts, tab, sent, key, 1);
     }
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < kLdsSlots; i += kT)
-        if (lc[i]) hbm_add(keys, counts, mask, sent, lk[i], lc[i]);
+        if (lc[i]) hbm_add(keys, counts, tab, sent, lk[i], lc[i]);
 }
 
 // W = 16: state 0 empty, 1 being written, 2 ready; rounds over the whole wave
@@ -141,12 +162,13 @@ __global__ __launch_bounds__(kT) void k_wcount_hash16(const uint8_t* __restrict_
                                                       unsigned long long* __restrict__ klo,
                                                       unsigned long long* __restrict__ khi,
                                                       unsigned int* __restrict__ state,
-                                                      unsigned long long* __restrict__ counts, uint64_t mask) {
+                                                      unsigned long long* __restrict__ counts, HbmTab tab) {
+    const uint64_t mask = tab.mask;
     const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kT;
     for (uint64_t base = static_cast<uint64_t>(blockIdx.x) * kT; base < n; base += stride) {
         const uint64_t i = base + threadIdx.x;
         bool pending = i < n;
-        uint64_t lo = 0, hi = 0, s = 0;
+        uint64_t lo = 0, hi = 0, s = 0, probes = 0;
         if (pending) {
             lo = *reinterpret_cast<const uint64_t*>(in + 16 * i);
             hi = *reinterpret_cast<const uint64_t*>(in + 16 * i + 8);
@@ -156,6 +178,7 @@ __global__ __launch_bounds__(kT) void k_wcount_hash16(const uint8_t* __restrict_
             if (pending) {
                 uint32_t st = __hip_atomic_load(state + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if (st == 0 && atomicCAS(state + s, 0u, 1u) == 0u) {
+                    tab.claimed();
                     __hip_atomic_store(klo + s, lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     __hip_atomic_store(khi + s, hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -167,6 +190,9 @@ __global__ __launch_bounds__(kT) void k_wcount_hash16(const uint8_t* __restrict_
                     const uint64_t b = __hip_atomic_load(khi + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     if (a == lo && b == hi) {
                         atomicAdd(counts + s, 1ull);
+                        pending = false;
+                    } else if (++probes >= tab.max_probe) {  // the table is too small: counted again, larger
+                        atomicOr(tab.overflow, 1u);
                         pending = false;
                     } else {
                         s = (s + 1) & mask;
@@ -204,15 +230,19 @@ uint32_t grid_for(uint64_t items, uint32_t per_thread, uint32_t cap) {
 
 }  // namespace
 
-uint64_t wcount_slots(uint32_t width, uint64_t n) {
+uint64_t wcount_slots(uint32_t width, uint64_t distinct) {
     if (width <= 2) return 1ull << (8 * width);
     uint64_t s = 1024;
-    while (s < 2 * n) s <<= 1;
+    while (s < 2 * distinct) s <<= 1;
     return s;
 }
 
 hipError_t wcount_launch(const WCountArgs& a, hipStream_t st) {
     if (a.n == 0) return hipSuccess;
+    // claims up to 3/4 of the slots; probe runs up to 4,096 slots (the whole
+    // table when the host says this is the last size it will try)
+    const HbmTab tab{a.used, a.overflow, a.slots - 1, a.unbounded ? a.slots : std::min<uint64_t>(a.slots, 4096),
+                     a.unbounded ? a.slots : a.slots / 4 * 3};
     switch (a.width) {
         case 1:
             hipLaunchKernelGGL(k_wcount_direct<1>, dim3(static_cast<uint32_t>((a.n + kDirectPerBlock - 1) / kDirectPerBlock)),
@@ -228,21 +258,24 @@ hipError_t wcount_launch(const WCountArgs& a, hipStream_t st) {
         }
         case 4:
             hipLaunchKernelGGL(k_wcount_hash<4>, dim3(grid_for(a.n, 64, 4096)), dim3(kT), 0, st, a.in, a.n, a.keys_lo,
-                               a.counts, a.slots - 1, a.sent);
+                               a.counts, tab, a.sent);
             break;
         case 8:
             hipLaunchKernelGGL(k_wcount_hash<8>, dim3(grid_for(a.n, 64, 4096)), dim3(kT), 0, st, a.in, a.n, a.keys_lo,
-                               a.counts, a.slots - 1, a.sent);
+                               a.counts, tab, a.sent);
             break;
         case 16:
             hipLaunchKernelGGL(k_wcount_hash16, dim3(grid_for(a.n, 16, 8192)), dim3(kT), 0, st, a.in, a.n, a.keys_lo,
-                               a.keys_hi, a.state, a.counts, a.slots - 1);
+                               a.keys_hi, a.state, a.counts, tab);
             break;
         default:
             return hipErrorInvalidValue;
     }
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess || a.width <= 2) return e;
+    return hipGetLastError();
+}
+
+hipError_t wextract_launch(const WCountArgs& a, hipStream_t st) {
+    if (a.n == 0 || a.width <= 2) return hipSuccess;
     hipLaunchKernelGGL(k_wextract, dim3(grid_for(a.slots, 16, 8192)), dim3(kT), 0, st, a.keys_lo,
                        a.width == 16 ? a.keys_hi : nullptr, a.counts, a.slots, a.out_lo, a.out_hi, a.out_c, a.nout);
     return hipGetLastError();

@@ -92,11 +92,24 @@ int huff_comm_init(huff_ctx* ctx, const uint8_t id[HUFF_COMM_ID_BYTES], int worl
 
 void huff_comm_free(huff_comm* c) { delete c; }
 
+// The world the communicator itself reports (ncclCommCount /
+// ncclCommUserRank), not the arguments it was created with: a bench line can
+// then prove how many ranks RCCL joined (huff/src/comp.rs:161-172 is the
+// merge this communicator replaces).
 int huff_comm_world(const huff_comm* c, int* world, int* rank) {
     if (!c || !world || !rank) return fail(HUFF_E_INVALID_ARG, "null argument");
-    *world = c->world;
-    *rank = c->rank;
-    return HUFF_OK;
+    return guarded([&]() -> huff::Status {
+        int n = 0, r = 0;
+        NCCL_TRY(ncclCommCount(c->comm, &n));
+        NCCL_TRY(ncclCommUserRank(c->comm, &r));
+        if (n != c->world || r != c->rank)
+            return huff::Status::err(HUFF_E_HIP, "RCCL reports world " + std::to_string(n) + " rank " +
+                                                     std::to_string(r) + ", created as world " +
+                                                     std::to_string(c->world) + " rank " + std::to_string(c->rank));
+        *world = n;
+        *rank = r;
+        return huff::Status::ok();
+    });
 }
 
 int huff_mgpu_pack_rows(huff_enc* e, const int64_t* rows, int world, int rank, uint8_t* d_out, size_t out_cap,
@@ -141,20 +154,21 @@ int huff_mgpu_compress(huff_comm* c, huff_enc* e, uint8_t* d_out, size_t out_cap
     if (tree_out) *tree_out = nullptr;
     // A rank that cannot run its pass 1 still takes part in the collective,
     // with a row that marks it failed (tail count -1): every rank then
-    // returns an error instead of the others blocking in ncclAllGather.
-    std::string local;
-    if (!e || !d_out || !tree_out) local = "null argument";
-    else if (e->ctx != c->ctx) local = "a job of another context";
-    else if (reinterpret_cast<uintptr_t>(d_out) & 15) local = "d_out must be 16-byte aligned";
+    // returns an error instead of the others blocking in ncclAllGather. The
+    // local failure keeps its own status code (argument, HIP, memory).
+    huff::Status local;
+    if (!e || !d_out || !tree_out) local = huff::Status::err(HUFF_E_INVALID_ARG, "null argument");
+    else if (e->ctx != c->ctx) local = huff::Status::err(HUFF_E_INVALID_ARG, "a job of another context");
+    else if (reinterpret_cast<uintptr_t>(d_out) & 15)
+        local = huff::Status::err(HUFF_E_INVALID_ARG, "d_out must be 16-byte aligned");
     return guarded([&]() -> huff::Status {
         huff_ctx* ctx = c->ctx;
+        // a context that cannot be activated cannot post its row either: the
+        // other ranks would block in the collective, so say so loudly
         HUFF_TRY(ctx->activate());
         const size_t world = static_cast<size_t>(c->world);
-        if (local.empty()) {
-            const huff::Status st = e->hist_row(static_cast<long long*>(c->row.p));
-            if (st) local = st.msg;
-        }
-        if (!local.empty()) {
+        if (!local) local = e->hist_row(static_cast<long long*>(c->row.p));
+        if (local) {
             static const std::vector<int64_t> bad = [] {
                 std::vector<int64_t> r(kRowWords, 0);
                 r[257] = -1;
@@ -166,7 +180,7 @@ int huff_mgpu_compress(huff_comm* c, huff_enc* e, uint8_t* d_out, size_t out_cap
         HIP_TRY_RT(hipMemcpyAsync(c->host_rows.p, c->rows.p, kRowWords * 8 * world, hipMemcpyDeviceToHost,
                                   ctx->stream));
         HUFF_TRY(ctx->sync());
-        if (!local.empty()) return huff::Status::err(HUFF_E_INVALID_ARG, local);
+        if (local) return local;
         const int rc = huff_mgpu_pack_rows(e, static_cast<const int64_t*>(c->host_rows.p), c->world, c->rank, d_out,
                                            out_cap, tree_out, bit_base_out, bits_out, owned_bytes_out);
         if (rc != HUFF_OK) return huff::Status::err(rc, huff::capi::last_error());

@@ -115,6 +115,13 @@ bool fixed8_disabled() {
     return e && *e && *e != '0';
 }
 
+// HUFF_SPLIT=0: index-free byte streams take the older sample + mark path
+// (the wide decoders still use it; the tests run both)
+bool split_disabled() {
+    const char* e = std::getenv("HUFF_SPLIT");  // read per call: tests flip it
+    return e && *e == '0';
+}
+
 uint32_t decode_check_mode() {
     const char* e = std::getenv("HUFF_DEC_VARIANT");  // read per call: tests flip it
     if (!e) return 0;
@@ -1328,6 +1335,119 @@ static Status decode_indexless_single(huff_ctx* ctx, const uint8_t* d_comp, uint
     return Status::ok();
 }
 
+// The split index-free decoder (isplit.hip) for codes <= 32 bits: k_sync
+// (speculative walk + in-group fix-up -> lane records), k_fix_rec, the scan
+// of the block letters, one host read of the total, k_emit. *done = false
+// when the stream does not fit its limits (the caller takes the older path).
+static Status decode_split(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_bytes, uint64_t valid_bits,
+                           const huff_tree* t, const DecTables* dt, DevBuf& out, uint64_t* nsym, uint8_t* d_user,
+                           size_t user_cap, unsigned long long* d_end, bool* done) {
+    *done = false;
+    if (dt->maxdepth > 32 || !dt->sbits) return Status::ok();
+    // S as the sync pass of the older path: a multiple of the gcd g of the
+    // code lengths near 992 bits, preferring S = 32 mod 64 (odd dword stride
+    // between the lanes' stage reads), below 1024 (10-bit record fields)
+    uint32_t g = 0;
+    double mean = 0;
+    for (const LeafCode& lc : t->t.leaves()) {
+        g = std::gcd(g, lc.len);
+        mean += std::ldexp(static_cast<double>(lc.len), -static_cast<int>(lc.len));  // ~ bits per letter
+    }
+    if (g == 0) g = 1;
+    mean = std::max(mean, 1.0);
+    const uint64_t seg_target = 992;
+    uint64_t S = static_cast<uint64_t>(g) * ((seg_target + g - 1) / g);
+    for (uint64_t k = (seg_target + g - 1) / g, tries = 0; tries < 128; ++k, ++tries)
+        if ((static_cast<uint64_t>(g) * k) % 64 == 32) {
+            S = static_cast<uint64_t>(g) * k;
+            break;
+        }
+    if (S >= 1024) S = static_cast<uint64_t>(g) * (1023 / g);
+    if (S < 256) return Status::ok();
+    const uint64_t nseg = (valid_bits + S - 1) / S;
+    if (nseg > 0xFFFFFFFFull / dev::kSplitRmax) return Status::ok();
+    // lanes per segment: about 48 letters each (at most 56 expected), so a
+    // lane's letters fit one 64-letter pass of k_emit's registers
+    uint32_t lg_r = 0;
+    while ((1u << lg_r) < dev::kSplitRmax && static_cast<double>(S >> lg_r) / mean > 56.0) ++lg_r;
+    dev::SplitArgs a{};
+    a.comp = d_comp;
+    a.comp_bytes = comp_bytes;
+    a.valid_bits = valid_bits;
+    a.seg_bits = S;
+    a.nseg = nseg;
+    a.lg_r = lg_r;
+    a.nsamp = std::min<uint32_t>(dev::kSampMax, static_cast<uint32_t>((S - 1) / dev::kSampBits));
+    a.lut = static_cast<const uint32_t*>(ctx->d_lut.p);
+    a.lut_bits = dt->bits;
+    a.max_len = dt->maxdepth;
+    a.stab = reinterpret_cast<const uint16_t*>(static_cast<const uint32_t*>(ctx->d_lut.p) + dt->soff);
+    a.stab_bits = dt->sbits;
+    a.wtab = reinterpret_cast<const uint16_t*>(static_cast<const uint32_t*>(ctx->d_lut.p) + dt->woff);
+    if (dt->l2words) {
+        a.l2 = static_cast<const uint32_t*>(ctx->d_lut.p) + dt->l2off;
+        a.l2_words = dt->l2words;
+    }
+    // k_emit's stage: the block's 256 lanes from its first segment's 16-B
+    // granule, the last lane's overrun past the next block's first theta
+    // (< 300 bits), a code and the window's read-ahead
+    a.stage_bytes = static_cast<uint32_t>((((256 * S) >> lg_r) + 128 + 512 + 128 + 7) / 8 + 15) & ~15u;
+    // its output image: the block's expected letters with a margin (a block
+    // with more writes straight to HBM)
+    const double exp_letters = 256.0 * static_cast<double>(S >> lg_r) / mean;
+    a.img_bytes = static_cast<uint32_t>(std::min(1.25 * exp_letters + 1024.0, 64.0 * 1024)) & ~15u;
+    if (dev::split_sync_lds_bytes(a) > 140 * 1024 || dev::split_emit_lds_bytes(a) > 160 * 1024) return Status::ok();
+    IndexlessSync& st = ctx->indexless_ws();
+    const uint64_t nl = nseg << lg_r;
+    const uint64_t nblk = dev::split_blocks(nseg, lg_r);
+    HUFF_TRY(st.rec.ensure(nl * 4));
+    HUFF_TRY(st.xd.ensure(nseg + 16));
+    HUFF_TRY(st.btot.ensure(nblk * 8));
+    HUFF_TRY(st.boff.ensure((nblk + 1) * 8));
+    HUFF_TRY(st.fixlist.ensure(nseg * 4 + 4));
+    HUFF_TRY(st.flag.ensure((dev::kFixRounds + 1) * 4));
+    HUFF_TRY(st.tsum.ensure((nblk / 1024 + 2) * 8));
+    a.rec = static_cast<uint32_t*>(st.rec.p);
+    a.xd = static_cast<uint8_t*>(st.xd.p);
+    a.btot = static_cast<unsigned long long*>(st.btot.p);
+    a.boff = static_cast<const unsigned long long*>(st.boff.p);
+    a.fixlist = static_cast<uint32_t*>(st.fixlist.p);
+    a.flags = static_cast<unsigned int*>(st.flag.p);
+    hipStream_t strm = ctx->stream;
+    HIP_TRY(hipMemsetAsync(st.flag.p, 0, (dev::kFixRounds + 1) * 4, strm));
+    HUFF_TRY(ctx->timed("split_sync", [&] { return dev::launch_split_sync(a, strm); }));
+    HUFF_TRY(ctx->timed("split_fix", [&] { return dev::launch_split_fix(a, strm); }));
+    HIP_TRY(dev::launch_scan(static_cast<const uint64_t*>(st.btot.p), static_cast<uint32_t>(nblk), 0,
+                             static_cast<uint64_t*>(st.boff.p), static_cast<uint64_t*>(st.tsum.p), strm));
+    uint64_t total = 0;
+    HIP_TRY(hipMemcpyAsync(&total, static_cast<uint64_t*>(st.boff.p) + nblk, 8, hipMemcpyDeviceToHost, strm));
+    HUFF_TRY(ctx->sync());
+    *nsym = total;
+    *done = true;
+    if (total == 0) {
+        if (d_end) HIP_TRY(hipMemsetAsync(d_end, 0, 8, strm));
+        return Status::ok();
+    }
+    uint8_t* dst;
+    if (d_user) {
+        if (total > user_cap) return Status::err(HUFF_E_BUFFER_TOO_SMALL, "output buffer too small");
+        dst = d_user;
+    } else {
+        HUFF_TRY(out.ensure(total + 16));
+        dst = static_cast<uint8_t*>(out.p);
+    }
+    // the kernel stores 16-B pieces: a misaligned output is decoded into an
+    // aligned buffer, then copied
+    const bool bounce = reinterpret_cast<uintptr_t>(dst) & 15;
+    if (bounce) HUFF_TRY(ctx->d_align.ensure(total + 64));
+    a.out = bounce ? static_cast<uint8_t*>(ctx->d_align.p) : dst;
+    a.end_bit = d_end;
+    HUFF_TRY(ctx->timed("split_emit", [&] { return dev::launch_split_emit(a, strm); }));
+    HIP_TRY(hipEventRecord(ctx->lut_free, strm));
+    if (bounce) HIP_TRY(hipMemcpyAsync(dst, ctx->d_align.p, total, hipMemcpyDeviceToDevice, strm));
+    return Status::ok();
+}
+
 Status decode_indexless_dev(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_bytes, uint64_t valid_bits,
                             const huff_tree* t, DevBuf& out, uint64_t* nsym, uint8_t* d_user, size_t user_cap,
                             unsigned long long* d_end) {
@@ -1415,6 +1535,11 @@ Status decode_indexless_dev(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_
         bool done = false;
         HUFF_TRY(decode_indexless_single(ctx, d_comp, comp_bytes, valid_bits, t, dt, out, nsym, d_user, user_cap, d_end,
                                          &done));
+        if (done) return Status::ok();
+    }
+    if (!decode_check_mode() && !split_disabled()) {
+        bool done = false;
+        HUFF_TRY(decode_split(ctx, d_comp, comp_bytes, valid_bits, t, dt, out, nsym, d_user, user_cap, d_end, &done));
         if (done) return Status::ok();
     }
     IndexlessSync& st = ctx->indexless_ws();

@@ -67,6 +67,8 @@ void build_multi_table(const HuffTree& t, uint32_t mbits, DecTables& out);
 
 // HUFF_DISABLE_FIXED8=1 forces the general kernels even for all-8-bit codes
 bool fixed8_disabled();
+// HUFF_SPLIT=0: index-free byte decode through the older sample + mark path
+bool split_disabled();
 // HUFF_DEC_VARIANT=11 -> k_decode_fixed's self-checking build (mode 1; else 0)
 uint32_t decode_check_mode();
 
@@ -256,6 +258,7 @@ struct IndexlessSync {
     const DecTables* dt = nullptr;  // tables of the tree, uploaded to ctx->d_lut
     DevBuf s, x0, c, off, flag, tsum, samp, tm, dl, fixlist;
     DevBuf ifd;  // the single-pass decoder's flags, ticket, total and look-back words
+    DevBuf rec, xd, btot, boff;  // the split decoder's lane records, exits, block letters and offsets
     dev::IndexlessArgs a{};
     uint64_t total = 0;
 };

@@ -151,7 +151,14 @@ Status huff_wenc::upload_dec(const huff_wtree* t) {
 Status huff_wenc::decode(const huff_wtree* t, const uint8_t* d_comp, uint64_t comp_bytes, uint8_t* d_out,
                          const uint64_t* sub_abs, bool skip_packed) {
     HUFF_TRY(ctx->activate());
-    if (reinterpret_cast<uintptr_t>(d_comp) & 3) return Status::err(HUFF_E_INVALID_ARG, "stream must be 4-byte aligned");
+    if (reinterpret_cast<uintptr_t>(d_comp) & 15) {
+        // the decoders read the stream in dwords and 16-B pieces: a stream at
+        // any other alignment (packed into a tensor view at an odd offset,
+        // which huff_wenc_pack allows) is copied once to an aligned buffer
+        HUFF_TRY(ctx->d_comp_align.ensure(comp_bytes + 64));
+        HIP_TRY(hipMemcpyAsync(ctx->d_comp_align.p, d_comp, comp_bytes, hipMemcpyDeviceToDevice, ctx->stream));
+        d_comp = static_cast<const uint8_t*>(ctx->d_comp_align.p);
+    }
     HUFF_TRY(upload_dec(t));
     huff::dev::WideDecArgs a{};
     a.comp = d_comp;
@@ -233,16 +240,16 @@ Status wweights_map_host(huff_ctx* ctx, uint32_t width, const uint8_t* letters, 
     a.in = static_cast<const uint8_t*>(ctx->d_in.p);
     a.n = n;
     a.width = width;
-    a.slots = dev::wcount_slots(width, n);
-    DevBuf cnt, klo, khi, state, olo, ohi, oc, misc;
-    HUFF_TRY(cnt.ensure(a.slots * 8));
-    HIP_TRY(hipMemsetAsync(cnt.p, 0, a.slots * 8, s));
-    a.counts = static_cast<unsigned long long*>(cnt.p);
-    auto put = [&](uint64_t lo, uint64_t hi, uint64_t c) {
+    const auto put = [&](uint64_t lo, uint64_t hi, uint64_t c) {
         for (uint32_t j = 0; j < width; ++j) uniq.push_back(static_cast<uint8_t>(j < 8 ? lo >> (8 * j) : hi >> (8 * (j - 8))));
         counts.push_back(c);
     };
+    DevBuf cnt, klo, khi, state, olo, ohi, oc, misc;
     if (width <= 2) {  // direct bins: ascending by construction
+        a.slots = dev::wcount_slots(width, n);
+        HUFF_TRY(cnt.ensure(a.slots * 8));
+        HIP_TRY(hipMemsetAsync(cnt.p, 0, a.slots * 8, s));
+        a.counts = static_cast<unsigned long long*>(cnt.p);
         HUFF_TRY(ctx->timed("wweights", [&] { return dev::wcount_launch(a, s); }));
         std::vector<uint64_t> bins(a.slots);
         HIP_TRY(hipMemcpyAsync(bins.data(), cnt.p, a.slots * 8, hipMemcpyDeviceToHost, s));
@@ -251,31 +258,54 @@ Status wweights_map_host(huff_ctx* ctx, uint32_t width, const uint8_t* letters, 
             if (bins[k]) put(k, 0, bins[k]);
         return Status::ok();
     }
-    const uint64_t cap = std::min<uint64_t>(n, a.slots);
-    HUFF_TRY(klo.ensure(a.slots * 8));
-    HIP_TRY(hipMemsetAsync(klo.p, 0xFF, a.slots * 8, s));
-    a.keys_lo = static_cast<unsigned long long*>(klo.p);
-    if (width == 16) {
-        HUFF_TRY(khi.ensure(a.slots * 8));
-        HUFF_TRY(state.ensure(a.slots * 4));
-        HIP_TRY(hipMemsetAsync(state.p, 0, a.slots * 4, s));
-        HUFF_TRY(ohi.ensure(cap * 8));
-        a.keys_hi = static_cast<unsigned long long*>(khi.p);
-        a.state = static_cast<unsigned int*>(state.p);
-        a.out_hi = static_cast<unsigned long long*>(ohi.p);
+    // the HBM table sized for a guess of the distinct letters (at most 2^19,
+    // 8 MiB of slots for W = 4 / 8) and grown when the kernel reports it too
+    // full: ~16-32 B per slot, so a table for n distinct letters of a 1 GiB
+    // input would be ~12x the input where a few thousand letters are the
+    // common case. The largest size (2 n slots) counts without limits.
+    const uint64_t max_slots = dev::wcount_slots(width, n);
+    a.slots = std::min(max_slots, dev::wcount_slots(width, std::min<uint64_t>(n, 1ull << 19)));
+    HUFF_TRY(misc.ensure(32));
+    uint64_t m[4] = {};  // nout, sent, used, overflow
+    for (;;) {
+        a.unbounded = a.slots >= max_slots ? 1u : 0u;
+        HUFF_TRY(cnt.ensure(a.slots * 8));
+        HIP_TRY(hipMemsetAsync(cnt.p, 0, a.slots * 8, s));
+        a.counts = static_cast<unsigned long long*>(cnt.p);
+        HUFF_TRY(klo.ensure(a.slots * 8));
+        HIP_TRY(hipMemsetAsync(klo.p, 0xFF, a.slots * 8, s));
+        a.keys_lo = static_cast<unsigned long long*>(klo.p);
+        if (width == 16) {
+            HUFF_TRY(khi.ensure(a.slots * 8));
+            HUFF_TRY(state.ensure(a.slots * 4));
+            HIP_TRY(hipMemsetAsync(state.p, 0, a.slots * 4, s));
+            a.keys_hi = static_cast<unsigned long long*>(khi.p);
+            a.state = static_cast<unsigned int*>(state.p);
+        }
+        HIP_TRY(hipMemsetAsync(misc.p, 0, 32, s));
+        a.nout = static_cast<unsigned long long*>(misc.p);
+        a.sent = a.nout + 1;
+        a.used = a.nout + 2;
+        a.overflow = reinterpret_cast<unsigned int*>(a.nout + 3);
+        HUFF_TRY(ctx->timed("wweights", [&] { return dev::wcount_launch(a, s); }));
+        HIP_TRY(hipMemcpyAsync(m, misc.p, 32, hipMemcpyDeviceToHost, s));
+        HUFF_TRY(ctx->sync());
+        if (!(m[3] & 1) || a.unbounded) break;
+        // at least m[2] distinct letters: room for twice as many, or 4x the slots
+        a.slots = std::min(max_slots, std::max(a.slots * 4, dev::wcount_slots(width, 2 * m[2])));
     }
+    // the outputs hold the claimed slots only
+    const uint64_t cap = std::max<uint64_t>(m[2], 1);
     HUFF_TRY(olo.ensure(cap * 8));
     HUFF_TRY(oc.ensure(cap * 8));
-    HUFF_TRY(misc.ensure(16));
-    HIP_TRY(hipMemsetAsync(misc.p, 0, 16, s));
+    if (width == 16) HUFF_TRY(ohi.ensure(cap * 8));
     a.out_lo = static_cast<unsigned long long*>(olo.p);
     a.out_c = static_cast<unsigned long long*>(oc.p);
-    a.nout = static_cast<unsigned long long*>(misc.p);
-    a.sent = a.nout + 1;
-    HUFF_TRY(ctx->timed("wweights", [&] { return dev::wcount_launch(a, s); }));
-    uint64_t m[2] = {};
-    HIP_TRY(hipMemcpyAsync(m, misc.p, 16, hipMemcpyDeviceToHost, s));
+    a.out_hi = width == 16 ? static_cast<unsigned long long*>(ohi.p) : nullptr;
+    HIP_TRY(dev::wextract_launch(a, s));
+    HIP_TRY(hipMemcpyAsync(m, misc.p, 8, hipMemcpyDeviceToHost, s));
     HUFF_TRY(ctx->sync());
+    if (m[0] > cap) return Status::err(HUFF_E_HIP, "wide weights: more used slots than claims");
     std::vector<uint64_t> lo(m[0]), hi(width == 16 ? m[0] : 0), c(m[0]);
     if (m[0]) {
         HIP_TRY(hipMemcpyAsync(lo.data(), olo.p, m[0] * 8, hipMemcpyDeviceToHost, s));
@@ -340,9 +370,12 @@ Status wdecode_indexless_dev(huff_ctx* ctx, const huff_wtree* t, const uint8_t* 
                              uint64_t valid_bits, uint8_t* d_out, size_t cap_letters, uint64_t* n_out) {
     *n_out = 0;
     if (valid_bits == 0) return Status::ok();
-    if (reinterpret_cast<uintptr_t>(d_comp) & 15)
-        return Status::err(HUFF_E_INVALID_ARG, "compressed stream must be 16-byte aligned");
     HUFF_TRY(ctx->activate());
+    if (reinterpret_cast<uintptr_t>(d_comp) & 15) {  // the sync kernels stage 16-B pieces: an aligned copy
+        HUFF_TRY(ctx->d_comp_align.ensure(comp_bytes + 64));
+        HIP_TRY(hipMemcpyAsync(ctx->d_comp_align.p, d_comp, comp_bytes, hipMemcpyDeviceToDevice, ctx->stream));
+        d_comp = static_cast<const uint8_t*>(ctx->d_comp_align.p);
+    }
     // synchronise on the tree's shape (the sync kernels only use code lengths)
     const huff_tree* shape = t->shape_tree();
     const DecTables* dt = nullptr;

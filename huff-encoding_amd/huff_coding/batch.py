@@ -34,6 +34,10 @@ def batch_hist(ctx, data: torch.Tensor, offsets: torch.Tensor) -> torch.Tensor:
     assert data.is_cuda and data.dtype == torch.uint8 and data.is_contiguous()
     assert offsets.is_cuda and offsets.dtype == torch.int64 and offsets.is_contiguous()
     ns = offsets.numel() - 1
+    if ns > 0:  # offsets ascending inside the data (one device reduction, one host read)
+        ok = (offsets[0] >= 0) & (offsets[-1] <= data.numel()) & (offsets[1:] >= offsets[:-1]).all()
+        if not bool(ok.item()):
+            raise ValueError("offsets must ascend from >= 0 to <= data.numel()")
     hist = torch.empty((max(ns, 0), 256), dtype=torch.int64, device=data.device)
     _check(load().huff_batch_hist(ctx.h, C.c_void_p(data.data_ptr()), C.c_void_p(offsets.data_ptr()), ns,
                                   C.c_void_p(hist.data_ptr())))
@@ -46,7 +50,7 @@ class BatchTrees:
     tree_nbits: torch.Tensor  # [S] int32
     codes: torch.Tensor       # [S, 256] int64: code << 8 | len
     max_len: torch.Tensor     # [S] int32
-    status: torch.Tensor      # [S] int32: 0, E_EMPTY_WEIGHTS or E_CODE_TOO_LONG
+    status: torch.Tensor      # [S] int32: 0, E_EMPTY_WEIGHTS, E_CODE_TOO_LONG or E_INVALID_ARG (weights >= 2^54)
 
 
 def batch_trees(ctx, hist: torch.Tensor) -> BatchTrees:
@@ -65,3 +69,4 @@ def batch_trees(ctx, hist: torch.Tensor) -> BatchTrees:
 
 E_EMPTY_WEIGHTS = _lib.E_EMPTY_WEIGHTS
 E_CODE_TOO_LONG = _lib.E_CODE_TOO_LONG
+E_INVALID_ARG = _lib.E_INVALID_ARG

@@ -195,6 +195,19 @@ class NativeComm:
         dist.broadcast_object_list(obj, src=0, group=group)
         return cls(ctx, world, rank, obj[0])
 
+    def world(self):
+        """(world, rank) as RCCL itself reports them (ncclCommCount /
+        ncclCommUserRank through huff_comm_world)"""
+        import ctypes as C
+
+        from ._lib import load
+
+        from . import _check
+
+        w, r = C.c_int(), C.c_int()
+        _check(load().huff_comm_world(self.h, C.byref(w), C.byref(r)))
+        return w.value, r.value
+
     def compress(self, job, d_out: int, out_cap: int):
         """huff_mgpu_compress: (HuffTree, bit_base, bits, owned_bytes); a short
         buffer raises HuffError with .bits_needed / .bit_base"""

@@ -276,17 +276,21 @@ int huff_dev_decompress(huff_ctx* ctx, const huff_tree* t, const uint8_t* d_comp
  * launch each, synchronous):
  *  huff_batch_hist:  d_hist[s][256] = the byte weights (ByteWeights::
  *                    from_bytes, weights.rs:265-279) of stream s =
- *                    d_in[d_offsets[s], d_offsets[s + 1]).
+ *                    d_in[d_offsets[s], d_offsets[s + 1]) (any length; an
+ *                    offset pair with d_offsets[s + 1] < d_offsets[s] counts
+ *                    as an empty stream).
  *  huff_batch_trees: HuffTree::from_weights of each d_hist[s] (tree_inner.rs:
  *                    281-320, with the reference's exact BinaryHeap tie order)
  *                    -> d_tree_bits + s * tree_stride: as_bin (tree_inner.rs:
  *                    632-663), MSB first, d_tree_nbits[s] bits; d_codes[s][l] =
  *                    code << 8 | len of letter l (0: no code); d_max_len[s];
  *                    d_status[s] = HUFF_OK, HUFF_E_EMPTY_WEIGHTS (all weights
- *                    zero: "provided empty weights") or HUFF_E_CODE_TOO_LONG (a
+ *                    zero: "provided empty weights"), HUFF_E_CODE_TOO_LONG (a
  *                    code longer than 56 bits: its d_codes entry is 0; the
- *                    tree bits are complete). tree_stride >=
- *                    HUFF_TREE_BITS_MAX_BYTES; per-stream weights < 2^54. */
+ *                    tree bits are complete) or HUFF_E_INVALID_ARG (the
+ *                    stream's weights sum to 2^54 or more, counting the byte-0
+ *                    re-yield: no tree, 0 tree bits). tree_stride >=
+ *                    HUFF_TREE_BITS_MAX_BYTES. */
 #define HUFF_TREE_BITS_MAX_BYTES 322
 int huff_batch_hist(huff_ctx* ctx, const uint8_t* d_in, const uint64_t* d_offsets, uint32_t nstreams,
                     uint64_t* d_hist);

@@ -93,10 +93,13 @@ void huff_wenc_free(huff_wenc* e);
 int huff_wenc_bits(huff_wenc* e, const huff_wtree* t, uint64_t* total_bits);
 /* pass B into d_out (any alignment, out_cap >= ceil(bits / 8)) */
 int huff_wenc_pack(huff_wenc* e, const huff_wtree* t, uint8_t* d_out, size_t out_cap, uint64_t* total_bits);
-/* restart-index decode of this job's pack output into d_out (n * width bytes) */
+/* restart-index decode of this job's pack output into d_out (n * width bytes);
+ * d_comp at any alignment (a stream not 16-B aligned is first copied to an
+ * aligned buffer of the context) */
 int huff_wenc_decode(huff_wenc* e, const huff_wtree* t, const uint8_t* d_comp, uint8_t* d_out);
-/* self-synchronising decode of a device stream (no index): returns the count
- * in *n_out; d_out NULL = count only */
+/* self-synchronising decode of a device stream (no index), d_comp at any
+ * alignment (as huff_wenc_decode): returns the count in *n_out; d_out NULL =
+ * count only */
 int huff_dev_wdecompress(huff_ctx* ctx, const huff_wtree* t, const uint8_t* d_comp, size_t comp_bytes,
                          uint8_t padding, void* d_out, size_t out_cap_letters, size_t* n_out);
 

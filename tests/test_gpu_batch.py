@@ -114,3 +114,38 @@ def test_batch_trees_deep_and_quirks(H, O, ctx):
         assert status[s] == (batch.E_CODE_TOO_LONG if deep else 0)
         got = {l: format(int(v) >> 8, "0%db" % (int(v) & 0xFF)) for l, v in enumerate(codes[s]) if v}
         assert got == {l: c for l, c in oc.items() if len(c) <= 56}, s
+
+
+def test_batch_limits(H, O, ctx):
+    """weights summing to 2^54 or more (the heap keys hold weight << 10) get
+    HUFF_E_INVALID_ARG, the byte-0 re-yield counted; 2^54 - 1 still builds;
+    descending offsets are refused before the launch"""
+    import torch
+
+    from huff_coding import batch
+
+    rows = []
+    r = np.zeros(256, np.int64)
+    r[[3, 4]] = [1 << 53, 1 << 53]
+    rows.append(r)  # exactly 2^54
+    r = np.zeros(256, np.int64)
+    r[[3, 4]] = [(1 << 53) - 1, 1 << 53]
+    rows.append(r)  # 2^54 - 1: fine
+    r = np.zeros(256, np.int64)
+    r[[0, 5]] = [(1 << 53), (1 << 52)]
+    rows.append(r)  # byte 0 re-yielded: 2^53 + 2^52 + 2^53 >= 2^54
+    r = np.zeros(256, np.int64)
+    r[7] = 1 << 60
+    rows.append(r)  # one heavy letter
+    hist = torch.from_numpy(np.stack(rows)).cuda()
+    t = batch.batch_trees(ctx, hist)
+    torch.cuda.synchronize()
+    st = t.status.cpu().numpy()
+    assert list(st) == [batch.E_INVALID_ARG, 0, batch.E_INVALID_ARG, batch.E_INVALID_ARG]
+    ot = O.Tree.from_weights(O.weights_from_array(rows[1].astype(np.uint64)))
+    assert t.tree_nbits.cpu().numpy()[1] == len(ot.as_bin())
+    data = torch.zeros(100, dtype=torch.uint8, device="cuda")
+    with pytest.raises(ValueError):
+        batch.batch_hist(ctx, data, torch.tensor([0, 50, 40], dtype=torch.int64, device="cuda"))
+    with pytest.raises(ValueError):
+        batch.batch_hist(ctx, data, torch.tensor([0, 101], dtype=torch.int64, device="cuda"))

@@ -826,6 +826,7 @@ def test_native_comm_world1_mgpu_compress(H, O, ctx, kind):
     x = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
     D.generate(ctx, kind, 0x5EED0002, x.data_ptr(), n, cdf=D.zipf_cdf(1.2) if kind == "zipf" else None)
     comm = mgpu.NativeComm(ctx, 1, 0, mgpu.NativeComm.unique_id())
+    assert comm.world() == (1, 0)  # as RCCL reports it (ncclCommCount / ncclCommUserRank)
     job = H.EncodeJob(ctx, x.data_ptr(), n)
     out = torch.zeros(n + 128, dtype=torch.uint8, device="cuda")
     tree, base, bits, owned = comm.compress(job, out.data_ptr(), out.numel())
@@ -850,4 +851,9 @@ def test_native_comm_world1_mgpu_compress(H, O, ctx, kind):
     with pytest.raises(H.HuffError) as ei:
         comm.compress(job, small.data_ptr(), 64)
     assert ei.value.bits_needed == bits
+    # a failing rank (misaligned output) still joins the collective and
+    # reports its own error
+    with pytest.raises(H.HuffError) as ei:
+        comm.compress(job, out.data_ptr() + 3, out.numel() - 3)
+    assert "aligned" in str(ei.value)
     comm.close()

@@ -1,0 +1,145 @@
+"""The split index-free decoder (isplit.hip) against the oracle.
+
+Streams are written by the CPU restatement (oracle/, comp.rs:419-451) with no
+restart index, as the reference writes every CompressData and .hff payload,
+and decoded on the device through huff_dev_decompress (comp.rs:487-519): the
+default path for codes <= 32 bits (k_sync -> k_fix_rec -> scan -> k_emit).
+The cases cover its paths: lanes merging with their speculative walk, codes
+longer than the 12-bit table, 1-8 lanes per segment, lanes past 64 letters,
+blocks past the LDS image, slowly resynchronising codes (the fix-up rounds),
+tiny and ragged streams, misaligned outputs, the count-only query, garbage
+payloads, and equality with the older sample + mark path (HUFF_SPLIT=0).
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def roundtrip(H, O, ctx, data, misalign=0):
+    """oracle-encode `data`, decode it on the device, compare byte for byte
+    and check that nothing past the letters was written"""
+    import torch
+    from huff_coding import device as D
+
+    t = O.Tree.from_weights(O.weights_from_bytes(data))
+    code, ln = t.code_table()
+    host = np.frombuffer(data, np.uint8)
+    comp, bits = O.fast_encode(host, code, ln, threads=8)
+    pad = (8 - bits % 8) % 8
+    tree = H.HuffTree.try_from_bin(t.as_bin())
+    dc = torch.zeros(comp.size + 64, dtype=torch.uint8, device="cuda")
+    if comp.size:
+        dc[: comp.size] = torch.from_numpy(comp).cuda()
+    torch.cuda.synchronize()
+    n = len(data)
+    assert D.decompress_dev(ctx, tree, dc.data_ptr(), comp.size, pad, 0, 0) == n
+    out = torch.full((n + 80,), 0xAB, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()  # the library runs on its own stream
+    got = D.decompress_dev(ctx, tree, dc.data_ptr() if comp.size else 0, comp.size, pad,
+                           out.data_ptr() + misalign, n + 16)
+    torch.cuda.synchronize()
+    assert got == n
+    res = out.cpu().numpy()
+    bad = np.nonzero(res[misalign: misalign + n] != host)[0]
+    assert bad.size == 0, (bad[:10], bad.size)
+    assert (res[misalign + n:] == 0xAB).all(), "wrote past the letters"
+    return comp, pad, tree
+
+
+def index_free_cases(O, rng):
+    yield "zipf-16MiB", O.gen_zipf(0x5EED0002, (1 << 24) + 12345).tobytes()
+    yield "text-16MiB", O.gen_text(0x5EED0005, (1 << 24) + 999).tobytes()
+    yield "uniform40", rng.integers(0, 40, 3_000_001, dtype=np.uint8).tobytes()
+    yield "geometric-long", np.minimum(rng.geometric(0.45, 2_000_003) - 1, 255).astype(np.uint8).tobytes()
+    x = np.minimum(rng.geometric(0.45, 1_000_000) - 1, 255).astype(np.uint8)
+    x[rng.integers(0, x.size, 3000)] = rng.integers(0, 256, 3000, dtype=np.uint8)  # codes > 12 bits
+    yield "long-codes", x.tobytes()
+    skew = np.where(rng.random(2_000_000) < 0.95, 0, rng.integers(1, 200, 2_000_000)).astype(np.uint8)
+    yield "skewed-95", skew.tobytes()  # lanes past 64 letters, blocks past the image
+    skew = np.where(rng.random(1_500_000) < 0.995, 7, rng.integers(0, 3, 1_500_000)).astype(np.uint8)
+    yield "skewed-99.5", skew.tobytes()  # ~1 bit per letter: ~120 letters per lane at R = 8
+    runs = np.repeat(rng.integers(0, 6, 40_000, dtype=np.uint8), rng.integers(1, 300, 40_000))
+    yield "runs", runs.tobytes()
+    for n in (1, 2, 3, 63, 64, 65, 255, 256, 1000, 4095, 65537):
+        yield f"small-{n}", rng.integers(0, 7, n, dtype=np.uint8).tobytes()
+    yield "two-letters", rng.integers(0, 2, 100_001, dtype=np.uint8).tobytes()
+    # near-fixed lengths {7, 8} (160 letters, equal weights) and {5, 6}:
+    # resynchronise slowly, so many lanes leave their segment unmerged
+    yield "lengths-7-8", rng.integers(0, 160, 2_000_001, dtype=np.uint8).tobytes()
+    yield "lengths-5-6", rng.integers(0, 40, 2_000_001, dtype=np.uint8).tobytes()
+    # equal counts of 8 / 64 letters: all codes 3 / 6 bits (gcd 3: S = 1023 - ...)
+    for k in (8, 64):
+        yield f"fixed-{k}", rng.permutation(np.tile(np.arange(1, k + 1, dtype=np.uint8), 600_000 // k)).tobytes()
+    # codes up to 23 bits (Fibonacci-like counts)
+    fib = [1, 1]
+    while len(fib) < 24:
+        fib.append(fib[-1] + fib[-2])
+    letters = np.repeat(np.arange(24, dtype=np.uint8), np.array(fib) * 3)
+    yield "fibonacci-24", rng.permutation(letters).tobytes()
+
+
+@pytest.fixture(scope="module")
+def cases(O):
+    return list(index_free_cases(O, np.random.default_rng(2024)))
+
+
+def test_split_matches_oracle(H, O, ctx, cases):
+    for name, data in cases:
+        roundtrip(H, O, ctx, data)
+
+
+@pytest.mark.parametrize("l2", [True, False], ids=["l2-lds", "l2-global"])
+def test_split_codes_past_table(H, O, ctx, l2, monkeypatch):
+    """codes of 13-23 bits: the sync pass's level-2 length table in LDS, and
+    with HUFF_NO_L2=1 the global multi-level table"""
+    if not l2:
+        monkeypatch.setenv("HUFF_NO_L2", "1")
+    rng = np.random.default_rng(29)
+    for p, n in ((0.08, 2_000_000), (0.2, 700_001), (0.35, 65536 * 5 + 3)):
+        roundtrip(H, O, ctx, np.minimum(rng.geometric(p, n), 255).astype(np.uint8).tobytes())
+
+
+def test_split_misaligned_output(H, O, ctx, cases):
+    for name, data in cases[:4]:
+        roundtrip(H, O, ctx, data[:1_000_003], misalign=3)
+
+
+def test_split_equals_older_path(H, O, ctx, monkeypatch):
+    """the same stream through the split path and HUFF_SPLIT=0"""
+    import torch
+    from huff_coding import device as D
+
+    data = O.gen_zipf(0x5EED0002, 1 << 23).tobytes()
+    comp, pad, tree = roundtrip(H, O, ctx, data)
+    dc = torch.from_numpy(np.concatenate([comp, np.zeros(64, np.uint8)])).cuda()
+    outs = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("HUFF_SPLIT", flag)
+        out = torch.empty(len(data) + 64, dtype=torch.uint8, device="cuda")
+        assert D.decompress_dev(ctx, tree, dc.data_ptr(), comp.size, pad, out.data_ptr(), len(data) + 64) == len(data)
+        outs.append(out[: len(data)].clone())
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+
+
+def test_split_garbage_payloads(H, O, ctx):
+    """random payloads under fixed trees: whatever the bits, the letters and
+    the dropped final code match the reference walk"""
+    import torch
+    from huff_coding import device as D
+
+    rng = np.random.default_rng(77)
+    trees = [O.Tree.from_weights(O.weights_from_bytes(b"abracadabra alakazam")),
+             O.Tree.from_weights(O.weights_from_bytes(O.gen_zipf(0x5EED0002, 1 << 16).tobytes()))]
+    for t in trees:
+        tree = H.HuffTree.try_from_bin(t.as_bin())
+        for n in (1, 2, 7, 300, 5000, 123_457, 1_000_003):
+            payload = rng.integers(0, 256, n, dtype=np.uint8)
+            for pad in (0, 3, 7):
+                want = O.decompress(payload.tobytes(), pad, t)
+                dc = torch.from_numpy(np.concatenate([payload, np.zeros(64, np.uint8)])).cuda()
+                out = torch.empty(len(want) + 64, dtype=torch.uint8, device="cuda")
+                got = D.decompress_dev(ctx, tree, dc.data_ptr(), n, pad, out.data_ptr(), len(want) + 64)
+                torch.cuda.synchronize()
+                assert got == len(want) and out[:got].cpu().numpy().tobytes() == want, (n, pad)

@@ -243,6 +243,30 @@ def test_large_alphabet_table_in_hbm(W, O, ctx, dtype, k):
     assert np.array_equal(W.decompress(cd, ctx), letters)
 
 
+@pytest.mark.parametrize("dtype", [np.uint32, np.uint64, "u128"])
+def test_weights_map_table_growth(W, ctx, dtype):
+    """build_weights_map's HBM table starts at 2^20 slots (claims up to 3/4)
+    and grows when the kernel reports it full: 1.2 M distinct letters force
+    one growth; a large input over 10 letters never does (the round-3 table
+    took 2 n slots whatever the alphabet). Counts equal numpy's, ascending."""
+    rng = np.random.default_rng(41)
+    for distinct, n in ((1_200_000, 3_000_001), (10, 8_000_001)):
+        if dtype == "u128":
+            keys = np.unique(rng.integers(0, 2**63, (distinct * 2, 2), dtype=np.uint64), axis=0)[:distinct]
+            pairs = np.ascontiguousarray(keys[rng.integers(0, keys.shape[0], n)])  # (lo, hi) per letter
+            wmap = W.build_weights_map(pairs.view(np.dtype("V16")).reshape(-1), ctx)
+            u, c = np.unique(pairs[:, ::-1], axis=0, return_counts=True)  # ascending (hi, lo)
+            want_keys = [int(lo) | (int(hi) << 64) for hi, lo in u]
+        else:
+            alphabet = np.unique(rng.integers(0, np.iinfo(dtype).max, distinct * 2, dtype=dtype))[:distinct]
+            letters = alphabet[rng.integers(0, alphabet.size, n)]
+            wmap = W.build_weights_map(letters, ctx)
+            u, c = np.unique(letters, return_counts=True)
+            want_keys = [int(x) for x in u]
+        assert list(wmap.keys()) == want_keys
+        assert list(wmap.values()) == [int(x) for x in c]
+
+
 @pytest.mark.parametrize("dtype", [np.uint8, np.uint16, np.int32, np.int64])
 def test_device_pack_any_alignment(W, O, ctx, dtype):
     """pass 2 into an output at every offset mod 16: the bytes equal the
@@ -276,6 +300,19 @@ def test_device_pack_any_alignment(W, O, ctx, dtype):
         got = dec.cpu().numpy()
         assert got[off:off + n * w].tobytes() == letters.tobytes(), off
         assert (got[:off] == 0xCD).all() and (got[off + n * w:] == 0xCD).all(), off
+    # a stream packed at an odd offset decodes in place (the runtime copies a
+    # misaligned stream to an aligned buffer): restart index and index-free
+    for off in (1, 3, 13):
+        buf = torch.zeros(nb + 64, dtype=torch.uint8, device="cuda")
+        job.pack(t, buf.data_ptr() + off, nb)
+        dec = torch.empty(n * w + 64, dtype=torch.uint8, device="cuda")
+        job.decode(t, buf.data_ptr() + off, dec.data_ptr())
+        torch.cuda.synchronize()
+        assert dec[: n * w].cpu().numpy().tobytes() == letters.tobytes(), off
+        dec.zero_()
+        got_n = W.decompress_dev(ctx, t, buf.data_ptr() + off, nb, opad, dec.data_ptr(), n)
+        torch.cuda.synchronize()
+        assert got_n == n and dec[: n * w].cpu().numpy().tobytes() == letters.tobytes(), off
 
 
 def test_device_job_large(W, ctx):
