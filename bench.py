@@ -200,11 +200,11 @@ class Setup:
                     "source": "torch.distributed gloo group (no RCCL: rehearsal)"}
         try:
             if self.comm is not None:
-                w, r = self.comm.world()
+                w, r = self.comm.observed_world()
             elif self.world == 1:
                 c = mgpu.NativeComm(self.ctx, 1, 0, mgpu.NativeComm.unique_id())
                 try:
-                    w, r = c.world()
+                    w, r = c.observed_world()
                 finally:
                     c.close()
             else:

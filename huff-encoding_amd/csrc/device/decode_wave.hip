@@ -532,10 +532,15 @@ hipError_t launch_decode_fixed(const DecodeArgs& a, hipStream_t s) {
     // production: one task per wave (a one-shot grid, as the byte map's): the
     // dispatcher refills the CUs as waves finish — same-box A/B against the
     // resident persistent grid Zipf 0.506 -> 0.501 ms, text 0.433 -> 0.423,
-    // index-free text 1.18 -> 1.14 ms. HUFF_DEC_ONESHOT=0 restores the
-    // persistent grid; the check build keeps it.
+    // index-free text 1.18 -> 1.14 ms. The check build keeps the persistent
+    // grid (and so does a HUFF_DIAG build run with HUFF_DEC_ONESHOT=0).
+#ifdef HUFF_DIAG
     const char* o = std::getenv("HUFF_DEC_ONESHOT");
-    if (!a.check_mode && !(o && *o == '0')) cap = want;
+    const bool oneshot = !(o && *o == '0');
+#else
+    constexpr bool oneshot = true;
+#endif
+    if (!a.check_mode && oneshot) cap = want;
     const uint32_t grid = static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>(want, cap)));
     hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), lds, s, a);
     return hipGetLastError();

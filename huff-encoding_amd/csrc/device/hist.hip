@@ -117,43 +117,49 @@ __global__ __launch_bounds__(kThreads) void k_hist(const uint8_t* __restrict__ b
 // issued before the first count, the chunk's row is written, and the global
 // weights are summed from the rows afterwards (k_rows_sum) instead of with
 // per-workgroup atomics.
-template <int LOGC>
-__global__ __launch_bounds__(kThreads) void k_hist1(const uint8_t* __restrict__ base, uint64_t lo, uint64_t hi,
-                                                    uint32_t* __restrict__ chunk_hist,
-                                                    unsigned long long* __restrict__ gw) {
+// HUFF_HIST_THREADS: the workgroup's threads (256: 16 loads of 16 B per
+// lane; 512: 8 per lane with twice the waves sharing one LDS histogram)
+#ifndef HUFF_HIST_THREADS
+#define HUFF_HIST_THREADS 256
+#endif
+template <int LOGC, int T = HUFF_HIST_THREADS>
+__global__ __launch_bounds__(T) void k_hist1(const uint8_t* __restrict__ base, uint64_t lo, uint64_t hi,
+                                             uint32_t* __restrict__ chunk_hist,
+                                             unsigned long long* __restrict__ gw) {
     constexpr uint32_t C = 1u << LOGC;  // LDS copies of the histogram
+    constexpr int NL = kChunk / 16 / T;  // 16-B loads per lane
     if (blockIdx.x == 0)  // k_rows_sum (next on the stream) accumulates into gw
-        for (uint32_t i = threadIdx.x; i < kHistCopies * 256; i += kThreads) gw[i] = 0;
+        for (uint32_t i = threadIdx.x; i < kHistCopies * 256; i += T) gw[i] = 0;
     __shared__ __attribute__((aligned(16))) uint32_t h[256 * C];
     const uint32_t t = threadIdx.x;
     const uint32_t lane_c = t & (C - 1);
     const uint32_t c = blockIdx.x;
     const uint64_t cbeg = static_cast<uint64_t>(c) * kChunk;
     const bool full = cbeg >= lo && cbeg + kChunk <= hi;
-    uint4 v[16];
+    uint4 v[NL];
     if (full) {
         const uint4* p = reinterpret_cast<const uint4*>(base + cbeg) + t;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) v[r] = ld_nt(p + r * kThreads);
+        for (int r = 0; r < NL; ++r) v[r] = ld_nt(p + r * T);
     }
     __builtin_amdgcn_sched_barrier(0);  // loads first, no use of v[] hoisted above them
     uint4* h4 = reinterpret_cast<uint4*>(h);
 #pragma unroll
-    for (uint32_t i = 0; i < 256 * C / 4 / kThreads; ++i) h4[t + i * kThreads] = make_uint4(0, 0, 0, 0);
+    for (uint32_t i = 0; i < 256 * C / 4 / T; ++i) h4[t + i * T] = make_uint4(0, 0, 0, 0);
     // a bare barrier (no fence): the LDS zeroing is complete, the loads stay in flight
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0), vmcnt/expcnt untouched
     __builtin_amdgcn_s_barrier();
     if (full) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
+        for (int r = 0; r < NL; ++r) {
             count_word<LOGC>(h, v[r].x, lane_c);
             count_word<LOGC>(h, v[r].y, lane_c);
             count_word<LOGC>(h, v[r].z, lane_c);
             count_word<LOGC>(h, v[r].w, lane_c);
         }
     } else {
-        for (int r = 0; r < 16; ++r) {
-            const uint64_t off = cbeg + static_cast<uint64_t>(r) * kRound + t * 16;
+        for (int r = 0; r < NL; ++r) {
+            const uint64_t off = cbeg + static_cast<uint64_t>(r) * (16 * T) + t * 16;
             if (off + 16 <= lo || off >= hi) continue;
             uint4 x;
             if (off + 16 <= hi) {
@@ -167,10 +173,12 @@ __global__ __launch_bounds__(kThreads) void k_hist1(const uint8_t* __restrict__ 
         }
     }
     __syncthreads();
-    uint32_t s = 0;
+    if (t < 256) {
+        uint32_t s = 0;
 #pragma unroll 8
-    for (uint32_t j = 0; j < C; ++j) s += h[(t << LOGC) | ((j + t) & (C - 1))];
-    chunk_hist[static_cast<uint64_t>(c) * 256 + t] = s;
+        for (uint32_t j = 0; j < C; ++j) s += h[(t << LOGC) | ((j + t) & (C - 1))];
+        chunk_hist[static_cast<uint64_t>(c) * 256 + t] = s;
+    }
 }
 
 // gw[copy][b] += sum over a stripe of chunks of chunk_hist[c][b]
@@ -354,7 +362,7 @@ hipError_t launch_hist(const uint8_t* base, uint64_t lo, uint64_t hi, uint32_t n
     if (chunk_hist) {  // per-chunk rows wanted: one-shot grid, then the row sum
         // 32 copies: 16 measured equal on uniform bytes and 20 % slower on
         // Zipf (same-address conflicts between lanes l and l + 16)
-        hipLaunchKernelGGL(k_hist1<HUFF_HIST_LOGC>, dim3(nchunks), dim3(kThreads), 0, s, base, lo, hi, chunk_hist, gw);
+        hipLaunchKernelGGL(k_hist1<HUFF_HIST_LOGC>, dim3(nchunks), dim3(HUFF_HIST_THREADS), 0, s, base, lo, hi, chunk_hist, gw);
         const uint32_t g = nchunks < 512 ? nchunks : 512;
         hipLaunchKernelGGL(k_rows_sum, dim3(g), dim3(256), 0, s, chunk_hist, nchunks, gw);
         if (done.host) hipLaunchKernelGGL(k_hist_publish, dim3(1), dim3(256), 0, s, gw, done.host, done.tag);

@@ -261,9 +261,11 @@ __device__ __forceinline__ void samp_pick(const uint32_t (&sv)[kSampMax], uint32
 template <bool SLOW>
 __global__ __launch_bounds__(kThreads) void k_spec_lds(IndexlessArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    const uint16_t* stab = load_stab(a, lds);
-    const uint16_t* wtab = a.wtab ? stab : nullptr;  // one table serves single and multi-code steps
+    TabLoad tl;
+    issue_tables(a, tl);
     const Staged st = with_l2(stage_block(a, lds + tables_words(a)), a, lds);
+    const uint16_t* stab = store_tables(a, tl, lds);
+    const uint16_t* wtab = a.wtab ? stab : nullptr;  // one table serves single and multi-code steps
     __syncthreads();
     const uint64_t i0 = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
     const bool live = i0 < a.nseg;  // no early return: the fix-up below has a barrier
@@ -441,8 +443,10 @@ template <bool SLOW>
 __global__ __launch_bounds__(kThreads) void k_mark_lds(IndexlessArgs a, const uint64_t* __restrict__ off,
                                                        uint64_t* __restrict__ sub_abs, uint32_t shift) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    const uint16_t* stab = load_stab(a, lds);
+    TabLoad tl;
+    issue_tables(a, tl);
     const Staged st = with_l2(stage_block(a, lds + tables_words(a)), a, lds);
+    const uint16_t* stab = store_tables(a, tl, lds);
     __syncthreads();
     const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
     if (i >= a.nseg) return;

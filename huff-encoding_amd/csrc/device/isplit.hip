@@ -43,6 +43,18 @@ namespace huff::dev {
 
 namespace {
 
+// k_emit's output image: 1 = over the stage (a lane's letters, <= 128, wait
+// in registers until every lane has read its bits; a block with a longer
+// lane writes straight to HBM), 0 = beside it
+#ifndef SPLIT_OVERLAP
+#define SPLIT_OVERLAP 0
+#endif
+// k_sync's multi-code windows: 1 = bits from the cursor position and the
+// code count from summed raw entries (segwalk.hpp multi_chunk_pos)
+#ifndef SPLIT_ESUM
+#define SPLIT_ESUM 0
+#endif
+
 constexpr uint32_t kT = 256;
 constexpr uint32_t kRecD = 10;  // rec: start - theta in bits [0, 10), letters above
 
@@ -74,11 +86,13 @@ __global__ __launch_bounds__(kT) void k_sync(SplitArgs a) {
     __shared__ uint64_t ex_l[kT];
     __shared__ uint32_t bt[kSplitRmax];
     const uint32_t t = threadIdx.x;
-    const uint16_t* stab = load_stab(a, lds);
-    const uint16_t* wtab = a.wtab ? stab : nullptr;  // one table serves single and multi-code steps
+    TabLoad tl;
+    issue_tables(a, tl);
     const uint32_t tw = (tables_words(a) + 3) & ~3u;
     uint32_t* smp = lds + tw;  // [nsamp][kT]: (offset from the segment start) | spec index << 16
     const Staged st = with_l2(stage_block(a, lds + tw + a.nsamp * kT), a, lds);
+    const uint16_t* stab = store_tables(a, tl, lds);
+    const uint16_t* wtab = a.wtab ? stab : nullptr;  // one table serves single and multi-code steps
     if (t < kSplitRmax) bt[t] = 0;
     __syncthreads();
     const uint64_t i0 = static_cast<uint64_t>(blockIdx.x) * kT + t;
@@ -119,7 +133,11 @@ __global__ __launch_bounds__(kT) void k_sync(SplitArgs a) {
         const uint64_t span = static_cast<uint64_t>(kChunkSteps) * (a.max_len > K ? a.max_len : K);
         while (cur + span < end) {
             uint32_t U, N;
+#if SPLIT_ESUM
+            U = multi_chunk_pos<SLOW>(c, N, wtab, stab, K, a.lut, Kg);
+#else
             c.multi_chunk<SLOW>(U, N, wtab, stab, K, a.lut, Kg);
+#endif
             cur += U;
             cnt += N;
             note();
@@ -451,20 +469,27 @@ struct ECur {
 __device__ __forceinline__ void put_run(uint8_t* img, uint32_t F, const uint32_t (&o)[16], uint32_t m) {
     const uint32_t r = F & 3u;
     const uint32_t m0 = F >> 2;
+    const uint32_t il = (m - 1 + r) >> 2;  // the dword holding the last letter (m >= 1)
     uint32_t* img32 = reinterpret_cast<uint32_t*>(img);
+    uint32_t vl = 0;
 #pragma unroll
     for (int i = 0; i <= 16; ++i) {
         const uint32_t hi = i < 16 ? o[i] : 0u, lo = i > 0 ? o[i - 1] : 0u;
         const uint32_t v = r ? __builtin_amdgcn_alignbyte(hi, lo, 4 - r) : hi;
         const int32_t j0 = 4 * i - static_cast<int32_t>(r);  // the letter in the dword's byte 0
-        if (j0 >= 0 && j0 + 4 <= static_cast<int32_t>(m)) {
-            img32[m0 + i] = v;
-        } else if (j0 + 4 > 0 && j0 < static_cast<int32_t>(m)) {
-#pragma unroll
-            for (int s = 0; s < 4; ++s)
-                if (j0 + s >= 0 && j0 + s < static_cast<int32_t>(m)) img[4 * (m0 + i) + s] = static_cast<uint8_t>(v >> (8 * s));
-        }
+        if (j0 >= 0 && j0 + 4 <= static_cast<int32_t>(m)) img32[m0 + i] = v;
+        vl = static_cast<uint32_t>(i) == il ? v : vl;
     }
+    // the partial dwords at both ends, shared with the neighbouring runs: byte
+    // stores of this run's letters only
+    const uint32_t e = (m + r) & 3u;  // letters in the last dword when it is partial
+    if (r) {  // the first dword: bytes r .. 3 (letters 0 .. 3 - r, those below m)
+        const uint32_t v0 = o[0] << (8 * r);
+        const uint32_t hi = il == 0 && e ? e : 4u;
+        for (uint32_t s = r; s < hi; ++s) img[4 * m0 + s] = static_cast<uint8_t>(v0 >> (8 * s));
+    }
+    if (e && (il > 0 || !r))  // the last dword (when not also the first): bytes 0 .. e - 1
+        for (uint32_t s = 0; s < e; ++s) img[4 * (m0 + il) + s] = static_cast<uint8_t>(vl >> (8 * s));
 }
 
 template <bool SLOW>
@@ -477,15 +502,20 @@ __global__ __launch_bounds__(kT) void k_emit(SplitArgs a) {
     const uint32_t tab_bytes = (tab_words * 4 + 15) & ~15u;
     uint16_t* stab = reinterpret_cast<uint16_t*>(smem);
     uint32_t* stage = reinterpret_cast<uint32_t*>(smem + tab_bytes);
-    uint8_t* img = smem + tab_bytes + a.stage_bytes;
+    uint8_t* img = SPLIT_OVERLAP ? smem + tab_bytes : smem + tab_bytes + a.stage_bytes;
     const uint64_t nl = a.nseg << a.lg_r;
     const uint64_t j = static_cast<uint64_t>(blockIdx.x) * kT + t;
     const bool live = j < nl;
+    // every global read of the prologue goes out before the first wait: the
+    // lane record, the block's output offset (and the total, for the end
+    // bit), the table and the stage
     const uint32_t rec = live ? a.rec[j] : 0u;
-    const uint32_t n = rec >> kRecD;
-    const uint64_t start = live ? theta(a, j >> a.lg_r, static_cast<uint32_t>(j & ((1u << a.lg_r) - 1))) +
-                                      (rec & ((1u << kRecD) - 1))
-                                : 0;
+    const uint64_t O = a.boff[blockIdx.x];
+    const uint64_t total = a.end_bit ? a.boff[gridDim.x] : 0;
+    const auto rt = buf_rsrc(a.stab, tab_words * 4);
+    uint4 tv[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) tv[k] = buf_ld16(rt, (t + kT * k) * 16);
     // the block's bits from its first segment's 16-B granule
     const uint64_t byte_lo = (((static_cast<uint64_t>(blockIdx.x) * kT >> a.lg_r) * a.seg_bits) >> 3) & ~15ull;
     {
@@ -504,8 +534,15 @@ __global__ __launch_bounds__(kT) void k_emit(SplitArgs a) {
                     w4[p0 + k * kT] = make_uint4(__builtin_bswap32(v[k].x), __builtin_bswap32(v[k].y),
                                                  __builtin_bswap32(v[k].z), __builtin_bswap32(v[k].w));
         }
-        for (uint32_t k = t; k < tab_words; k += kT) reinterpret_cast<uint32_t*>(stab)[k] = reinterpret_cast<const uint32_t*>(a.stab)[k];
+        uint4* s4 = reinterpret_cast<uint4*>(stab);  // the table (its loads went out first)
+#pragma unroll
+        for (int k = 0; k < 2; ++k)
+            if (t + kT * k < tab_bytes / 16) s4[t + kT * k] = tv[k];
     }
+    const uint32_t n = rec >> kRecD;
+    const uint64_t start = live ? theta(a, j >> a.lg_r, static_cast<uint32_t>(j & ((1u << a.lg_r) - 1))) +
+                                      (rec & ((1u << kRecD) - 1))
+                                : 0;
     // the lanes' output offsets in the block
     const uint32_t inc = wave_scan_incl(n);
     if (lane == 63) wtot[wave] = inc;
@@ -517,15 +554,15 @@ __global__ __launch_bounds__(kT) void k_emit(SplitArgs a) {
         cb += wtot[w];
     }
     const uint32_t off_l = before + inc - n;
-    const uint64_t O = a.boff[blockIdx.x];
-    const uint64_t total = a.boff[gridDim.x];
     // the lane with the stream's last code records the bit after it (the
     // file path's windows continue from there)
     const bool last_code = n && a.end_bit && O + off_l + n == total;
     const uint32_t img0 = static_cast<uint32_t>(O & 15);
     const uint32_t stage_last = a.stage_bytes / 4 - 1;
     const uint32_t rel = static_cast<uint32_t>(start - byte_lo * 8);
-    if (img0 + cb > a.img_bytes) {  // more letters than the image: straight to HBM, byte by byte (rare)
+    // more letters than the image (or, image over the stage, a lane with more
+    // than its registers hold): straight to HBM, byte by byte (rare)
+    if (img0 + cb > a.img_bytes || (SPLIT_OVERLAP && __syncthreads_or(n > 128))) {
         if (n) {
             ECur c;
             c.init(stage, stage_last, rel);
@@ -538,6 +575,31 @@ __global__ __launch_bounds__(kT) void k_emit(SplitArgs a) {
         }
         return;
     }
+#if SPLIT_OVERLAP
+    {
+        uint32_t o0[16], o1[16];
+        ECur c;
+        c.init(stage, stage_last, rel);
+        auto batch = [&](uint32_t (&o)[16], uint32_t m) {
+#pragma unroll
+            for (int s = 0; s < 64; ++s) {
+                if (static_cast<uint32_t>(s) < m) {
+                    if ((s & 1) == 0) c.refill();
+                    const uint32_t e = c.step<SLOW>(stab, K, a.lut, a.lut_bits);
+                    if ((s & 3) == 0) o[s >> 2] = e >> 8;
+                    else o[s >> 2] = __builtin_amdgcn_perm(e, o[s >> 2], (s & 3) == 1 ? 0x0C0C0500u : (s & 3) == 2 ? 0x0C050100u : 0x05020100u);
+                }
+            }
+        };
+        const uint32_t m0 = n < 64 ? n : 64u, m1 = n - m0;
+        if (n) batch(o0, m0);
+        if (m1) batch(o1, m1);
+        if (last_code) *a.end_bit = byte_lo * 8 + c.pos();
+        __syncthreads();  // every lane has read its bits: the image may overwrite the stage
+        if (m0) put_run(img, img0 + off_l, o0, m0);
+        if (m1) put_run(img, img0 + off_l + 64, o1, m1);
+    }
+#else
     if (n) {
         ECur c;
         c.init(stage, stage_last, rel);
@@ -557,6 +619,7 @@ __global__ __launch_bounds__(kT) void k_emit(SplitArgs a) {
         }
         if (last_code) *a.end_bit = byte_lo * 8 + c.pos();
     }
+#endif
     __syncthreads();
     // the image to HBM: 16-B pieces, whole where the block owns all 16 bytes
     const uint64_t gbase = O - img0;
@@ -583,7 +646,7 @@ size_t split_sync_lds_bytes(const SplitArgs& a) {
 
 size_t split_emit_lds_bytes(const SplitArgs& a) {
     const size_t tab = ((((1u << a.stab_bits) + 1) / 2) * 4 + 15) & ~size_t(15);
-    return tab + a.stage_bytes + a.img_bytes;
+    return tab + (SPLIT_OVERLAP ? std::max<size_t>(a.stage_bytes, a.img_bytes) : a.stage_bytes + a.img_bytes);
 }
 
 hipError_t launch_split_sync(const SplitArgs& a, hipStream_t s) {

@@ -210,39 +210,6 @@ hipError_t launch_split_sync(const SplitArgs& a, hipStream_t s);
 hipError_t launch_split_fix(const SplitArgs& a, hipStream_t s);  // round 0 (list), rounds, sweep
 hipError_t launch_split_emit(const SplitArgs& a, hipStream_t s);
 
-// single-pass index-free decode (ifdec.hip)
-constexpr uint32_t kIfdPrefixCap = 32;  // letters a lane's fix-up walk keeps before it gives up (slow lane)
-constexpr uint32_t kIfdStageMax = 4 * 256 * 16;  // a block's staged bytes (4 pieces per thread in flight)
-struct IfdArgs {
-    const uint8_t* comp;          // stream; bit 0 = MSB of comp[0]
-    uint64_t comp_bytes;
-    uint64_t valid_bits;          // B
-    uint32_t seg_bits;            // S (multiple of the gcd of the code lengths)
-    uint64_t nseg;
-    uint32_t nblocks;             // ifd_blocks(nseg) workgroups
-    const uint16_t* stab;         // single-symbol table (k_decode_fixed's)
-    uint32_t stab_bits;
-    const uint32_t* lut;          // multi-level table (codes longer than stab_bits)
-    uint32_t lut_bits;
-    uint32_t max_len;             // <= 32
-    uint32_t cu_count;            // the persistent grid
-    uint8_t* out;                 // 16-B aligned
-    uint64_t out_cap;
-    unsigned long long* status;   // [nblocks] look-back words, zeroed
-    unsigned long long* exits;    // [nblocks] a block's true exit + 1 (for a repair of the next block's anchor)
-    unsigned int* ticket;         // zeroed
-    unsigned int* flags;          // zeroed; 2: out_cap too small, 4: the look-back gave up
-    unsigned long long* total;    // letters
-    unsigned long long* end_bit;  // may be null: the bit after the last complete code
-    unsigned long long* dbg;      // [nblocks][8] phase timestamps (builds with IFD_DBG only; else unused)
-    // LDS layout (ifd_layout)
-    uint32_t stage_off, stage_bytes, qm_off, pf_off, ex_off, cnt_off, misc_off, out_off, out_img;
-};
-IfdArgs ifd_layout(uint32_t stab_bits, uint32_t seg_bits, uint32_t max_len);  // LDS fields only
-uint32_t ifd_blocks(uint64_t nseg);
-size_t ifd_lds_bytes(const IfdArgs& a);
-hipError_t launch_ifd(const IfdArgs& a, hipStream_t s);
-
 constexpr uint32_t kSampBits = 128;
 constexpr uint32_t kSampMax = 8;  // samples kept per segment (nsamp <= kSampMax)
 constexpr uint32_t kNoMerge = 0xFFFFFFFFu;

@@ -160,6 +160,35 @@ struct Cursor {
     }
 };
 
+// kChunkSteps multi-code windows as multi_chunk, with the bits taken from the
+// cursor's position and the code count from a plain sum of the raw walk-table
+// entries: E = sum(first length) + (U << 8) + (N << 12), the first lengths
+// adding up to < 256 (<= 8 x 12 bits: non-slow entries only; a slow step adds
+// its own (len << 8) + (1 << 12)), so N = (E - (U << 8)) >> 12. Two VALU per
+// window fewer than summing the fields. Returns U; N through the reference.
+template <bool SLOW>
+__device__ __forceinline__ uint32_t multi_chunk_pos(Cursor& c, uint32_t& N, const uint16_t* wtab, const uint16_t* stab,
+                                                    uint32_t K, const uint32_t* glut, uint32_t Kg) {
+    const uint32_t p0 = 32 * c.rp - (c.X & 63);
+    uint32_t E = 0;
+#pragma unroll
+    for (int k = 0; k < kChunkSteps; ++k) {
+        if ((k & 1) == 0) c.refill();
+        const uint32_t e = wtab[static_cast<uint32_t>(c.buf >> 32) >> (32 - K)];
+        if (SLOW && (e & kSsSlow)) {
+            E += (c.step<SLOW>(stab, K, glut, Kg) << 8) + (1u << 12);
+        } else {
+            const uint32_t u = (e >> 8) & 15u;
+            c.buf <<= u;
+            c.X -= u;
+            E += e;
+        }
+    }
+    const uint32_t U = 32 * c.rp - (c.X & 63) - p0;
+    N = (E - (U << 8)) >> 12;
+    return U;
+}
+
 // LDS: [single-symbol table][level-2 table][staged input ...]
 template <class A>
 __device__ __forceinline__ uint32_t stab_words(const A& a) {
@@ -169,14 +198,51 @@ template <class A>
 __device__ __forceinline__ uint32_t tables_words(const A& a) {
     return stab_words(a) + a.l2_words;
 }
+// The tables in LDS by 16-B buffer loads, all of a thread's issued at once
+// (issue_tables) and stored after the block's stage loads have been issued
+// too (store_tables), so the table and stage latencies overlap: the loop of
+// 4-B loads and LDS stores this replaces waited out an L2 round trip per
+// iteration, ~8 of them per workgroup before the first code was read.
+// Tables: the walk table when there is one (its low bits are stab's lengths),
+// else stab (<= 8 KiB: 2 pieces per thread), then the level-2 table
+// (<= kL2MaxWords: 6 pieces per thread).
+constexpr uint32_t kTabPieces = 2, kL2Pieces = 6;
+constexpr uint32_t kL2MaxWords = 4 * 256 * kL2Pieces;
+struct TabLoad {
+    uint4 t[kTabPieces];
+    uint4 l[kL2Pieces];
+};
+template <class A>
+__device__ __forceinline__ void issue_tables(const A& a, TabLoad& tl) {
+    const uint32_t words = ((1u << a.stab_bits) + 1) / 2;
+    const auto r1 = buf_rsrc(a.wtab ? a.wtab : a.stab, words * 4);
+#pragma unroll
+    for (uint32_t k = 0; k < kTabPieces; ++k) tl.t[k] = buf_ld16(r1, (threadIdx.x + 256 * k) * 16);
+    if (a.l2_words) {
+        const auto r2 = buf_rsrc(a.l2, a.l2_words * 4);
+#pragma unroll
+        for (uint32_t k = 0; k < kL2Pieces; ++k) tl.l[k] = buf_ld16(r2, (threadIdx.x + 256 * k) * 16);
+    }
+}
+template <class A>
+__device__ __forceinline__ const uint16_t* store_tables(const A& a, const TabLoad& tl, uint32_t* lds) {
+    const uint32_t sp = stab_words(a) / 4, lp = (a.l2_words + 3) / 4;
+    uint4* l4 = reinterpret_cast<uint4*>(lds);
+#pragma unroll
+    for (uint32_t k = 0; k < kTabPieces; ++k)
+        if (threadIdx.x + 256 * k < sp) l4[threadIdx.x + 256 * k] = tl.t[k];
+    if (a.l2_words) {
+#pragma unroll
+        for (uint32_t k = 0; k < kL2Pieces; ++k)
+            if (threadIdx.x + 256 * k < lp) l4[sp + threadIdx.x + 256 * k] = tl.l[k];
+    }
+    return reinterpret_cast<const uint16_t*>(lds);
+}
 template <class A>
 __device__ __forceinline__ const uint16_t* load_stab(const A& a, uint32_t* lds) {
-    // the walk table when there is one (its low bits are stab's lengths), else stab
-    const uint32_t words = ((1u << a.stab_bits) + 1) / 2;
-    const uint32_t* src = reinterpret_cast<const uint32_t*>(a.wtab ? a.wtab : a.stab);
-    for (uint32_t i = threadIdx.x; i < words; i += blockDim.x) lds[i] = src[i];
-    for (uint32_t i = threadIdx.x; i < a.l2_words; i += blockDim.x) lds[stab_words(a) + i] = a.l2[i];
-    return reinterpret_cast<const uint16_t*>(lds);
+    TabLoad tl;
+    issue_tables(a, tl);
+    return store_tables(a, tl, lds);
 }
 template <class A>
 __device__ __forceinline__ Staged with_l2(Staged st, const A& a, const uint32_t* lds) {

@@ -52,60 +52,6 @@ huff::Status huff_tree::dec_tables(const huff::DecTables** out) const {
     return huff::Status::ok();
 }
 
-const std::vector<uint32_t>& huff_tree::sync_sample() const {
-    std::lock_guard<std::mutex> g(m);
-    if (!sync.empty()) return sync;
-    constexpr uint32_t kBits = 1u << 17, kTrials = 2048;
-    const auto& nodes = t.nodes();
-    if (t.root_is_leaf()) {  // every bit is a code: every offset is a boundary
-        sync.assign(kTrials, 0);
-        return sync;
-    }
-    uint64_t x = 0x9E3779B97F4A7C15ull ^ id;  // xorshift64: deterministic per tree
-    auto next = [&x]() {
-        x ^= x << 13;
-        x ^= x >> 7;
-        x ^= x << 17;
-        return x;
-    };
-    std::vector<uint8_t> bit(kBits), bound(kBits + 1, 0);
-    for (uint32_t i = 0; i < kBits; i += 64) {
-        const uint64_t r = next();
-        for (uint32_t j = 0; j < 64; ++j) bit[i + j] = static_cast<uint8_t>((r >> j) & 1u);
-    }
-    // one code from bit q: its length, or 0 when it runs off the string
-    auto code_len = [&](uint32_t q) -> uint32_t {
-        int32_t n = t.root();
-        for (uint32_t len = 1; q + len <= kBits; ++len) {
-            n = bit[q + len - 1] ? nodes[n].right : nodes[n].left;
-            if (nodes[n].is_leaf) return len;
-        }
-        return 0;
-    };
-    for (uint32_t q = 0;;) {
-        bound[q] = 1;
-        const uint32_t l = code_len(q);
-        if (!l) break;
-        q += l;
-    }
-    sync.reserve(kTrials);
-    for (uint32_t i = 0; i < kTrials; ++i) {
-        const uint32_t p = static_cast<uint32_t>(next() % (kBits / 2));
-        uint32_t q = p;
-        while (!bound[q]) {
-            const uint32_t l = code_len(q);
-            if (!l) {
-                q = kBits;  // never resynchronised within the string
-                break;
-            }
-            q += l;
-        }
-        sync.push_back(q - p);
-    }
-    std::sort(sync.begin(), sync.end());
-    return sync;
-}
-
 huff_compress_data::~huff_compress_data() { delete tree; }
 
 namespace huff {
@@ -1101,9 +1047,7 @@ Status indexless_sync(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_bytes,
     // codes <= 32 bits take the LDS-staged kernels, longer codes 2048-bit segments
     // (~992 bits: with the one 8 KiB walk table a workgroup's LDS stays under
     // 40 KiB, 4 workgroups per CU; 1024-bit segments measured ~1.5 % slower)
-    uint64_t seg_target = dt->maxdepth <= 32 ? 992 : 2048;
-    if (const char* e = std::getenv("HUFF_IDX_SEG"))  // experiment: segment bits
-        if (std::atoi(e) >= 256) seg_target = static_cast<uint64_t>(std::atoi(e));
+    const uint64_t seg_target = dt->maxdepth <= 32 ? 992 : 2048;
     uint64_t S = static_cast<uint64_t>(g) * ((seg_target + g - 1) / g);
     // the LDS-staged kernels read lane i's bits from dword ~S/32 * i: with an
     // even dword stride every lane starts on the same few banks (1024 bits: all
@@ -1180,161 +1124,6 @@ Status indexless_mark(huff_ctx* ctx, IndexlessSync& st, DevBuf& sub_abs, uint32_
     return Status::ok();
 }
 
-// The single-pass index-free decoder (ifdec.hip) is opt-in: HUFF_IFD=1 runs
-// it for self-synchronising codes, =2 for every stream. Measured slower than
-// the multi-kernel path on 1 GiB (Zipf 3.4-3.6 ms vs 1.31, text 2.0 vs 1.16:
-// its blocks are latency-bound at 3 workgroups per CU and the look-back stalls
-// whole generations of blocks), so it is not the default.
-static bool ifd_enabled() {
-    const char* e = std::getenv("HUFF_IFD");
-    return e && (*e == '1' || *e == '2');
-}
-
-// The single-pass decoder (ifdec.hip) for codes <= 32 bits. *done = false
-// when the stream must go through the multi-kernel path instead (an anchor
-// did not resynchronise: some non-self-synchronising code).
-static Status decode_indexless_single(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_bytes, uint64_t valid_bits,
-                                      const huff_tree* t, const DecTables* dt, DevBuf& out, uint64_t* nsym,
-                                      uint8_t* d_user, size_t user_cap, unsigned long long* d_end, bool* done) {
-    *done = false;
-    // S: a multiple of the gcd of the code lengths, sized for ~48 letters per
-    // segment under the tree's own length distribution (a Huffman tree's
-    // letter of depth d has probability ~2^-d), preferring an odd dword
-    // stride between lanes (S = 32 mod 64: the lanes' stage reads spread over
-    // the LDS banks)
-    uint32_t g = 0;
-    double mean = 0;
-    for (const LeafCode& lc : t->t.leaves()) {
-        g = std::gcd(g, lc.len);
-        mean += std::ldexp(static_cast<double>(lc.len), -static_cast<int>(lc.len));
-    }
-    if (g == 0) g = 1;
-    uint64_t target = static_cast<uint64_t>(48.0 * std::max(mean, 1.0));
-    target = std::min<uint64_t>(std::max<uint64_t>(target, 64), 2048);
-    // codes that resynchronise slowly (near-fixed-length: lengths {5, 6} or
-    // {7, 8}) would leave many lanes unmerged inside their segments: those
-    // streams take the multi-kernel path (HUFF_IFD=2 forces this one)
-    {
-        const std::vector<uint32_t>& sy = t->sync_sample();
-        const size_t over = static_cast<size_t>(sy.end() - std::upper_bound(sy.begin(), sy.end(),
-                                                                             static_cast<uint32_t>(target / 2)));
-        const char* f = std::getenv("HUFF_IFD");
-        if (over * 500 > sy.size() && !(f && *f == '2')) return Status::ok();
-    }
-    bool forced = false;
-    if (const char* e = std::getenv("HUFF_IFD_SEG"))  // tests / experiments: segment bits (tiny S forces slow lanes)
-        if (std::atoi(e) >= 8) {
-            target = static_cast<uint64_t>(std::atoi(e));
-            forced = true;
-        }
-    uint64_t S = g * std::max<uint64_t>(1, (target + g / 2) / g);
-    for (uint64_t d = 0; !forced && d <= target / 8; ++d) {
-        const uint64_t lo = target > d ? target - d : 0, hi = target + d;
-        if (lo && lo % g == 0 && lo % 64 == 32) { S = lo; break; }
-        if (hi % g == 0 && hi % 64 == 32) { S = hi; break; }
-    }
-    const uint64_t nseg = (valid_bits + S - 1) / S;
-    if (nseg >= (1ull << 40)) return Status::ok();
-    dev::IfdArgs a = dev::ifd_layout(dt->sbits, static_cast<uint32_t>(S), dt->maxdepth);
-    a.comp = d_comp;
-    a.comp_bytes = comp_bytes;
-    a.valid_bits = valid_bits;
-    a.seg_bits = static_cast<uint32_t>(S);
-    a.nseg = nseg;
-    a.nblocks = dev::ifd_blocks(nseg);
-    a.stab = reinterpret_cast<const uint16_t*>(static_cast<const uint32_t*>(ctx->d_lut.p) + dt->soff);
-    a.stab_bits = dt->sbits;
-    a.lut = static_cast<const uint32_t*>(ctx->d_lut.p);
-    a.lut_bits = dt->bits;
-    a.max_len = dt->maxdepth;
-    a.cu_count = static_cast<uint32_t>(ctx->cu_count);
-    a.end_bit = d_end;
-    if (dev::ifd_lds_bytes(a) > 160 * 1024 || a.stage_bytes > dev::kIfdStageMax) return Status::ok();
-    // scratch: flags[16] | stats timers u64[8] | ticket | pad | total | status[nblocks] | exits[nblocks]
-    IndexlessSync& st = ctx->indexless_ws();
-    const size_t scratch = 144 + 16 * static_cast<size_t>(a.nblocks);
-    HUFF_TRY(st.ifd.ensure(scratch));
-    uint8_t* sp = static_cast<uint8_t*>(st.ifd.p);
-    a.flags = reinterpret_cast<unsigned int*>(sp);
-    a.ticket = reinterpret_cast<unsigned int*>(sp + 128);
-    a.total = reinterpret_cast<unsigned long long*>(sp + 136);
-    a.status = reinterpret_cast<unsigned long long*>(sp + 144);
-    a.exits = a.status + a.nblocks;
-    // the output: the caller's buffer, or `out` sized for the tree's
-    // expected letters (grown and rerun if the stream has more)
-    uint64_t cap = 0;
-    uint8_t* dst = nullptr;
-    auto place = [&](uint64_t want) -> Status {
-        if (d_user) {
-            cap = user_cap;
-            dst = d_user;
-        } else {
-            HUFF_TRY(out.ensure(want + 64));
-            cap = want;
-            dst = static_cast<uint8_t*>(out.p);
-        }
-        if (reinterpret_cast<uintptr_t>(dst) & 15) {  // the kernel stores 16-B pieces
-            HUFF_TRY(ctx->d_align.ensure(cap + 64));
-            dst = static_cast<uint8_t*>(ctx->d_align.p);
-        }
-        return Status::ok();
-    };
-    HUFF_TRY(place(static_cast<uint64_t>(1.25 * static_cast<double>(valid_bits) / std::max(mean, 1.0)) + 4096));
-    hipStream_t strm = ctx->stream;
-    uint64_t res[18] = {};
-    for (int attempt = 0; attempt < 2; ++attempt) {
-        a.out = dst;
-        a.out_cap = cap;
-        HIP_TRY(hipMemsetAsync(st.ifd.p, 0, scratch, strm));
-        // HUFF_IFD_DBG=<file>: per-block phase timestamps of an IFD_DBG build
-        const char* dbg_path = std::getenv("HUFF_IFD_DBG");
-        DevBuf dbg;
-        if (dbg_path) {
-            HUFF_TRY(dbg.ensure(64 * static_cast<size_t>(a.nblocks)));
-            HIP_TRY(hipMemsetAsync(dbg.p, 0, 64 * static_cast<size_t>(a.nblocks), strm));
-            a.dbg = static_cast<unsigned long long*>(dbg.p);
-        }
-        HUFF_TRY(ctx->timed("indexless_decode", [&] { return dev::launch_ifd(a, strm); }));
-        if (dbg_path) {
-            std::vector<uint64_t> h(8 * static_cast<size_t>(a.nblocks));
-            HIP_TRY(hipMemcpyAsync(h.data(), dbg.p, 64 * static_cast<size_t>(a.nblocks), hipMemcpyDeviceToHost, strm));
-            HUFF_TRY(ctx->sync());
-            if (FILE* f = std::fopen(dbg_path, "wb")) {
-                std::fwrite(h.data(), 8, h.size(), f);
-                std::fclose(f);
-            }
-            a.dbg = nullptr;
-        }
-        HIP_TRY(hipMemcpyAsync(res, st.ifd.p, 144, hipMemcpyDeviceToHost, strm));
-        HUFF_TRY(ctx->sync());
-        const uint32_t flags = static_cast<uint32_t>(res[0]);
-        if (std::getenv("HUFF_IFD_TRACE")) {
-            const uint32_t* f = reinterpret_cast<const uint32_t*>(res);
-            std::fprintf(stderr, "ifd: S=%llu nseg=%llu blocks=%u flags=%u total=%llu cap=%llu slow=%u ovf=%u "
-                         "settle=%u repair=%u big=%u\n", static_cast<unsigned long long>(S),
-                         static_cast<unsigned long long>(nseg), a.nblocks, flags,
-                         static_cast<unsigned long long>(res[17]), static_cast<unsigned long long>(cap), f[8], f[9],
-                         f[10], f[11], f[12]);
-            std::fprintf(stderr, "ifd cycles (sum over blocks, thread 0): decode %.3g fix %.3g count %.3g image %.3g "
-                         "lookback %.3g final %.3g copy %.3g stage %.3g\n", double(res[8]), double(res[9]),
-                         double(res[10]), double(res[11]), double(res[12]), double(res[13]), double(res[14]),
-                         double(res[15]));
-        }
-        // 1: not self-synchronising here; 4: a look-back gave up waiting (never
-        // seen; it would mean blocks ran out of index order): the multi-kernel path
-        if (flags & 5u) return Status::ok();
-        *nsym = res[17];
-        if (!(flags & 2u)) break;
-        if (d_user) return Status::err(HUFF_E_BUFFER_TOO_SMALL, "output buffer too small");
-        HUFF_TRY(place(res[17]));
-    }
-    if (dst != (d_user ? d_user : static_cast<uint8_t*>(out.p)) && *nsym)
-        HIP_TRY(hipMemcpyAsync(d_user ? d_user : out.p, dst, *nsym, hipMemcpyDeviceToDevice, strm));
-    HIP_TRY(hipEventRecord(ctx->lut_free, strm));
-    *done = true;
-    return Status::ok();
-}
-
 // The split index-free decoder (isplit.hip) for codes <= 32 bits: k_sync
 // (speculative walk + in-group fix-up -> lane records), k_fix_rec, the scan
 // of the block letters, one host read of the total, k_emit. *done = false
@@ -1384,7 +1173,7 @@ static Status decode_split(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_b
     a.stab = reinterpret_cast<const uint16_t*>(static_cast<const uint32_t*>(ctx->d_lut.p) + dt->soff);
     a.stab_bits = dt->sbits;
     a.wtab = reinterpret_cast<const uint16_t*>(static_cast<const uint32_t*>(ctx->d_lut.p) + dt->woff);
-    if (dt->l2words) {
+    if (dt->l2words && !std::getenv("HUFF_NO_L2")) {  // HUFF_NO_L2=1: the global tables (A/B, tests)
         a.l2 = static_cast<const uint32_t*>(ctx->d_lut.p) + dt->l2off;
         a.l2_words = dt->l2words;
     }
@@ -1530,12 +1319,6 @@ Status decode_indexless_dev(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_
         }
         HIP_TRY(hipEventRecord(ctx->lut_free, ctx->stream));
         return Status::ok();
-    }
-    if (dt->maxdepth <= 32 && ifd_enabled() && !decode_check_mode()) {
-        bool done = false;
-        HUFF_TRY(decode_indexless_single(ctx, d_comp, comp_bytes, valid_bits, t, dt, out, nsym, d_user, user_cap, d_end,
-                                         &done));
-        if (done) return Status::ok();
     }
     if (!decode_check_mode() && !split_disabled()) {
         bool done = false;

@@ -82,18 +82,10 @@ struct huff_tree {
     mutable std::mutex m;
     mutable std::unique_ptr<huff::EncTables> enc;
     mutable std::unique_ptr<huff::DecTables> dec;
-    mutable std::vector<uint32_t> sync;  // sorted resynchronisation distances (sync_sample)
 
     huff_tree();
     const huff::EncTables& enc_tables() const;
     huff::Status dec_tables(const huff::DecTables** out) const;
-    // Monte-Carlo resynchronisation distances of the code, in bits: a random
-    // bit string decoded from bit 0 gives each letter with probability
-    // 2^-depth (the tree's own letter distribution); from random offsets a
-    // second decoder walks until it lands on one of the first decoder's
-    // boundaries. Sorted; computed once per tree (~1 ms), for the index-free
-    // decoder's choice of path and segment length.
-    const std::vector<uint32_t>& sync_sample() const;
 };
 
 // Host-side copy of the encoder's restart index (travels with CompressData).
@@ -257,7 +249,6 @@ Status decode_indexless_dev(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_
 struct IndexlessSync {
     const DecTables* dt = nullptr;  // tables of the tree, uploaded to ctx->d_lut
     DevBuf s, x0, c, off, flag, tsum, samp, tm, dl, fixlist;
-    DevBuf ifd;  // the single-pass decoder's flags, ticket, total and look-back words
     DevBuf rec, xd, btot, boff;  // the split decoder's lane records, exits, block letters and offsets
     dev::IndexlessArgs a{};
     uint64_t total = 0;

@@ -195,7 +195,7 @@ class NativeComm:
         dist.broadcast_object_list(obj, src=0, group=group)
         return cls(ctx, world, rank, obj[0])
 
-    def world(self):
+    def observed_world(self):
         """(world, rank) as RCCL itself reports them (ncclCommCount /
         ncclCommUserRank through huff_comm_world)"""
         import ctypes as C
