@@ -43,18 +43,6 @@ namespace huff::dev {
 
 namespace {
 
-// k_emit's output image: 1 = over the stage (a lane's letters, <= 128, wait
-// in registers until every lane has read its bits; a block with a longer
-// lane writes straight to HBM), 0 = beside it
-#ifndef SPLIT_OVERLAP
-#define SPLIT_OVERLAP 0
-#endif
-// k_sync's multi-code windows: 1 = bits from the cursor position and the
-// code count from summed raw entries (segwalk.hpp multi_chunk_pos)
-#ifndef SPLIT_ESUM
-#define SPLIT_ESUM 0
-#endif
-
 constexpr uint32_t kT = 256;
 constexpr uint32_t kRecD = 10;  // rec: start - theta in bits [0, 10), letters above
 
@@ -79,6 +67,30 @@ __device__ __forceinline__ uint32_t get_at(const uint32_t (&v)[N], uint32_t k) {
 }
 
 // ---- A: speculative walk + in-workgroup fix-up -> lane records -------------
+
+// The checkpoints at the first of a single-code chunk's boundaries po[0, kmax)
+// (offsets from the segment start, c0 letters before the chunk) at or past
+// each threshold theta(i, nq + 1), ...: exact lane starts, so the lanes'
+// letter counts stay close to the host's sizing
+__device__ __forceinline__ void mark_ck(uint32_t (&ck)[kSplitRmax - 1], uint32_t& nq, uint64_t& next_th,
+                                        const SplitArgs& a, uint64_t i, uint64_t start,
+                                        const uint32_t (&po)[kChunkSteps], uint32_t c0, uint32_t kmax) {
+    const uint32_t R = 1u << a.lg_r;
+    while (nq + 1 < R && kmax && next_th - start <= get_at(po, kmax - 1)) {
+        const uint32_t th = static_cast<uint32_t>(next_th - start);
+        uint32_t v = 0;
+        bool f = false;
+#pragma unroll
+        for (uint32_t k = 0; k < kChunkSteps; ++k) {
+            const bool h = !f && k < kmax && po[k] >= th;
+            v = h ? po[k] | ((c0 + k + 1) << 16) : v;
+            f = f || h;
+        }
+        put_at(ck, nq, v);
+        ++nq;
+        next_th = nq + 1 < R ? theta(a, i, nq + 1) : ~0ull;
+    }
+}
 
 template <bool SLOW>
 __global__ __launch_bounds__(kT) void k_sync(SplitArgs a) {
@@ -121,30 +133,37 @@ __global__ __launch_bounds__(kT) void k_sync(SplitArgs a) {
             smp[next_k * kT + t] = static_cast<uint32_t>(cur - start) | (cnt << 16);
             next_bit = ++next_k < a.nsamp ? next_bit + kSampBits : ~0ull;
         }
-        while (cur >= next_th) {
-            put_at(ck, nq, static_cast<uint32_t>(cur - start) | (cnt << 16));
-            ++nq;
-            next_th = nq + 1 < R ? theta(a, i, nq + 1) : ~0ull;
-        }
     };
+    // multi-code chunks while the chunk's last boundary stays below `end` (so
+    // no boundary inside one is the exit), a checkpoint at the first window
+    // end at or past each threshold (a lane starts within one window's codes
+    // of its threshold); single codes to the exit
     if (wtab) {
-        // multi-code chunks while the chunk's last boundary stays below `end`
-        // (so no boundary inside it can be the exit); single codes after
         const uint64_t span = static_cast<uint64_t>(kChunkSteps) * (a.max_len > K ? a.max_len : K);
         while (cur + span < end) {
-            uint32_t U, N;
-#if SPLIT_ESUM
-            U = multi_chunk_pos<SLOW>(c, N, wtab, stab, K, a.lut, Kg);
-#else
-            c.multi_chunk<SLOW>(U, N, wtab, stab, K, a.lut, Kg);
-#endif
+            uint32_t U, N, q[kChunkSteps];
+            c.multi_chunk<SLOW>(U, N, q, wtab, stab, K, a.lut, Kg);
+            while (next_th <= cur + U) {  // (no threshold left: ~0)
+                const uint32_t th = static_cast<uint32_t>(next_th - cur);
+                uint32_t v = 0;
+                bool f = false;
+#pragma unroll
+                for (uint32_t k = 0; k < kChunkSteps; ++k) {
+                    const bool h = !f && (q[k] & 0xFFFFu) >= th;
+                    v = h ? q[k] : v;
+                    f = f || h;
+                }
+                put_at(ck, nq, static_cast<uint32_t>(cur - start + (v & 0xFFFFu)) | ((cnt + (v >> 16)) << 16));
+                ++nq;
+                next_th = nq + 1 < R ? theta(a, i, nq + 1) : ~0ull;
+            }
             cur += U;
             cnt += N;
             note();
         }
     }
     for (;;) {
-        uint32_t L[kChunkSteps];
+        uint32_t L[kChunkSteps], po[kChunkSteps];
         c.chunk<SLOW>(L, stab, K, a.lut, Kg);
         // the first boundary at or past `end` inside this chunk?
         uint64_t p = cur, ex = ~0ull;
@@ -152,11 +171,13 @@ __global__ __launch_bounds__(kT) void k_sync(SplitArgs a) {
 #pragma unroll
         for (int k = 0; k < kChunkSteps; ++k) {
             p += L[k];
+            po[k] = static_cast<uint32_t>(p - start);
             const bool hit = ex == ~0ull && p >= end;
             ex = hit ? p : ex;
             ec = hit ? static_cast<uint32_t>(k + 1) : ec;
         }
         if (ex != ~0ull) {
+            mark_ck(ck, nq, next_th, a, i, start, po, cnt, ec - 1);  // thresholds past those boundaries start at the exit
             cnt += ec;
             if (ex > B) {  // an incomplete final code is dropped (comp.rs:493-516)
                 ex = B;
@@ -165,6 +186,7 @@ __global__ __launch_bounds__(kT) void k_sync(SplitArgs a) {
             cur = ex;
             break;
         }
+        mark_ck(ck, nq, next_th, a, i, start, po, cnt, kChunkSteps);
         cur = p;
         cnt += kChunkSteps;
         note();
@@ -190,13 +212,14 @@ __global__ __launch_bounds__(kT) void k_sync(SplitArgs a) {
         uint32_t fq = 0;  // checkpoints re-recorded on the true path: ck[0, fq)
         uint64_t fth = R > 1 ? theta(a, i, 1) : ~0ull;
         for (;;) {
-            uint32_t L[kChunkSteps];
+            uint32_t L[kChunkSteps], po[kChunkSteps];
             w.chunk<SLOW>(L, stab, K, a.lut, Kg);
             uint64_t p = pa, pex = 0;
             int hit = -1, ex = -1;
 #pragma unroll
             for (int j = 0; j < kChunkSteps; ++j) {
                 p += L[j];
+                po[j] = static_cast<uint32_t>(p - start);
                 hit = (hit < 0 && ex < 0 && p == pk) ? j : hit;
                 const bool e = ex < 0 && hit < 0 && p >= end;
                 ex = e ? j : ex;
@@ -205,17 +228,15 @@ __global__ __launch_bounds__(kT) void k_sync(SplitArgs a) {
             if (hit >= 0) {  // merged on the sample: true-local index tt
                 const uint32_t tt = na + static_cast<uint32_t>(hit) + 1;
                 const uint32_t dl = tt - ik;  // (mod 2^32) true-local = spec-local + dl past the merge
-                for (uint32_t q = fq; q + 1 < R; ++q) {
-                    // thresholds up to the merge point: the merge point itself;
-                    // later ones: the speculative checkpoint (on the merged path)
-                    const uint32_t v = theta(a, i, q + 1) <= pk ? static_cast<uint32_t>(pk - start) | (tt << 16)
-                                                                : get_at(ck, q) + (dl << 16);
-                    put_at(ck, q, v);
-                }
+                // thresholds up to the merge point: on this chunk; later ones:
+                // the speculative checkpoint (on the merged path)
+                mark_ck(ck, fq, fth, a, i, start, po, na, static_cast<uint32_t>(hit) + 1);
+                for (uint32_t q = fq; q + 1 < R; ++q) put_at(ck, q, get_at(ck, q) + (dl << 16));
                 cnt += dl;
                 break;
             }
             if (ex >= 0) {  // a new exit
+                mark_ck(ck, fq, fth, a, i, start, po, na, static_cast<uint32_t>(ex));
                 cnt = na + static_cast<uint32_t>(ex) + 1;
                 if (pex > B) {  // an incomplete final code is dropped
                     pex = B;
@@ -226,13 +247,9 @@ __global__ __launch_bounds__(kT) void k_sync(SplitArgs a) {
                 for (uint32_t q = fq; q + 1 < R; ++q) put_at(ck, q, static_cast<uint32_t>(cur - start) | (cnt << 16));
                 break;
             }
+            mark_ck(ck, fq, fth, a, i, start, po, na, kChunkSteps);
             pa = p;
             na += kChunkSteps;
-            while (pa >= fth) {
-                put_at(ck, fq, static_cast<uint32_t>(pa - start) | (na << 16));
-                ++fq;
-                fth = fq + 1 < R ? theta(a, i, fq + 1) : ~0ull;
-            }
             while (pa > pk) {  // passed the sample without landing on it: the next one
                 const uint32_t sv = k < a.nsamp ? smp[k * kT + t] : ~0u;
                 ++k;
@@ -502,7 +519,7 @@ __global__ __launch_bounds__(kT) void k_emit(SplitArgs a) {
     const uint32_t tab_bytes = (tab_words * 4 + 15) & ~15u;
     uint16_t* stab = reinterpret_cast<uint16_t*>(smem);
     uint32_t* stage = reinterpret_cast<uint32_t*>(smem + tab_bytes);
-    uint8_t* img = SPLIT_OVERLAP ? smem + tab_bytes : smem + tab_bytes + a.stage_bytes;
+    uint8_t* img = smem + tab_bytes;  // the output image lies over the stage (written after the decode)
     const uint64_t nl = a.nseg << a.lg_r;
     const uint64_t j = static_cast<uint64_t>(blockIdx.x) * kT + t;
     const bool live = j < nl;
@@ -560,9 +577,10 @@ __global__ __launch_bounds__(kT) void k_emit(SplitArgs a) {
     const uint32_t img0 = static_cast<uint32_t>(O & 15);
     const uint32_t stage_last = a.stage_bytes / 4 - 1;
     const uint32_t rel = static_cast<uint32_t>(start - byte_lo * 8);
-    // more letters than the image (or, image over the stage, a lane with more
-    // than its registers hold): straight to HBM, byte by byte (rare)
-    if (img0 + cb > a.img_bytes || (SPLIT_OVERLAP && __syncthreads_or(n > 128))) {
+    // more letters than the image, or a lane with more than its registers
+    // hold: straight to HBM, byte by byte (rare: the host sizes the lanes for
+    // ~48 letters)
+    if (img0 + cb > a.img_bytes || __syncthreads_or(n > 64)) {
         if (n) {
             ECur c;
             c.init(stage, stage_last, rel);
@@ -575,51 +593,43 @@ __global__ __launch_bounds__(kT) void k_emit(SplitArgs a) {
         }
         return;
     }
-#if SPLIT_OVERLAP
+    // As k_decode_fixed: no per-lane predicate on the steps. Every lane makes
+    // as many lookups as the wave's longest lane (a scalar bound, checked
+    // every 4 letters); a shorter lane decodes on into its successor's bits
+    // and drops those letters (the stage reads are clamped). The letters wait
+    // in registers until every lane has read its bits, then go into the
+    // image, which lies over the stage.
+    uint32_t o0[16];
     {
-        uint32_t o0[16], o1[16];
-        ECur c;
-        c.init(stage, stage_last, rel);
-        auto batch = [&](uint32_t (&o)[16], uint32_t m) {
+        uint32_t wmax = n;
 #pragma unroll
-            for (int s = 0; s < 64; ++s) {
-                if (static_cast<uint32_t>(s) < m) {
-                    if ((s & 1) == 0) c.refill();
-                    const uint32_t e = c.step<SLOW>(stab, K, a.lut, a.lut_bits);
-                    if ((s & 3) == 0) o[s >> 2] = e >> 8;
-                    else o[s >> 2] = __builtin_amdgcn_perm(e, o[s >> 2], (s & 3) == 1 ? 0x0C0C0500u : (s & 3) == 2 ? 0x0C050100u : 0x05020100u);
-                }
-            }
-        };
-        const uint32_t m0 = n < 64 ? n : 64u, m1 = n - m0;
-        if (n) batch(o0, m0);
-        if (m1) batch(o1, m1);
-        if (last_code) *a.end_bit = byte_lo * 8 + c.pos();
-        __syncthreads();  // every lane has read its bits: the image may overwrite the stage
-        if (m0) put_run(img, img0 + off_l, o0, m0);
-        if (m1) put_run(img, img0 + off_l + 64, o1, m1);
-    }
-#else
-    if (n) {
-        ECur c;
-        c.init(stage, stage_last, rel);
-        for (uint32_t base = 0; base < n; base += 64) {
-            const uint32_t m = n - base < 64 ? n - base : 64u;
-            uint32_t o[16];
-#pragma unroll
-            for (int s = 0; s < 64; ++s) {
-                if (static_cast<uint32_t>(s) < m) {
-                    if ((s & 1) == 0) c.refill();
-                    const uint32_t e = c.step<SLOW>(stab, K, a.lut, a.lut_bits);
-                    if ((s & 3) == 0) o[s >> 2] = e >> 8;
-                    else o[s >> 2] = __builtin_amdgcn_perm(e, o[s >> 2], (s & 3) == 1 ? 0x0C0C0500u : (s & 3) == 2 ? 0x0C050100u : 0x05020100u);
-                }
-            }
-            put_run(img, img0 + off_l + base, o, m);
+        for (int k = 1; k < 64; k <<= 1) {
+            const uint32_t y = static_cast<uint32_t>(__shfl_xor(static_cast<int>(wmax), k));
+            wmax = y > wmax ? y : wmax;
         }
-        if (last_code) *a.end_bit = byte_lo * 8 + c.pos();
+        const uint32_t steps = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(wmax)));
+        ECur c;
+        c.init(stage, stage_last, rel);
+#pragma unroll
+        for (int s = 0; s < 64; ++s) {
+            if ((s & 3) == 0 && static_cast<uint32_t>(s) >= steps) break;
+            if ((s & 1) == 0) c.refill();
+            const uint32_t e = c.step<SLOW>(stab, K, a.lut, a.lut_bits);
+            if ((s & 3) == 0) o0[s >> 2] = e >> 8;
+            else o0[s >> 2] = __builtin_amdgcn_perm(e, o0[s >> 2], (s & 3) == 1 ? 0x0C0C0500u : (s & 3) == 2 ? 0x0C050100u : 0x05020100u);
+        }
     }
-#endif
+    if (last_code) {  // the bit after exactly n codes (one lane of the grid walks them again)
+        ECur c;
+        c.init(stage, stage_last, rel);
+        for (uint32_t k = 0; k < n; ++k) {
+            c.refill();
+            c.step<SLOW>(stab, K, a.lut, a.lut_bits);
+        }
+        *a.end_bit = byte_lo * 8 + c.pos();
+    }
+    __syncthreads();  // every lane has read its bits: the image may overwrite the stage
+    if (n) put_run(img, img0 + off_l, o0, n);
     __syncthreads();
     // the image to HBM: 16-B pieces, whole where the block owns all 16 bytes
     const uint64_t gbase = O - img0;
@@ -646,12 +656,12 @@ size_t split_sync_lds_bytes(const SplitArgs& a) {
 
 size_t split_emit_lds_bytes(const SplitArgs& a) {
     const size_t tab = ((((1u << a.stab_bits) + 1) / 2) * 4 + 15) & ~size_t(15);
-    return tab + (SPLIT_OVERLAP ? std::max<size_t>(a.stage_bytes, a.img_bytes) : a.stage_bytes + a.img_bytes);
+    return tab + std::max<size_t>(a.stage_bytes, a.img_bytes);
 }
 
 hipError_t launch_split_sync(const SplitArgs& a, hipStream_t s) {
     if (a.nseg == 0) return hipSuccess;
-    if (a.max_len > 32 || a.seg_bits >= 1024 || (1u << a.lg_r) > kSplitRmax || a.nsamp > kSampMax || !a.stab)
+    if (a.max_len > 32 || a.seg_bits > 2048 || (1u << a.lg_r) > kSplitRmax || a.nsamp > kSampMax || !a.stab)
         return hipErrorInvalidValue;
     const bool slow = a.max_len > a.stab_bits;
     hipLaunchKernelGGL(slow ? k_sync<true> : k_sync<false>, dim3((a.nseg + kT - 1) / kT), dim3(kT),

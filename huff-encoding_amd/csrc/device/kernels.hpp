@@ -179,7 +179,7 @@ struct SplitArgs {
     const uint8_t* comp;          // 16-B aligned
     uint64_t comp_bytes;
     uint64_t valid_bits;          // B
-    uint64_t seg_bits;            // S (< 1024, a multiple of the gcd of the code lengths)
+    uint64_t seg_bits;            // S (<= 2048, a multiple of the gcd of the code lengths)
     uint64_t nseg;
     uint32_t lg_r;                // R = 1 << lg_r lanes per segment (R <= kSplitRmax)
     uint32_t nsamp;               // merge samples per segment (every kSampBits bits; <= kSampMax)

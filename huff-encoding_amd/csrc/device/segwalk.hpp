@@ -158,36 +158,30 @@ struct Cursor {
             }
         }
     }
-};
-
-// kChunkSteps multi-code windows as multi_chunk, with the bits taken from the
-// cursor's position and the code count from a plain sum of the raw walk-table
-// entries: E = sum(first length) + (U << 8) + (N << 12), the first lengths
-// adding up to < 256 (<= 8 x 12 bits: non-slow entries only; a slow step adds
-// its own (len << 8) + (1 << 12)), so N = (E - (U << 8)) >> 12. Two VALU per
-// window fewer than summing the fields. Returns U; N through the reference.
-template <bool SLOW>
-__device__ __forceinline__ uint32_t multi_chunk_pos(Cursor& c, uint32_t& N, const uint16_t* wtab, const uint16_t* stab,
-                                                    uint32_t K, const uint32_t* glut, uint32_t Kg) {
-    const uint32_t p0 = 32 * c.rp - (c.X & 63);
-    uint32_t E = 0;
+    // as above, with the running totals after each window: q[k] = U | N << 16
+    template <bool SLOW>
+    __device__ __forceinline__ void multi_chunk(uint32_t& U, uint32_t& N, uint32_t (&q)[kChunkSteps],
+                                                const uint16_t* wtab, const uint16_t* stab, uint32_t K,
+                                                const uint32_t* glut, uint32_t Kg) {
+        uint32_t Q = 0;
 #pragma unroll
-    for (int k = 0; k < kChunkSteps; ++k) {
-        if ((k & 1) == 0) c.refill();
-        const uint32_t e = wtab[static_cast<uint32_t>(c.buf >> 32) >> (32 - K)];
-        if (SLOW && (e & kSsSlow)) {
-            E += (c.step<SLOW>(stab, K, glut, Kg) << 8) + (1u << 12);
-        } else {
-            const uint32_t u = (e >> 8) & 15u;
-            c.buf <<= u;
-            c.X -= u;
-            E += e;
+        for (int k = 0; k < kChunkSteps; ++k) {
+            if ((k & 1) == 0) refill();
+            const uint32_t e = wtab[static_cast<uint32_t>(buf >> 32) >> (32 - K)];
+            if (SLOW && (e & kSsSlow)) {
+                Q += step<SLOW>(stab, K, glut, Kg) + (1u << 16);
+            } else {
+                const uint32_t u = (e >> 8) & 15u;
+                buf <<= u;
+                X -= u;
+                Q += u + ((e >> 12) << 16);
+            }
+            q[k] = Q;
         }
+        U = Q & 0xFFFFu;
+        N = Q >> 16;
     }
-    const uint32_t U = 32 * c.rp - (c.X & 63) - p0;
-    N = (E - (U << 8)) >> 12;
-    return U;
-}
+};
 
 // LDS: [single-symbol table][level-2 table][staged input ...]
 template <class A>

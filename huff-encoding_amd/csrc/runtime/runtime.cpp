@@ -61,11 +61,12 @@ bool fixed8_disabled() {
     return e && *e && *e != '0';
 }
 
-// HUFF_SPLIT=0: index-free byte streams take the older sample + mark path
-// (the wide decoders still use it; the tests run both)
-bool split_disabled() {
+// HUFF_SPLIT=1: index-free byte streams take the split decoder (isplit.hip)
+// instead of the sample + mark path (measured slower on the GPU: DESIGN §11;
+// the tests run both)
+bool split_enabled() {
     const char* e = std::getenv("HUFF_SPLIT");  // read per call: tests flip it
-    return e && *e == '0';
+    return e && *e && *e != '0';
 }
 
 uint32_t decode_check_mode() {
@@ -1124,6 +1125,16 @@ Status indexless_mark(huff_ctx* ctx, IndexlessSync& st, DevBuf& sub_abs, uint32_
     return Status::ok();
 }
 
+// build-time policy of the split decoder (A/B builds, tools/build_variant.sh):
+// the letters a lane is sized for, and the longest segment (k_sync stages 256
+// segments: 1,100 bits keep its LDS at 3 workgroups per CU)
+#ifndef SPLIT_LANE_LETTERS
+#define SPLIT_LANE_LETTERS 46.0
+#endif
+#ifndef SPLIT_SEG_MAX
+#define SPLIT_SEG_MAX 1100.0
+#endif
+
 // The split index-free decoder (isplit.hip) for codes <= 32 bits: k_sync
 // (speculative walk + in-group fix-up -> lane records), k_fix_rec, the scan
 // of the block letters, one host read of the total, k_emit. *done = false
@@ -1133,9 +1144,6 @@ static Status decode_split(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_b
                            size_t user_cap, unsigned long long* d_end, bool* done) {
     *done = false;
     if (dt->maxdepth > 32 || !dt->sbits) return Status::ok();
-    // S as the sync pass of the older path: a multiple of the gcd g of the
-    // code lengths near 992 bits, preferring S = 32 mod 64 (odd dword stride
-    // between the lanes' stage reads), below 1024 (10-bit record fields)
     uint32_t g = 0;
     double mean = 0;
     for (const LeafCode& lc : t->t.leaves()) {
@@ -1144,21 +1152,28 @@ static Status decode_split(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_b
     }
     if (g == 0) g = 1;
     mean = std::max(mean, 1.0);
-    const uint64_t seg_target = 992;
-    uint64_t S = static_cast<uint64_t>(g) * ((seg_target + g - 1) / g);
-    for (uint64_t k = (seg_target + g - 1) / g, tries = 0; tries < 128; ++k, ++tries)
-        if ((static_cast<uint64_t>(g) * k) % 64 == 32) {
-            S = static_cast<uint64_t>(g) * k;
+    // lanes of ~SPLIT_LANE_LETTERS letters (k_emit holds a lane's letters in
+    // one 64-letter register batch; a block with a longer lane writes bytes
+    // straight to HBM): R lanes per segment, the fewest with R x that
+    // lane's bits >= 640 (segments long enough that the fix-up walks stay a
+    // small part of them), S = R lanes' bits in [256, SPLIT_SEG_MAX], a
+    // multiple of the gcd g of the code lengths
+    const double lane_bits = SPLIT_LANE_LETTERS * mean;
+    uint32_t lg_r = 0;
+    while ((1u << lg_r) < dev::kSplitRmax && static_cast<double>(1u << lg_r) * lane_bits < 640.0) ++lg_r;
+    const uint64_t want = static_cast<uint64_t>(
+        std::min<double>(std::max<double>(static_cast<double>(1u << lg_r) * lane_bits, 256.0), SPLIT_SEG_MAX));
+    // preferring S = 32 mod 64 within 64 bits below (an odd dword stride
+    // between the lanes' stage reads)
+    uint64_t S = std::max<uint64_t>(g, want / g * g);
+    for (uint64_t c = S; c + 64 > S && c >= g; c -= g)
+        if (c % 64 == 32) {
+            S = c;
             break;
         }
-    if (S >= 1024) S = static_cast<uint64_t>(g) * (1023 / g);
-    if (S < 256) return Status::ok();
+    if (S < 256 || S < 2 * dt->maxdepth) return Status::ok();
     const uint64_t nseg = (valid_bits + S - 1) / S;
     if (nseg > 0xFFFFFFFFull / dev::kSplitRmax) return Status::ok();
-    // lanes per segment: about 48 letters each (at most 56 expected), so a
-    // lane's letters fit one 64-letter pass of k_emit's registers
-    uint32_t lg_r = 0;
-    while ((1u << lg_r) < dev::kSplitRmax && static_cast<double>(S >> lg_r) / mean > 56.0) ++lg_r;
     dev::SplitArgs a{};
     a.comp = d_comp;
     a.comp_bytes = comp_bytes;
@@ -1184,7 +1199,7 @@ static Status decode_split(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_b
     // its output image: the block's expected letters with a margin (a block
     // with more writes straight to HBM)
     const double exp_letters = 256.0 * static_cast<double>(S >> lg_r) / mean;
-    a.img_bytes = static_cast<uint32_t>(std::min(1.25 * exp_letters + 1024.0, 64.0 * 1024)) & ~15u;
+    a.img_bytes = static_cast<uint32_t>(std::min(1.15 * exp_letters + 512.0, 64.0 * 1024)) & ~15u;
     if (dev::split_sync_lds_bytes(a) > 140 * 1024 || dev::split_emit_lds_bytes(a) > 160 * 1024) return Status::ok();
     IndexlessSync& st = ctx->indexless_ws();
     const uint64_t nl = nseg << lg_r;
@@ -1320,7 +1335,7 @@ Status decode_indexless_dev(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_
         HIP_TRY(hipEventRecord(ctx->lut_free, ctx->stream));
         return Status::ok();
     }
-    if (!decode_check_mode() && !split_disabled()) {
+    if (!decode_check_mode() && split_enabled()) {
         bool done = false;
         HUFF_TRY(decode_split(ctx, d_comp, comp_bytes, valid_bits, t, dt, out, nsym, d_user, user_cap, d_end, &done));
         if (done) return Status::ok();

@@ -24,12 +24,11 @@ def pytest_configure(config):
 
 
 def _ensure_built():
-    lib = os.path.join(PKG, "lib", "libhuffgpu.so")
-    if not os.path.exists(lib):
-        subprocess.run(["make", "-s", "-C", PKG, "-j8"], check=True)
-    so = os.path.join(ORACLE, "build", "liboracle.so")
-    if not os.path.exists(so):
-        subprocess.run(["make", "-s", "-C", ORACLE], check=True)
+    """`make` is incremental: always run it, so a test never loads a library
+    older than its sources (a pushed tree without build/ rebuilds from
+    scratch, which takes ~30 s)"""
+    subprocess.run(["make", "-s", "-C", PKG, "-j8"], check=True)
+    subprocess.run(["make", "-s", "-C", ORACLE], check=True)
 
 
 _ensure_built()

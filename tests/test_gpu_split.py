@@ -2,18 +2,26 @@
 
 Streams are written by the CPU restatement (oracle/, comp.rs:419-451) with no
 restart index, as the reference writes every CompressData and .hff payload,
-and decoded on the device through huff_dev_decompress (comp.rs:487-519): the
-default path for codes <= 32 bits (k_sync -> k_fix_rec -> scan -> k_emit).
+and decoded on the device through huff_dev_decompress (comp.rs:487-519) with
+HUFF_SPLIT=1, the opt-in path for codes <= 32 bits (k_sync -> k_fix_rec ->
+scan -> k_emit; measured slower than the default sample + mark path, DESIGN
+§11).
 The cases cover its paths: lanes merging with their speculative walk, codes
 longer than the 12-bit table, 1-8 lanes per segment, lanes past 64 letters,
 blocks past the LDS image, slowly resynchronising codes (the fix-up rounds),
 tiny and ragged streams, misaligned outputs, the count-only query, garbage
-payloads, and equality with the older sample + mark path (HUFF_SPLIT=0).
+payloads, and equality with the default sample + mark path (HUFF_SPLIT=0).
 """
 import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True)
+def split_on(monkeypatch):
+    """the split decoder is opt-in (HUFF_SPLIT=1)"""
+    monkeypatch.setenv("HUFF_SPLIT", "1")
 
 
 def roundtrip(H, O, ctx, data, misalign=0):
@@ -106,7 +114,7 @@ def test_split_misaligned_output(H, O, ctx, cases):
 
 
 def test_split_equals_older_path(H, O, ctx, monkeypatch):
-    """the same stream through the split path and HUFF_SPLIT=0"""
+    """the same stream through the split path and the default one"""
     import torch
     from huff_coding import device as D
 
@@ -143,3 +151,38 @@ def test_split_garbage_payloads(H, O, ctx):
                 got = D.decompress_dev(ctx, tree, dc.data_ptr(), n, pad, out.data_ptr(), len(want) + 64)
                 torch.cuda.synchronize()
                 assert got == len(want) and out[:got].cpu().numpy().tobytes() == want, (n, pad)
+
+
+@pytest.mark.parametrize("kind", ["zipf", "text"])
+def test_split_full_size_foreign_stream(H, O, ctx, kind, monkeypatch):
+    """BASELINE size: the 1 GiB Zipf (configs[2]) and text streams written on
+    the CPU by the oracle's table-driven encoder (no restart index, as the
+    reference writes every stream: comp.rs:128-184, 487-519), decoded through
+    huff_dev_decompress by both index-free paths and compared with the input
+    on the device"""
+    import os
+
+    import torch
+    from huff_coding import device as D
+
+    n = 1 << 30
+    host = O.gen_zipf(0x5EED0002, n) if kind == "zipf" else O.gen_text(0x5EED0005, n)
+    t = O.Tree.from_weights(O.weights_from_array(O.fast_hist(host, 16)))
+    code, ln = t.code_table()
+    comp, bits = O.fast_encode(host, code, ln, threads=min(16, os.cpu_count() or 1))
+    pad = (8 - bits % 8) % 8
+    tree = H.HuffTree.try_from_bin(t.as_bin())
+    x = torch.from_numpy(host).cuda()
+    del host
+    dc = torch.zeros(comp.size + 64, dtype=torch.uint8, device="cuda")
+    dc[: comp.size] = torch.from_numpy(comp).cuda()
+    del comp
+    out = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
+    for flag in ("1", "0"):  # the split decoder and the default sample + mark path
+        monkeypatch.setenv("HUFF_SPLIT", flag)
+        out.fill_(0)
+        torch.cuda.synchronize()
+        got = D.decompress_dev(ctx, tree, dc.data_ptr(), dc.numel() - 64, pad, out.data_ptr(), n + 64)
+        torch.cuda.synchronize()
+        assert got == n
+        assert torch.equal(out[:n], x), flag
