@@ -101,8 +101,7 @@ __global__ __launch_bounds__(kT) void k_sync(SplitArgs a) {
     TabLoad tl;
     issue_tables(a, tl);
     const uint32_t tw = (tables_words(a) + 3) & ~3u;
-    uint32_t* smp = lds + tw;  // [nsamp][kT]: (offset from the segment start) | spec index << 16
-    const Staged st = with_l2(stage_block(a, lds + tw + a.nsamp * kT), a, lds);
+    const Staged st = with_l2(stage_block(a, lds + tw), a, lds);
     const uint16_t* stab = store_tables(a, tl, lds);
     const uint16_t* wtab = a.wtab ? stab : nullptr;  // one table serves single and multi-code steps
     if (t < kSplitRmax) bt[t] = 0;
@@ -121,6 +120,11 @@ __global__ __launch_bounds__(kT) void k_sync(SplitArgs a) {
     uint32_t cnt = 0;
     // merge samples: the first step end at or past every kSampBits bits
     uint32_t next_k = 0;
+    // the samples (offset from the segment start | spec index << 16; ~0:
+    // none) stay in this lane's registers: only its own fix-up reads them
+    uint32_t smp[kSampMax];
+#pragma unroll
+    for (uint32_t q = 0; q < kSampMax; ++q) smp[q] = ~0u;
     uint64_t next_bit = (a.nsamp && live) ? start + kSampBits : ~0ull;
     // checkpoints ck[q - 1] = lane q's start (offset from `start`) | letters before it << 16
     uint32_t ck[kSplitRmax - 1];
@@ -130,7 +134,7 @@ __global__ __launch_bounds__(kT) void k_sync(SplitArgs a) {
     uint64_t next_th = R > 1 ? theta(a, i, 1) : ~0ull;
     auto note = [&]() {
         if (cur >= next_bit) {
-            smp[next_k * kT + t] = static_cast<uint32_t>(cur - start) | (cnt << 16);
+            put_at(smp, next_k, static_cast<uint32_t>(cur - start) | (cnt << 16));
             next_bit = ++next_k < a.nsamp ? next_bit + kSampBits : ~0ull;
         }
     };
@@ -191,9 +195,8 @@ __global__ __launch_bounds__(kT) void k_sync(SplitArgs a) {
         cnt += kChunkSteps;
         note();
     }
-    for (; next_k < a.nsamp; ++next_k) smp[next_k * kT + t] = ~0u;
     for (; nq + 1 < R; ++nq) put_at(ck, nq, static_cast<uint32_t>(cur - start) | (cnt << 16));
-    const uint32_t s0 = a.nsamp ? smp[t] : ~0u;  // the first sample (read back by this lane only)
+    const uint32_t s0 = smp[0];  // the first sample
 
     // fix-up inside the workgroup (the first lane's predecessor is in another
     // workgroup: k_fix_rec)
@@ -251,7 +254,7 @@ __global__ __launch_bounds__(kT) void k_sync(SplitArgs a) {
             pa = p;
             na += kChunkSteps;
             while (pa > pk) {  // passed the sample without landing on it: the next one
-                const uint32_t sv = k < a.nsamp ? smp[k * kT + t] : ~0u;
+                const uint32_t sv = k < a.nsamp ? get_at(smp, k) : ~0u;
                 ++k;
                 pk = sv == ~0u ? ~0ull : start + (sv & 0xFFFFu);
                 ik = sv >> 16;
@@ -651,7 +654,7 @@ __global__ __launch_bounds__(kT) void k_emit(SplitArgs a) {
 size_t split_sync_lds_bytes(const SplitArgs& a) {
     const size_t tw = (((((1u << a.stab_bits) + 1) / 2 + 3) & ~3u) + a.l2_words + 3) & ~size_t(3);
     const size_t stage = ((kT * a.seg_bits + 7) / 8 + 128 + 15) / 16 * 16;
-    return tw * 4 + static_cast<size_t>(a.nsamp) * kT * 4 + stage;
+    return tw * 4 + stage;
 }
 
 size_t split_emit_lds_bytes(const SplitArgs& a) {

@@ -1161,8 +1161,14 @@ static Status decode_split(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_b
     const double lane_bits = SPLIT_LANE_LETTERS * mean;
     uint32_t lg_r = 0;
     while ((1u << lg_r) < dev::kSplitRmax && static_cast<double>(1u << lg_r) * lane_bits < 640.0) ++lg_r;
+    // k_sync at 4 workgroups per CU: its tables, the stage of 256 segments
+    // and ~2 KiB of static LDS within 40 KiB (where the tables leave room)
+    const bool l2 = dt->l2words && !std::getenv("HUFF_NO_L2");
+    const double tw_bytes = 4.0 * (((((1u << dt->sbits) + 1) / 2 + 3) & ~3u) + (l2 ? dt->l2words : 0) + 3) / 4 * 4;
+    const double s_lds = (40960.0 - 2112.0 - tw_bytes - 144.0) / 32.0;
+    const double seg_max = s_lds >= 640.0 ? std::min<double>(s_lds, SPLIT_SEG_MAX) : SPLIT_SEG_MAX;
     const uint64_t want = static_cast<uint64_t>(
-        std::min<double>(std::max<double>(static_cast<double>(1u << lg_r) * lane_bits, 256.0), SPLIT_SEG_MAX));
+        std::min<double>(std::max<double>(static_cast<double>(1u << lg_r) * lane_bits, 256.0), seg_max));
     // preferring S = 32 mod 64 within 64 bits below (an odd dword stride
     // between the lanes' stage reads)
     uint64_t S = std::max<uint64_t>(g, want / g * g);
@@ -1188,7 +1194,7 @@ static Status decode_split(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_b
     a.stab = reinterpret_cast<const uint16_t*>(static_cast<const uint32_t*>(ctx->d_lut.p) + dt->soff);
     a.stab_bits = dt->sbits;
     a.wtab = reinterpret_cast<const uint16_t*>(static_cast<const uint32_t*>(ctx->d_lut.p) + dt->woff);
-    if (dt->l2words && !std::getenv("HUFF_NO_L2")) {  // HUFF_NO_L2=1: the global tables (A/B, tests)
+    if (l2) {  // HUFF_NO_L2=1: the global tables (A/B, tests)
         a.l2 = static_cast<const uint32_t*>(ctx->d_lut.p) + dt->l2off;
         a.l2_words = dt->l2words;
     }
