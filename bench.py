@@ -73,7 +73,22 @@ def cpu_info():
                     break
     except OSError:
         pass
-    return {"nproc": os.cpu_count(), "affinity": len(os.sched_getaffinity(0)), "cpu_model": model}
+    # the cgroup CPU quota (cgroup v2 cpu.max "<quota> <period>"): a mask of
+    # many threads may still get only this many CPUs' worth of time
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            quota = None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        try:  # cgroup v1
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f, open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as g:
+                q, per = int(f.read()), int(g.read())
+                quota = round(q / per, 2) if q > 0 else None
+        except (OSError, ValueError):
+            pass
+    return {"nproc": os.cpu_count(), "affinity": len(os.sched_getaffinity(0)), "cpu_model": model,
+            "cgroup_cpu_quota": quota}
 
 
 def cpu_baseline(workload: str, target_s: float):

@@ -8,7 +8,7 @@
 // from the first boundary at or past theta(i, q) = i S + q S / R (for q > 0
 // the first boundary the walk met there, see below) to the next lane's start.
 //
-//  A  k_sync: one workgroup over 256 segments staged in LDS (segwalk.hpp).
+//  A  k_split_sync: one workgroup over 256 segments staged in LDS (segwalk.hpp).
 //     Each lane walks its segment speculatively from i S (multi-code steps
 //     through the walk table), noting a merge sample every kSampBits bits and
 //     a CHECKPOINT at the first step end at or past each theta(i, q): the
@@ -27,7 +27,7 @@
 //     from the new path, the rest keep their positions with counts shifted.
 //     Rounds until no exit changes (decided on the device), then a sweep.
 //  scan of the block letters -> each block's first output letter.
-//  B  k_emit: one workgroup over 256 lanes: their bits staged in LDS, every
+//  B  k_split_emit: one workgroup over 256 lanes: their bits staged in LDS, every
 //     lane decodes its letters from its settled start (u16 single-symbol
 //     table, 64 letters per pass kept in registers by v_perm) into the
 //     block's LDS image at its offset, and the image leaves as coalesced
@@ -93,7 +93,7 @@ __device__ __forceinline__ void mark_ck(uint32_t (&ck)[kSplitRmax - 1], uint32_t
 }
 
 template <bool SLOW>
-__global__ __launch_bounds__(kT) void k_sync(SplitArgs a) {
+__global__ __launch_bounds__(kT) void k_split_sync(SplitArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     __shared__ uint64_t ex_l[kT];
     __shared__ uint32_t bt[kSplitRmax];
@@ -513,7 +513,7 @@ __device__ __forceinline__ void put_run(uint8_t* img, uint32_t F, const uint32_t
 }
 
 template <bool SLOW>
-__global__ __launch_bounds__(kT) void k_emit(SplitArgs a) {
+__global__ __launch_bounds__(kT) void k_split_emit(SplitArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     __shared__ uint32_t wtot[kT / 64];
     const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
@@ -667,7 +667,7 @@ hipError_t launch_split_sync(const SplitArgs& a, hipStream_t s) {
     if (a.max_len > 32 || a.seg_bits > 2048 || (1u << a.lg_r) > kSplitRmax || a.nsamp > kSampMax || !a.stab)
         return hipErrorInvalidValue;
     const bool slow = a.max_len > a.stab_bits;
-    hipLaunchKernelGGL(slow ? k_sync<true> : k_sync<false>, dim3((a.nseg + kT - 1) / kT), dim3(kT),
+    hipLaunchKernelGGL(slow ? k_split_sync<true> : k_split_sync<false>, dim3((a.nseg + kT - 1) / kT), dim3(kT),
                        split_sync_lds_bytes(a), s, a);
     return hipGetLastError();
 }
@@ -689,7 +689,7 @@ hipError_t launch_split_emit(const SplitArgs& a, hipStream_t s) {
         split_emit_lds_bytes(a) > 160 * 1024)
         return hipErrorInvalidValue;
     const bool slow = a.max_len > a.stab_bits;
-    hipLaunchKernelGGL(slow ? k_emit<true> : k_emit<false>, dim3(split_blocks(a.nseg, a.lg_r)), dim3(kT),
+    hipLaunchKernelGGL(slow ? k_split_emit<true> : k_split_emit<false>, dim3(split_blocks(a.nseg, a.lg_r)), dim3(kT),
                        split_emit_lds_bytes(a), s, a);
     return hipGetLastError();
 }

@@ -165,15 +165,15 @@ struct IndexlessArgs {
     uint32_t l2_words;
 };
 // Index-free decode split at the scan (isplit.hip), codes <= 32 bits:
-//   k_sync   (A): speculative walk of every S-bit segment + in-workgroup
-//                 fix-up; writes, per LANE (a segment cut into R pieces at
-//                 the first boundaries at or past i S + q S / R), a record
-//                 {start - theta, letter count}, the segment's exit and the
-//                 letter totals of the output blocks (256 lanes each)
-//   k_fix_rec    : cross-workgroup fix-up of the records (rounds + sweep)
+//   k_split_sync (A): speculative walk of every S-bit segment + in-workgroup
+//                     fix-up; writes, per LANE (a segment cut into R pieces
+//                     near i S + q S / R), a record {start - theta, letter
+//                     count}, the segment's exit and the letter totals of the
+//                     output blocks (256 lanes each)
+//   k_fix_rec         cross-workgroup fix-up of the records (rounds + sweep)
 //   scan of the block totals
-//   k_emit   (B): each lane decodes its letters from its settled start into
-//                 the block's LDS image; coalesced 16-B stores
+//   k_split_emit (B): each lane decodes its letters from its settled start
+//                     into the block's LDS image; coalesced 16-B stores
 constexpr uint32_t kSplitRmax = 8;
 struct SplitArgs {
     const uint8_t* comp;          // 16-B aligned
@@ -188,15 +188,15 @@ struct SplitArgs {
     uint32_t max_len;             // <= 32
     const uint16_t* stab;         // single-symbol table (letter, length)
     uint32_t stab_bits;
-    const uint16_t* wtab;         // walk table (k_sync); k_emit reads stab
-    const uint32_t* l2;           // level-2 length table (k_sync's slow steps; null: lut)
+    const uint16_t* wtab;         // walk table (k_split_sync); k_split_emit reads stab
+    const uint32_t* l2;           // level-2 length table (k_split_sync's slow steps; null: lut)
     uint32_t l2_words;
     uint32_t* rec;                // [nseg << lg_r] (start - theta) | count << 10
     uint8_t* xd;                  // [nseg] exit - segment end (< 32)
     unsigned long long* btot;     // [nblk] letters per output block (256 lanes)
-    uint32_t* fixlist;            // segments k_sync left unsettled (besides every workgroup's first)
+    uint32_t* fixlist;            // segments k_split_sync left unsettled (besides every workgroup's first)
     unsigned int* flags;          // [kFixRounds + 1] as IndexlessArgs::flags
-    // k_emit
+    // k_split_emit
     const unsigned long long* boff;  // [nblk + 1] exclusive scan of btot
     uint8_t* out;                 // 16-B aligned, boff[nblk] letters
     uint32_t stage_bytes;         // LDS stage per workgroup (a multiple of 16)

@@ -1126,7 +1126,7 @@ Status indexless_mark(huff_ctx* ctx, IndexlessSync& st, DevBuf& sub_abs, uint32_
 }
 
 // build-time policy of the split decoder (A/B builds, tools/build_variant.sh):
-// the letters a lane is sized for, and the longest segment (k_sync stages 256
+// the letters a lane is sized for, and the longest segment (k_split_sync stages 256
 // segments: 1,100 bits keep its LDS at 3 workgroups per CU)
 #ifndef SPLIT_LANE_LETTERS
 #define SPLIT_LANE_LETTERS 46.0
@@ -1135,9 +1135,9 @@ Status indexless_mark(huff_ctx* ctx, IndexlessSync& st, DevBuf& sub_abs, uint32_
 #define SPLIT_SEG_MAX 1100.0
 #endif
 
-// The split index-free decoder (isplit.hip) for codes <= 32 bits: k_sync
+// The split index-free decoder (isplit.hip) for codes <= 32 bits: k_split_sync
 // (speculative walk + in-group fix-up -> lane records), k_fix_rec, the scan
-// of the block letters, one host read of the total, k_emit. *done = false
+// of the block letters, one host read of the total, k_split_emit. *done = false
 // when the stream does not fit its limits (the caller takes the older path).
 static Status decode_split(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_bytes, uint64_t valid_bits,
                            const huff_tree* t, const DecTables* dt, DevBuf& out, uint64_t* nsym, uint8_t* d_user,
@@ -1152,7 +1152,7 @@ static Status decode_split(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_b
     }
     if (g == 0) g = 1;
     mean = std::max(mean, 1.0);
-    // lanes of ~SPLIT_LANE_LETTERS letters (k_emit holds a lane's letters in
+    // lanes of ~SPLIT_LANE_LETTERS letters (k_split_emit holds a lane's letters in
     // one 64-letter register batch; a block with a longer lane writes bytes
     // straight to HBM): R lanes per segment, the fewest with R x that
     // lane's bits >= 640 (segments long enough that the fix-up walks stay a
@@ -1161,7 +1161,7 @@ static Status decode_split(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_b
     const double lane_bits = SPLIT_LANE_LETTERS * mean;
     uint32_t lg_r = 0;
     while ((1u << lg_r) < dev::kSplitRmax && static_cast<double>(1u << lg_r) * lane_bits < 640.0) ++lg_r;
-    // k_sync at 4 workgroups per CU: its tables, the stage of 256 segments
+    // k_split_sync at 4 workgroups per CU: its tables, the stage of 256 segments
     // and ~2 KiB of static LDS within 40 KiB (where the tables leave room)
     const bool l2 = dt->l2words && !std::getenv("HUFF_NO_L2");
     const double tw_bytes = 4.0 * (((((1u << dt->sbits) + 1) / 2 + 3) & ~3u) + (l2 ? dt->l2words : 0) + 3) / 4 * 4;
@@ -1198,7 +1198,7 @@ static Status decode_split(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_b
         a.l2 = static_cast<const uint32_t*>(ctx->d_lut.p) + dt->l2off;
         a.l2_words = dt->l2words;
     }
-    // k_emit's stage: the block's 256 lanes from its first segment's 16-B
+    // k_split_emit's stage: the block's 256 lanes from its first segment's 16-B
     // granule, the last lane's overrun past the next block's first theta
     // (< 300 bits), a code and the window's read-ahead
     a.stage_bytes = static_cast<uint32_t>((((256 * S) >> lg_r) + 128 + 512 + 128 + 7) / 8 + 15) & ~15u;

@@ -3,8 +3,8 @@
 Streams are written by the CPU restatement (oracle/, comp.rs:419-451) with no
 restart index, as the reference writes every CompressData and .hff payload,
 and decoded on the device through huff_dev_decompress (comp.rs:487-519) with
-HUFF_SPLIT=1, the opt-in path for codes <= 32 bits (k_sync -> k_fix_rec ->
-scan -> k_emit; measured slower than the default sample + mark path, DESIGN
+HUFF_SPLIT=1, the opt-in path for codes <= 32 bits (k_split_sync -> k_fix_rec ->
+scan -> k_split_emit; measured slower than the default sample + mark path, DESIGN
 §11).
 The cases cover its paths: lanes merging with their speculative walk, codes
 longer than the 12-bit table, 1-8 lanes per segment, lanes past 64 letters,
