@@ -548,6 +548,7 @@ __global__ __launch_bounds__(kT) void k_split_emit(SplitArgs a) {
             uint4 v[4];
 #pragma unroll
             for (int k = 0; k < 4; ++k) v[k] = buf_ld16(rs, (p0 + k * kT) * 16);
+            keep_loads(v);
 #pragma unroll
             for (int k = 0; k < 4; ++k)
                 if (p0 + k * kT < np)

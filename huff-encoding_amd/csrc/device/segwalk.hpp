@@ -30,6 +30,14 @@ struct Staged {
 // lookahead may read, come back zero): the one-dword-at-a-time loop this
 // replaces waited out a memory latency per dword. Words stay in stream byte
 // order (the cursor swaps them).
+// the loads' results materialised here (an empty asm using them), so none
+// is sunk into a later conditional use
+template <int N>
+__device__ __forceinline__ void keep_loads(uint4 (&v)[N]) {
+#pragma unroll
+    for (int k = 0; k < N; ++k) asm volatile("" : "+v"(v[k].x), "+v"(v[k].y), "+v"(v[k].z), "+v"(v[k].w));
+}
+
 template <class A>
 __device__ __forceinline__ Staged stage_block(const A& a, uint32_t* w) {
     constexpr uint32_t kT = 256;
@@ -48,6 +56,10 @@ __device__ __forceinline__ Staged stage_block(const A& a, uint32_t* w) {
         uint4 v[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k) v[k] = buf_ld16(rs, (p0 + k * kT) * 16);
+        // every load issued before the first store: without this the
+        // compiler sank a load into its store's branch, issued it after the
+        // wait for the others, and paid a second memory latency per stage
+        keep_loads(v);
 #pragma unroll
         for (int k = 0; k < 8; ++k)
             if (p0 + k * kT < np) w4[p0 + k * kT] = v[k];
