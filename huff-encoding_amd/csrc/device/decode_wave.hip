@@ -70,6 +70,18 @@ __device__ __forceinline__ Task task_info(const DecodeArgs& a, uint64_t t, uint3
     const uint32_t ls = lane * kLaneSym;
     k.cnt = ls >= k.nsym ? 0u : (k.nsym - ls < kLaneSym ? k.nsym - ls : kLaneSym);
     k.skip = 0;
+    // the task's end (the next task's first bit) first: a scalar load with no
+    // dependence on the lane's entry, so both are in flight together (read
+    // after the lane's entry it cost a second memory latency per task)
+    const uint64_t next = k.sym0 + kTaskSym;
+    uint64_t end;
+    if (a.sub_abs64) {
+        end = next < a.n ? a.sub_abs64[next / kIdx] : a.end_bit;
+    } else if (next < a.n) {
+        end = a.sub16 ? a.task_base[t + 1] : a.chunk_start[next / kChunk] + a.sub_bit[next / kIdx];
+    } else {
+        end = a.chunk_start[a.nchunks];
+    }
     if (a.sub_abs64) {  // index-free streams: absolute start bit of every 64th symbol (k_mark_lds)
         k.lane_bit = k.cnt ? a.sub_abs64[k.sym0 / kIdx + lane] : 0;
         if constexpr (SKIP) {
@@ -86,17 +98,8 @@ __device__ __forceinline__ Task task_info(const DecodeArgs& a, uint64_t t, uint3
     const uint32_t f_lo = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(k.lane_bit)));
     const uint32_t f_hi = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(k.lane_bit >> 32)));
     const uint64_t first = (static_cast<uint64_t>(f_hi) << 32) | f_lo;
-    const uint64_t next = k.sym0 + kTaskSym;
-    uint64_t end;
-    if (a.sub_abs64) {
-        end = next < a.n ? a.sub_abs64[next / kIdx] : a.end_bit;
-        if constexpr (SKIP)  // the next task's first bit lies within its skipped codes
-            if (next < a.n) end = (end & kSkipPosMask) + (end >> 48) * a.max_len;
-    } else if (next < a.n) {
-        end = a.sub16 ? a.task_base[t + 1] : a.chunk_start[next / kChunk] + a.sub_bit[next / kIdx];
-    } else {
-        end = a.chunk_start[a.nchunks];
-    }
+    if constexpr (SKIP)  // the next task's first bit lies within its skipped codes (used only now)
+        if (a.sub_abs64 && next < a.n) end = (end & kSkipPosMask) + (end >> 48) * a.max_len;
     k.end = end;
     k.b0 = (first >> 3) & ~15ull;
     uint64_t b1 = ((end + 7) >> 3) + 32;  // lookahead: window + the dword read ahead
