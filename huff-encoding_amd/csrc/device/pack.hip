@@ -101,6 +101,11 @@ __global__ __launch_bounds__(pack_waves<LONG>() * 64) void k_pack(PackArgs a) {
     for (uint32_t c = blockIdx.x * kWaves + wave; c < a.nchunks; c += a.grid * kWaves) {
         const uint64_t sym0 = static_cast<uint64_t>(c) * kChunk;
         const uint64_t nsym = (a.n - sym0 < kChunk) ? a.n - sym0 : kChunk;
+        // the 8 input bytes before the chunk (chunks start 64 KiB apart: an
+        // aligned load), read with the chunk's first loads for the shared
+        // first byte below (byte-by-byte reads there waited out a memory
+        // latency per byte)
+        const uint64_t prev8 = (lane == 0 && sym0 >= 8) ? *reinterpret_cast<const uint64_t*>(a.in + sym0 - 8) : 0;
         const uint64_t cs = a.chunk_start[c];
         const uint64_t ce = a.chunk_start[c + 1];
         uint64_t stage_bit0 = (cs >> 7) << 7;  // global bit of stage word 0's MSB (16-B aligned)
@@ -129,8 +134,8 @@ __global__ __launch_bounds__(pack_waves<LONG>() * 64) void k_pack(PackArgs a) {
             int64_t pos = static_cast<int64_t>(cs);
             for (uint32_t k = 1; k <= 8 && pos > floor8; ++k) {
                 uint8_t b;
-                if (sym0 >= k) {
-                    b = a.in[sym0 - k];
+                if (sym0 >= k) {  // sym0 is 0 or >= 64 KiB
+                    b = static_cast<uint8_t>(prev8 >> (8 * (8 - k)));
                 } else {
                     const uint32_t j = k - static_cast<uint32_t>(sym0);
                     if (j > a.prev_tail_len) break;
