@@ -18,6 +18,14 @@ namespace huff::dev {
 namespace {
 
 constexpr int kThreads = 256;
+// 16-B pieces per lane: a workgroup maps kThreads * 16 * kPieces bytes and
+// stages its 32 KiB table once for them. Same-box A/B (1 GiB, ms, pass 2 /
+// decode): 2 pieces 0.533 / 0.536, 4 0.373-0.378 / 0.381, 8 0.371-0.372 /
+// 0.360, 16 0.395-0.403 / 0.394-0.399
+#ifndef HUFF_BYTEMAP_PIECES
+#define HUFF_BYTEMAP_PIECES 8
+#endif
+constexpr int kPieces = HUFF_BYTEMAP_PIECES;
 
 __device__ __forceinline__ uint32_t map4(const uint32_t* tab, uint32_t w, uint32_t copy) {
     const uint32_t b0 = tab[((w & 0xFFu) << 5) | copy];
@@ -28,20 +36,20 @@ __device__ __forceinline__ uint32_t map4(const uint32_t* tab, uint32_t w, uint32
 }
 
 
-// One-shot grid: workgroup w maps the 16 KiB [w * 16 KiB, +16 KiB), lane t
-// the four 16-B pieces t, t+256, t+512, t+768 of it (each a coalesced 4 KiB
+// One-shot grid: workgroup w maps the 32 KiB [w * 32 KiB, +32 KiB), lane t
+// the kPieces 16-B pieces t, t+256, t+512, ... of it (each a coalesced 4 KiB
 // row per wave set). The data loads are issued before the table is staged in
 // LDS, so the table setup hides under the HBM latency.
 __global__ __launch_bounds__(kThreads) void k_bytemap(BytemapArgs a) {
     __shared__ __attribute__((aligned(16))) uint32_t tab[256 * 32];
     const uint32_t t = threadIdx.x, copy = t & 31;
     const uint64_t nvec = a.n / 16;
-    const uint64_t v0 = static_cast<uint64_t>(blockIdx.x) * (kThreads * 4) + t;
+    const uint64_t v0 = static_cast<uint64_t>(blockIdx.x) * (kThreads * kPieces) + t;
     const uint4* src = reinterpret_cast<const uint4*>(a.src);
     uint4* dst = reinterpret_cast<uint4*>(a.dst);
-    uint4 x[4];
+    uint4 x[kPieces];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < kPieces; ++k) {
         const uint64_t v = v0 + k * kThreads;
         x[k] = v < nvec ? ld_nt(src + v) : make_uint4(0, 0, 0, 0);
     }
@@ -55,7 +63,7 @@ __global__ __launch_bounds__(kThreads) void k_bytemap(BytemapArgs a) {
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): table stores done; data loads stay in flight
     __builtin_amdgcn_s_barrier();
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < kPieces; ++k) {
         const uint64_t v = v0 + k * kThreads;
         if (v < nvec) {
             uint4 y;
@@ -122,7 +130,7 @@ hipError_t launch_arith_index(uint64_t n, uint32_t nchunks, uint64_t base_bits, 
 hipError_t launch_bytemap(const BytemapArgs& a, hipStream_t s) {
     if (a.n == 0 && !a.chunk_start) return hipSuccess;
     const uint64_t nvec = a.n / 16;
-    uint64_t blocks = (nvec + kThreads * 4 - 1) / (kThreads * 4);
+    uint64_t blocks = (nvec + kThreads * kPieces - 1) / (kThreads * kPieces);
     if (blocks < 1) blocks = 1;
     if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_bytemap, dim3(static_cast<uint32_t>(blocks)), dim3(kThreads), 0, s, a);
