@@ -19,11 +19,14 @@ namespace {
 
 constexpr int kThreads = 256;
 // 16-B pieces per lane: a workgroup maps kThreads * 16 * kPieces bytes and
-// stages its 32 KiB table once for them. Same-box A/B (1 GiB, ms, pass 2 /
-// decode): 2 pieces 0.533 / 0.536, 4 0.373-0.378 / 0.381, 8 0.371-0.372 /
-// 0.360, 16 0.395-0.403 / 0.394-0.399
+// stages its 32 KiB table once for them. Same-box A/B, 1 GiB: alone
+// (tools/kbench.py, pass 2 / decode ms) 2 pieces 0.533 / 0.536, 4 0.373-0.378
+// / 0.381, 8 0.371-0.372 / 0.360, 16 0.395-0.403 / 0.394-0.399; but inside
+// the bench's step (hist, pass 2, decode back to back) 4 pieces 0.351 /
+// 0.350 against 8 pieces 0.380 / 0.367 (1150 vs 1093 GB/s, 3 runs each):
+// 4 it is
 #ifndef HUFF_BYTEMAP_PIECES
-#define HUFF_BYTEMAP_PIECES 8
+#define HUFF_BYTEMAP_PIECES 4
 #endif
 constexpr int kPieces = HUFF_BYTEMAP_PIECES;
 
@@ -36,9 +39,9 @@ __device__ __forceinline__ uint32_t map4(const uint32_t* tab, uint32_t w, uint32
 }
 
 
-// One-shot grid: workgroup w maps the 32 KiB [w * 32 KiB, +32 KiB), lane t
-// the kPieces 16-B pieces t, t+256, t+512, ... of it (each a coalesced 4 KiB
-// row per wave set). The data loads are issued before the table is staged in
+// One-shot grid: workgroup w maps the 16 KiB [w * 16 KiB, +16 KiB), lane t
+// the kPieces (4) 16-B pieces t, t+256, t+512, t+768 of it (each a coalesced
+// 4 KiB row per wave set). The data loads are issued before the table is staged in
 // LDS, so the table setup hides under the HBM latency.
 __global__ __launch_bounds__(kThreads) void k_bytemap(BytemapArgs a) {
     __shared__ __attribute__((aligned(16))) uint32_t tab[256 * 32];
