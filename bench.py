@@ -63,6 +63,25 @@ def enwik8_path():
     return p if p and os.path.isfile(p) else None
 
 
+def cgroup_cpu_quota(root: str = "/sys/fs/cgroup"):
+    """CPUs' worth of time the cgroup grants (cgroup v2 cpu.max "<quota>
+    <period>", else v1 cfs_quota_us / cfs_period_us); None when unlimited or
+    unknown. A mask of many threads may still get only this many CPUs."""
+    try:
+        with open(os.path.join(root, "cpu.max")) as f:
+            q, per = f.read().split()[:2]
+            return None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    try:  # cgroup v1
+        with open(os.path.join(root, "cpu", "cpu.cfs_quota_us")) as f, \
+                open(os.path.join(root, "cpu", "cpu.cfs_period_us")) as g:
+            q, per = int(f.read()), int(g.read())
+            return round(q / per, 2) if q > 0 else None
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_info():
     model = None
     try:
@@ -73,20 +92,7 @@ def cpu_info():
                     break
     except OSError:
         pass
-    # the cgroup CPU quota (cgroup v2 cpu.max "<quota> <period>"): a mask of
-    # many threads may still get only this many CPUs' worth of time
-    quota = None
-    try:
-        with open("/sys/fs/cgroup/cpu.max") as f:
-            q, per = f.read().split()[:2]
-            quota = None if q == "max" else round(int(q) / int(per), 2)
-    except (OSError, ValueError):
-        try:  # cgroup v1
-            with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f, open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as g:
-                q, per = int(f.read()), int(g.read())
-                quota = round(q / per, 2) if q > 0 else None
-        except (OSError, ValueError):
-            pass
+    quota = cgroup_cpu_quota()
     return {"nproc": os.cpu_count(), "affinity": len(os.sched_getaffinity(0)), "cpu_model": model,
             "cgroup_cpu_quota": quota}
 
