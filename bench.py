@@ -206,38 +206,40 @@ class Setup:
         if world > 1 and self.nccl:
             self.comm, self.comm_note = self.native_comm()
         self.dx = mgpu.DeviceExchange(self.dev) if world > 1 and self.nccl and self.comm is None else None
-        self.flush = (torch.empty(512 << 20, dtype=torch.uint8, device="cuda")
-                      if args.scaling == "strong" else None)
+        self._flush = None
         self.ceil = None
         self.rccl_world = self.observed_world()
 
+    def flush_buffer(self):
+        """512 MiB rewritten before each strong-scaling step: no shard stays
+        in the 256 MiB Infinity Cache"""
+        if self._flush is None:
+            self._flush = torch.empty(512 << 20, dtype=torch.uint8, device="cuda")
+        return self._flush
+
     def observed_world(self):
         """the world size RCCL itself reports (ncclCommCount through
-        huff_comm_world) on the communicator the step uses — at N = 1 a
-        world-1 communicator made for the readout — checked equal on every
-        rank; with gloo (rehearsal) torch's group size, labelled so"""
+        huff_comm_world) on the communicator the step uses, checked equal on
+        every rank; at N = 1 the step runs no collective (said so); with gloo
+        (rehearsal) torch's group size, labelled so"""
+        if self.world == 1:
+            return {"world": 1, "source": "single rank: the step runs no collective"}
         if not self.nccl:
-            return {"world": dist.get_world_size() if self.world > 1 else 1,
-                    "source": "torch.distributed gloo group (no RCCL: rehearsal)"}
+            return {"world": dist.get_world_size(), "source": "torch.distributed gloo group (no RCCL: rehearsal)"}
+        if self.comm is None:
+            return {"world": None, "source": "no library communicator (torch RCCL all_gather)"}
+        # every rank reaches the all_reduce below, also one whose readout
+        # failed (a sentinel), so no rank blocks in it
+        note = None
         try:
-            if self.comm is not None:
-                w, r = self.comm.observed_world()
-            elif self.world == 1:
-                c = mgpu.NativeComm(self.ctx, 1, 0, mgpu.NativeComm.unique_id())
-                try:
-                    w, r = c.observed_world()
-                finally:
-                    c.close()
-            else:
-                return {"world": None, "source": "no library communicator (torch RCCL all_gather)"}
-        except Exception as e:  # reported, not fatal: the step does not depend on it
-            return {"world": None, "source": f"huff_comm_world failed: {e}"}
-        if self.world > 1:
-            t = torch.tensor([w, -w, int(r != self.rank)], device=self.dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            lo, hi, bad = -int(t[1].item()), int(t[0].item()), int(t[2].item())
-            if lo != hi or bad:
-                return {"world": None, "source": f"ranks disagree: RCCL world {lo}..{hi}, rank mismatch {bad}"}
+            w, r = self.comm.observed_world()
+        except Exception as e:
+            w, r, note = -1, -1, f"huff_comm_world failed on rank {self.rank}: {e}"
+        t = torch.tensor([w, -w, int(r != self.rank)], device=self.dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        lo, hi, bad = -int(t[1].item()), int(t[0].item()), int(t[2].item())
+        if note or lo != hi or bad or lo < 1:
+            return {"world": None, "source": note or f"ranks disagree: RCCL world {lo}..{hi}, rank mismatch {bad}"}
         return {"world": w, "source": "ncclCommCount / ncclCommUserRank via huff_comm_world"}
 
     def native_comm(self):
@@ -295,8 +297,11 @@ def make_input(s: Setup, kind: str, n: int):
     return x, src
 
 
-def run_workload(s: Setup, kind: str, n: int, with_cpu: bool):
+def run_workload(s: Setup, kind: str, n: int, with_cpu: bool, strong: bool = False):
+    """one bench record: `strong` times each step alone after an Infinity
+    Cache flush (SURVEY §8d's strong-scaling curve), else back to back"""
     args, world, rank = s.args, s.world, s.rank
+    flush = s.flush_buffer() if strong else None
     ctx = s.ctx
     x, data_src = make_input(s, kind, n)
     job = H.EncodeJob(ctx, x.data_ptr(), n)
@@ -344,7 +349,7 @@ def run_workload(s: Setup, kind: str, n: int, with_cpu: bool):
     ctx.set_timing(True)
     ctx.reset_timing()
     bits, tree = 0, None
-    if s.flush is None:
+    if flush is None:
         s.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -356,7 +361,7 @@ def run_workload(s: Setup, kind: str, n: int, with_cpu: bool):
     else:
         elapsed = 0.0
         for i in range(args.steps):
-            s.flush.fill_(i & 0xFF)  # torch's stream: outside the library's kernel timing
+            flush.fill_(i & 0xFF)  # torch's stream: outside the library's kernel timing
             s.barrier()
             torch.cuda.synchronize()
             t0 = time.perf_counter()
@@ -450,7 +455,7 @@ def run_workload(s: Setup, kind: str, n: int, with_cpu: bool):
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 4),
         "higher_is_better": True,
-        "scaling": args.scaling,
+        "scaling": "strong" if strong else "weak",
         "vs_baseline": None,
         "dtype": "u8",
         "data": data_src,
@@ -555,17 +560,55 @@ def file_path_bench(s: Setup, kind: str, n: int, steps: int):
         shutil.rmtree(d, ignore_errors=True)
 
 
+def free_port() -> int:
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def rank_guard(args, argv=None, environ=None, spawn=None):
+    """--gpus N means N ranks. Without a launcher (no WORLD_SIZE) and N > 1,
+    start N rank processes as children (torch.distributed.run on 127.0.0.1)
+    and return the exit code to exit with; a launcher whose world differs
+    from --gpus is an error (a wasted lease otherwise). Returns None when
+    this process is one of the N ranks. Runs before anything touches the GPU
+    (no device query, no exec: the ranks are children)."""
+    import subprocess
+    environ = os.environ if environ is None else environ
+    argv = sys.argv[1:] if argv is None else argv
+    ws = environ.get("WORLD_SIZE")
+    if ws is None:
+        if args.gpus <= 1:
+            return None
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+               "--master-addr", "127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__)] + list(argv)
+        print(f"bench.py: --gpus {args.gpus} without a launcher: starting {args.gpus} ranks", file=sys.stderr,
+              flush=True)
+        return (spawn or subprocess.call)(cmd)
+    if int(ws) != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={ws} ranks; refusing to "
+              f"report a {ws}-rank line as {args.gpus}", file=sys.stderr, flush=True)
+        return 2
+    return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="uniform", choices=sorted(SEEDS))
-    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"])
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+                    help="the main line's mode; the other mode is reported under 'scaling_other'")
     ap.add_argument("--bytes-per-gpu", type=int, default=1 << 30, help="weak scaling: bytes per rank")
     ap.add_argument("--total-bytes", type=int, default=1 << 30, help="strong scaling: bytes over all ranks")
     ap.add_argument("--side", default="zipf", choices=["zipf", "text", "none"],
                     help="N=1: a second workload reported under 'side' (configs[2] by default)")
+    ap.add_argument("--no-general", action="store_true",
+                    help="N=1: skip the 'general' record (the headline workload through the general "
+                         "scan + bit-pack kernels, HUFF_DISABLE_FIXED8=1)")
+    ap.add_argument("--no-other-scaling", action="store_true", help="skip the 'scaling_other' record")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--file-path", default="zipf", choices=["zipf", "text", "uniform", "none"],
                     help="N=1: time the .hff file path on a 1 GiB file of this workload")
@@ -574,10 +617,17 @@ def main():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: rehearse the N>1 path with several ranks on one GPU")
     args = ap.parse_args()
+    rc = rank_guard(args)
+    if rc is not None:
+        sys.exit(rc)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
+    ndev = torch.cuda.device_count()
+    if world > 1 and args.dist_backend == "nccl" and ndev < world:
+        print(f"bench.py: {world} RCCL ranks need {world} GPUs, this node shows {ndev}", file=sys.stderr, flush=True)
+        sys.exit(2)
+    local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, ndev)
     torch.cuda.set_device(local)
     if world > 1:
         if args.dist_backend == "nccl":
@@ -585,16 +635,40 @@ def main():
         else:
             dist.init_process_group("gloo")
     s = Setup(args, world, rank, local)
-    if args.scaling == "strong":
-        n = (args.total_bytes // world) & ~0xFFFF
-    else:
-        n = args.bytes_per_gpu
+    n_weak = args.bytes_per_gpu
+    n_strong = (args.total_bytes // world) & ~0xFFFF
+    strong = args.scaling == "strong"
     with_cpu = rank == 0 and world == 1 and not args.no_cpu_baseline
-    result = run_workload(s, args.workload, n, with_cpu)
+    result = run_workload(s, args.workload, n_strong if strong else n_weak, with_cpu, strong)
+    if not args.no_other_scaling:
+        # the 1/2/4/8 curve of the metric is strong scaling of 1 GiB
+        # (1 GiB / N per rank, caches flushed); the weak line (1 GiB per rank)
+        # beside it, whichever is the main line
+        o = run_workload(s, args.workload, n_weak if strong else n_strong, False, not strong)
+        result["scaling_other"] = {k: o[k] for k in ("scaling", "value", "unit", "ms_per_step", "n_gpus", "steps",
+                                                     "kernels", "roofline", "e2e")}
+        result["scaling_other"]["bytes_per_gpu"] = o["config"]["bytes_per_gpu"]
+        result["scaling_other"]["global_bytes"] = o["config"]["global_bytes"]
+    if world == 1 and not args.no_general:
+        # the north-star kernels (per-byte lookup + exclusive scan + bit-pack
+        # and the bit decoder) on the headline workload: the byte map off
+        prev = os.environ.get("HUFF_DISABLE_FIXED8")
+        os.environ["HUFF_DISABLE_FIXED8"] = "1"
+        try:
+            g = run_workload(s, args.workload, n_strong if strong else n_weak, False, strong)
+        finally:
+            if prev is None:
+                del os.environ["HUFF_DISABLE_FIXED8"]
+            else:
+                os.environ["HUFF_DISABLE_FIXED8"] = prev
+        result["general"] = {k: g[k] for k in ("value", "unit", "ms_per_step", "kernels", "roofline", "e2e",
+                                               "host_gap_ms")}
+        result["general"]["kernel_path"] = g["config"]["kernel_path"]
+        result["general"]["note"] = "the headline workload with HUFF_DISABLE_FIXED8=1 (general kernels)"
     if world == 1 and args.side != "none" and args.side != args.workload:
-        result["side"] = {args.side: run_workload(s, args.side, n, with_cpu)}
+        result["side"] = {args.side: run_workload(s, args.side, n_weak, with_cpu)}
     if world == 1 and args.file_path != "none":
-        result["file_path"] = file_path_bench(s, args.file_path, n, 2)
+        result["file_path"] = file_path_bench(s, args.file_path, n_weak, 2)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if s.comm is not None:

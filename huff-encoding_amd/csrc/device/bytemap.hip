@@ -57,11 +57,17 @@ __global__ __launch_bounds__(kThreads) void k_bytemap(BytemapArgs a) {
         x[k] = v < nvec ? ld_nt(src + v) : make_uint4(0, 0, 0, 0);
     }
     __builtin_amdgcn_sched_barrier(0);
-    {  // lane t stages entry t into its 32 copies (one 128-B run)
-        const uint32_t e = a.map[t];
-        uint4* row = reinterpret_cast<uint4*>(tab + (t << 5));
+    {  // store i of lane t fills the 16-B piece i * 256 + t (entry (i * 256 + t) / 8):
+       // a wave's ds_write_b128 covers 1 KiB contiguous, so every 8-lane group
+       // spans all 32 banks. (Lane t writing its own 128-B row put each group's
+       // 8 lanes on the same 4 banks: 8-way conflicts, 117 M conflict cycles
+       // per GiB, 70 % of the kernel's LDS cycles.)
+        uint4* p = reinterpret_cast<uint4*>(tab);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) row[i] = make_uint4(e, e, e, e);
+        for (int i = 0; i < 8; ++i) {
+            const uint32_t e = a.map[i * 32 + (t >> 3)];
+            p[i * kThreads + t] = make_uint4(e, e, e, e);
+        }
     }
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): table stores done; data loads stay in flight
     __builtin_amdgcn_s_barrier();

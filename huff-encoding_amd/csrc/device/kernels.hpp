@@ -164,52 +164,6 @@ struct IndexlessArgs {
     const uint32_t* l2;
     uint32_t l2_words;
 };
-// Index-free decode split at the scan (isplit.hip), codes <= 32 bits:
-//   k_split_sync (A): speculative walk of every S-bit segment + in-workgroup
-//                     fix-up; writes, per LANE (a segment cut into R pieces
-//                     near i S + q S / R), a record {start - theta, letter
-//                     count}, the segment's exit and the letter totals of the
-//                     output blocks (256 lanes each)
-//   k_fix_rec         cross-workgroup fix-up of the records (rounds + sweep)
-//   scan of the block totals
-//   k_split_emit (B): each lane decodes its letters from its settled start
-//                     into the block's LDS image; coalesced 16-B stores
-constexpr uint32_t kSplitRmax = 8;
-struct SplitArgs {
-    const uint8_t* comp;          // 16-B aligned
-    uint64_t comp_bytes;
-    uint64_t valid_bits;          // B
-    uint64_t seg_bits;            // S (<= 2048, a multiple of the gcd of the code lengths)
-    uint64_t nseg;
-    uint32_t lg_r;                // R = 1 << lg_r lanes per segment (R <= kSplitRmax)
-    uint32_t nsamp;               // merge samples per segment (every kSampBits bits; <= kSampMax)
-    const uint32_t* lut;          // multi-level table (codes longer than stab_bits)
-    uint32_t lut_bits;
-    uint32_t max_len;             // <= 32
-    const uint16_t* stab;         // single-symbol table (letter, length)
-    uint32_t stab_bits;
-    const uint16_t* wtab;         // walk table (k_split_sync); k_split_emit reads stab
-    const uint32_t* l2;           // level-2 length table (k_split_sync's slow steps; null: lut)
-    uint32_t l2_words;
-    uint32_t* rec;                // [nseg << lg_r] (start - theta) | count << 10
-    uint8_t* xd;                  // [nseg] exit - segment end (< 32)
-    unsigned long long* btot;     // [nblk] letters per output block (256 lanes)
-    uint32_t* fixlist;            // segments k_split_sync left unsettled (besides every workgroup's first)
-    unsigned int* flags;          // [kFixRounds + 1] as IndexlessArgs::flags
-    // k_split_emit
-    const unsigned long long* boff;  // [nblk + 1] exclusive scan of btot
-    uint8_t* out;                 // 16-B aligned, boff[nblk] letters
-    uint32_t stage_bytes;         // LDS stage per workgroup (a multiple of 16)
-    uint32_t img_bytes;           // LDS output image per workgroup (a multiple of 16)
-    unsigned long long* end_bit;  // may be null: the bit after the last complete code
-};
-__host__ __device__ inline uint64_t split_blocks(uint64_t nseg, uint32_t lg_r) { return ((nseg << lg_r) + 255) / 256; }
-size_t split_sync_lds_bytes(const SplitArgs& a);
-size_t split_emit_lds_bytes(const SplitArgs& a);
-hipError_t launch_split_sync(const SplitArgs& a, hipStream_t s);
-hipError_t launch_split_fix(const SplitArgs& a, hipStream_t s);  // round 0 (list), rounds, sweep
-hipError_t launch_split_emit(const SplitArgs& a, hipStream_t s);
-
 constexpr uint32_t kSampBits = 128;
 constexpr uint32_t kSampMax = 8;  // samples kept per segment (nsamp <= kSampMax)
 constexpr uint32_t kNoMerge = 0xFFFFFFFFu;

@@ -61,14 +61,6 @@ bool fixed8_disabled() {
     return e && *e && *e != '0';
 }
 
-// HUFF_SPLIT=1: index-free byte streams take the split decoder (isplit.hip)
-// instead of the sample + mark path (measured slower on the GPU: DESIGN §11;
-// the tests run both)
-bool split_enabled() {
-    const char* e = std::getenv("HUFF_SPLIT");  // read per call: tests flip it
-    return e && *e && *e != '0';
-}
-
 uint32_t decode_check_mode() {
     const char* e = std::getenv("HUFF_DEC_VARIANT");  // read per call: tests flip it
     if (!e) return 0;
@@ -1125,139 +1117,6 @@ Status indexless_mark(huff_ctx* ctx, IndexlessSync& st, DevBuf& sub_abs, uint32_
     return Status::ok();
 }
 
-// build-time policy of the split decoder (A/B builds, tools/build_variant.sh):
-// the letters a lane is sized for, and the longest segment (k_split_sync stages 256
-// segments: 1,100 bits keep its LDS at 3 workgroups per CU)
-#ifndef SPLIT_LANE_LETTERS
-#define SPLIT_LANE_LETTERS 46.0
-#endif
-#ifndef SPLIT_SEG_MAX
-#define SPLIT_SEG_MAX 1100.0
-#endif
-
-// The split index-free decoder (isplit.hip) for codes <= 32 bits: k_split_sync
-// (speculative walk + in-group fix-up -> lane records), k_fix_rec, the scan
-// of the block letters, one host read of the total, k_split_emit. *done = false
-// when the stream does not fit its limits (the caller takes the older path).
-static Status decode_split(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_bytes, uint64_t valid_bits,
-                           const huff_tree* t, const DecTables* dt, DevBuf& out, uint64_t* nsym, uint8_t* d_user,
-                           size_t user_cap, unsigned long long* d_end, bool* done) {
-    *done = false;
-    if (dt->maxdepth > 32 || !dt->sbits) return Status::ok();
-    uint32_t g = 0;
-    double mean = 0;
-    for (const LeafCode& lc : t->t.leaves()) {
-        g = std::gcd(g, lc.len);
-        mean += std::ldexp(static_cast<double>(lc.len), -static_cast<int>(lc.len));  // ~ bits per letter
-    }
-    if (g == 0) g = 1;
-    mean = std::max(mean, 1.0);
-    // lanes of ~SPLIT_LANE_LETTERS letters (k_split_emit holds a lane's letters in
-    // one 64-letter register batch; a block with a longer lane writes bytes
-    // straight to HBM): R lanes per segment, the fewest with R x that
-    // lane's bits >= 640 (segments long enough that the fix-up walks stay a
-    // small part of them), S = R lanes' bits in [256, SPLIT_SEG_MAX], a
-    // multiple of the gcd g of the code lengths
-    const double lane_bits = SPLIT_LANE_LETTERS * mean;
-    uint32_t lg_r = 0;
-    while ((1u << lg_r) < dev::kSplitRmax && static_cast<double>(1u << lg_r) * lane_bits < 640.0) ++lg_r;
-    // k_split_sync at 4 workgroups per CU: its tables, the stage of 256 segments
-    // and ~2 KiB of static LDS within 40 KiB (where the tables leave room)
-    const bool l2 = dt->l2words && !std::getenv("HUFF_NO_L2");
-    const double tw_bytes = 4.0 * (((((1u << dt->sbits) + 1) / 2 + 3) & ~3u) + (l2 ? dt->l2words : 0) + 3) / 4 * 4;
-    const double s_lds = (40960.0 - 2112.0 - tw_bytes - 144.0) / 32.0;
-    const double seg_max = s_lds >= 640.0 ? std::min<double>(s_lds, SPLIT_SEG_MAX) : SPLIT_SEG_MAX;
-    const uint64_t want = static_cast<uint64_t>(
-        std::min<double>(std::max<double>(static_cast<double>(1u << lg_r) * lane_bits, 256.0), seg_max));
-    // preferring S = 32 mod 64 within 64 bits below (an odd dword stride
-    // between the lanes' stage reads)
-    uint64_t S = std::max<uint64_t>(g, want / g * g);
-    for (uint64_t c = S; c + 64 > S && c >= g; c -= g)
-        if (c % 64 == 32) {
-            S = c;
-            break;
-        }
-    if (S < 256 || S < 2 * dt->maxdepth) return Status::ok();
-    const uint64_t nseg = (valid_bits + S - 1) / S;
-    if (nseg > 0xFFFFFFFFull / dev::kSplitRmax) return Status::ok();
-    dev::SplitArgs a{};
-    a.comp = d_comp;
-    a.comp_bytes = comp_bytes;
-    a.valid_bits = valid_bits;
-    a.seg_bits = S;
-    a.nseg = nseg;
-    a.lg_r = lg_r;
-    a.nsamp = std::min<uint32_t>(dev::kSampMax, static_cast<uint32_t>((S - 1) / dev::kSampBits));
-    a.lut = static_cast<const uint32_t*>(ctx->d_lut.p);
-    a.lut_bits = dt->bits;
-    a.max_len = dt->maxdepth;
-    a.stab = reinterpret_cast<const uint16_t*>(static_cast<const uint32_t*>(ctx->d_lut.p) + dt->soff);
-    a.stab_bits = dt->sbits;
-    a.wtab = reinterpret_cast<const uint16_t*>(static_cast<const uint32_t*>(ctx->d_lut.p) + dt->woff);
-    if (l2) {  // HUFF_NO_L2=1: the global tables (A/B, tests)
-        a.l2 = static_cast<const uint32_t*>(ctx->d_lut.p) + dt->l2off;
-        a.l2_words = dt->l2words;
-    }
-    // k_split_emit's stage: the block's 256 lanes from its first segment's 16-B
-    // granule, the last lane's overrun past the next block's first theta
-    // (< 300 bits), a code and the window's read-ahead
-    a.stage_bytes = static_cast<uint32_t>((((256 * S) >> lg_r) + 128 + 512 + 128 + 7) / 8 + 15) & ~15u;
-    // its output image: the block's expected letters with a margin (a block
-    // with more writes straight to HBM)
-    const double exp_letters = 256.0 * static_cast<double>(S >> lg_r) / mean;
-    a.img_bytes = static_cast<uint32_t>(std::min(1.15 * exp_letters + 512.0, 64.0 * 1024)) & ~15u;
-    if (dev::split_sync_lds_bytes(a) > 140 * 1024 || dev::split_emit_lds_bytes(a) > 160 * 1024) return Status::ok();
-    IndexlessSync& st = ctx->indexless_ws();
-    const uint64_t nl = nseg << lg_r;
-    const uint64_t nblk = dev::split_blocks(nseg, lg_r);
-    HUFF_TRY(st.rec.ensure(nl * 4));
-    HUFF_TRY(st.xd.ensure(nseg + 16));
-    HUFF_TRY(st.btot.ensure(nblk * 8));
-    HUFF_TRY(st.boff.ensure((nblk + 1) * 8));
-    HUFF_TRY(st.fixlist.ensure(nseg * 4 + 4));
-    HUFF_TRY(st.flag.ensure((dev::kFixRounds + 1) * 4));
-    HUFF_TRY(st.tsum.ensure((nblk / 1024 + 2) * 8));
-    a.rec = static_cast<uint32_t*>(st.rec.p);
-    a.xd = static_cast<uint8_t*>(st.xd.p);
-    a.btot = static_cast<unsigned long long*>(st.btot.p);
-    a.boff = static_cast<const unsigned long long*>(st.boff.p);
-    a.fixlist = static_cast<uint32_t*>(st.fixlist.p);
-    a.flags = static_cast<unsigned int*>(st.flag.p);
-    hipStream_t strm = ctx->stream;
-    HIP_TRY(hipMemsetAsync(st.flag.p, 0, (dev::kFixRounds + 1) * 4, strm));
-    HUFF_TRY(ctx->timed("split_sync", [&] { return dev::launch_split_sync(a, strm); }));
-    HUFF_TRY(ctx->timed("split_fix", [&] { return dev::launch_split_fix(a, strm); }));
-    HIP_TRY(dev::launch_scan(static_cast<const uint64_t*>(st.btot.p), static_cast<uint32_t>(nblk), 0,
-                             static_cast<uint64_t*>(st.boff.p), static_cast<uint64_t*>(st.tsum.p), strm));
-    uint64_t total = 0;
-    HIP_TRY(hipMemcpyAsync(&total, static_cast<uint64_t*>(st.boff.p) + nblk, 8, hipMemcpyDeviceToHost, strm));
-    HUFF_TRY(ctx->sync());
-    *nsym = total;
-    *done = true;
-    if (total == 0) {
-        if (d_end) HIP_TRY(hipMemsetAsync(d_end, 0, 8, strm));
-        return Status::ok();
-    }
-    uint8_t* dst;
-    if (d_user) {
-        if (total > user_cap) return Status::err(HUFF_E_BUFFER_TOO_SMALL, "output buffer too small");
-        dst = d_user;
-    } else {
-        HUFF_TRY(out.ensure(total + 16));
-        dst = static_cast<uint8_t*>(out.p);
-    }
-    // the kernel stores 16-B pieces: a misaligned output is decoded into an
-    // aligned buffer, then copied
-    const bool bounce = reinterpret_cast<uintptr_t>(dst) & 15;
-    if (bounce) HUFF_TRY(ctx->d_align.ensure(total + 64));
-    a.out = bounce ? static_cast<uint8_t*>(ctx->d_align.p) : dst;
-    a.end_bit = d_end;
-    HUFF_TRY(ctx->timed("split_emit", [&] { return dev::launch_split_emit(a, strm); }));
-    HIP_TRY(hipEventRecord(ctx->lut_free, strm));
-    if (bounce) HIP_TRY(hipMemcpyAsync(dst, ctx->d_align.p, total, hipMemcpyDeviceToDevice, strm));
-    return Status::ok();
-}
-
 Status decode_indexless_dev(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_bytes, uint64_t valid_bits,
                             const huff_tree* t, DevBuf& out, uint64_t* nsym, uint8_t* d_user, size_t user_cap,
                             unsigned long long* d_end) {
@@ -1340,11 +1199,6 @@ Status decode_indexless_dev(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_
         }
         HIP_TRY(hipEventRecord(ctx->lut_free, ctx->stream));
         return Status::ok();
-    }
-    if (!decode_check_mode() && split_enabled()) {
-        bool done = false;
-        HUFF_TRY(decode_split(ctx, d_comp, comp_bytes, valid_bits, t, dt, out, nsym, d_user, user_cap, d_end, &done));
-        if (done) return Status::ok();
     }
     IndexlessSync& st = ctx->indexless_ws();
     st.dt = dt;

@@ -67,8 +67,6 @@ void build_multi_table(const HuffTree& t, uint32_t mbits, DecTables& out);
 
 // HUFF_DISABLE_FIXED8=1 forces the general kernels even for all-8-bit codes
 bool fixed8_disabled();
-// HUFF_SPLIT=1: index-free byte decode through the split decoder (isplit.hip)
-bool split_enabled();
 // HUFF_DEC_VARIANT=11 -> k_decode_fixed's self-checking build (mode 1; else 0)
 uint32_t decode_check_mode();
 
@@ -249,7 +247,6 @@ Status decode_indexless_dev(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_
 struct IndexlessSync {
     const DecTables* dt = nullptr;  // tables of the tree, uploaded to ctx->d_lut
     DevBuf s, x0, c, off, flag, tsum, samp, tm, dl, fixlist;
-    DevBuf rec, xd, btot, boff;  // the split decoder's lane records, exits, block letters and offsets
     dev::IndexlessArgs a{};
     uint64_t total = 0;
 };

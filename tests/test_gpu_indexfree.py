@@ -1,27 +1,23 @@
-"""The split index-free decoder (isplit.hip) against the oracle.
+"""The index-free decoder (indexless.hip + the fixed-count decoder's skip
+build) against the oracle.
 
 Streams are written by the CPU restatement (oracle/, comp.rs:419-451) with no
 restart index, as the reference writes every CompressData and .hff payload,
-and decoded on the device through huff_dev_decompress (comp.rs:487-519) with
-HUFF_SPLIT=1, the opt-in path for codes <= 32 bits (k_split_sync -> k_fix_rec ->
-scan -> k_split_emit; measured slower than the default sample + mark path, DESIGN
-§11).
-The cases cover its paths: lanes merging with their speculative walk, codes
-longer than the 12-bit table, 1-8 lanes per segment, lanes past 64 letters,
-blocks past the LDS image, slowly resynchronising codes (the fix-up rounds),
-tiny and ragged streams, misaligned outputs, the count-only query, garbage
-payloads, and equality with the default sample + mark path (HUFF_SPLIT=0).
+and decoded on the device through huff_dev_decompress (comp.rs:487-519): the
+speculative pass, the fix-up, the scan, the marks and the decoder.
+The cases cover lanes merging with their speculative walk, codes longer than
+the 12-bit table (level-2 table in LDS and the global one), heavily skewed
+bytes (~1 bit per letter: many codes to skip per mark), slowly
+resynchronising codes (the fix-up rounds), tiny and ragged streams,
+misaligned outputs, the count-only query, garbage payloads, equality with
+the self-checking build (HUFF_DEC_VARIANT=11: exact walked marks), and the
+BASELINE-size streams. (Until round 4 these cases drove the opt-in split
+decoder, isplit.hip, measured slower and removed in round 5; git history.)
 """
 import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu
-
-
-@pytest.fixture(autouse=True)
-def split_on(monkeypatch):
-    """the split decoder is opt-in (HUFF_SPLIT=1)"""
-    monkeypatch.setenv("HUFF_SPLIT", "1")
 
 
 def roundtrip(H, O, ctx, data, misalign=0):
@@ -64,9 +60,9 @@ def index_free_cases(O, rng):
     x[rng.integers(0, x.size, 3000)] = rng.integers(0, 256, 3000, dtype=np.uint8)  # codes > 12 bits
     yield "long-codes", x.tobytes()
     skew = np.where(rng.random(2_000_000) < 0.95, 0, rng.integers(1, 200, 2_000_000)).astype(np.uint8)
-    yield "skewed-95", skew.tobytes()  # lanes past 64 letters, blocks past the image
+    yield "skewed-95", skew.tobytes()  # ~1.3 bits per letter: long skips between samples
     skew = np.where(rng.random(1_500_000) < 0.995, 7, rng.integers(0, 3, 1_500_000)).astype(np.uint8)
-    yield "skewed-99.5", skew.tobytes()  # ~1 bit per letter: ~120 letters per lane at R = 8
+    yield "skewed-99.5", skew.tobytes()  # ~1 bit per letter
     runs = np.repeat(rng.integers(0, 6, 40_000, dtype=np.uint8), rng.integers(1, 300, 40_000))
     yield "runs", runs.tobytes()
     for n in (1, 2, 3, 63, 64, 65, 255, 256, 1000, 4095, 65537):
@@ -92,14 +88,14 @@ def cases(O):
     return list(index_free_cases(O, np.random.default_rng(2024)))
 
 
-def test_split_matches_oracle(H, O, ctx, cases):
+def test_indexfree_matches_oracle(H, O, ctx, cases):
     for name, data in cases:
         roundtrip(H, O, ctx, data)
 
 
 @pytest.mark.parametrize("l2", [True, False], ids=["l2-lds", "l2-global"])
-def test_split_codes_past_table(H, O, ctx, l2, monkeypatch):
-    """codes of 13-23 bits: the sync pass's level-2 length table in LDS, and
+def test_indexfree_codes_past_table(H, O, ctx, l2, monkeypatch):
+    """codes of 13-23 bits: the walks' level-2 length table in LDS, and
     with HUFF_NO_L2=1 the global multi-level table"""
     if not l2:
         monkeypatch.setenv("HUFF_NO_L2", "1")
@@ -108,13 +104,14 @@ def test_split_codes_past_table(H, O, ctx, l2, monkeypatch):
         roundtrip(H, O, ctx, np.minimum(rng.geometric(p, n), 255).astype(np.uint8).tobytes())
 
 
-def test_split_misaligned_output(H, O, ctx, cases):
+def test_indexfree_misaligned_output(H, O, ctx, cases):
     for name, data in cases[:4]:
         roundtrip(H, O, ctx, data[:1_000_003], misalign=3)
 
 
-def test_split_equals_older_path(H, O, ctx, monkeypatch):
-    """the same stream through the split path and the default one"""
+def test_indexfree_equals_check_build(H, O, ctx, monkeypatch):
+    """the same stream through the default path (marks + skip codes) and the
+    self-checking build (HUFF_DEC_VARIANT=11: walked marks, end-bit checks)"""
     import torch
     from huff_coding import device as D
 
@@ -122,8 +119,8 @@ def test_split_equals_older_path(H, O, ctx, monkeypatch):
     comp, pad, tree = roundtrip(H, O, ctx, data)
     dc = torch.from_numpy(np.concatenate([comp, np.zeros(64, np.uint8)])).cuda()
     outs = []
-    for flag in ("1", "0"):
-        monkeypatch.setenv("HUFF_SPLIT", flag)
+    for flag in ("11", "0"):
+        monkeypatch.setenv("HUFF_DEC_VARIANT", flag)
         out = torch.empty(len(data) + 64, dtype=torch.uint8, device="cuda")
         assert D.decompress_dev(ctx, tree, dc.data_ptr(), comp.size, pad, out.data_ptr(), len(data) + 64) == len(data)
         outs.append(out[: len(data)].clone())
@@ -131,7 +128,7 @@ def test_split_equals_older_path(H, O, ctx, monkeypatch):
     assert torch.equal(outs[0], outs[1])
 
 
-def test_split_garbage_payloads(H, O, ctx):
+def test_indexfree_garbage_payloads(H, O, ctx):
     """random payloads under fixed trees: whatever the bits, the letters and
     the dropped final code match the reference walk"""
     import torch
@@ -154,12 +151,11 @@ def test_split_garbage_payloads(H, O, ctx):
 
 
 @pytest.mark.parametrize("kind", ["zipf", "text"])
-def test_split_full_size_foreign_stream(H, O, ctx, kind, monkeypatch):
+def test_indexfree_full_size_foreign_stream(H, O, ctx, kind, monkeypatch):
     """BASELINE size: the 1 GiB Zipf (configs[2]) and text streams written on
     the CPU by the oracle's table-driven encoder (no restart index, as the
     reference writes every stream: comp.rs:128-184, 487-519), decoded through
-    huff_dev_decompress by both index-free paths and compared with the input
-    on the device"""
+    huff_dev_decompress and compared with the input on the device"""
     import os
 
     import torch
@@ -178,11 +174,9 @@ def test_split_full_size_foreign_stream(H, O, ctx, kind, monkeypatch):
     dc[: comp.size] = torch.from_numpy(comp).cuda()
     del comp
     out = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
-    for flag in ("1", "0"):  # the split decoder and the default sample + mark path
-        monkeypatch.setenv("HUFF_SPLIT", flag)
-        out.fill_(0)
-        torch.cuda.synchronize()
-        got = D.decompress_dev(ctx, tree, dc.data_ptr(), dc.numel() - 64, pad, out.data_ptr(), n + 64)
-        torch.cuda.synchronize()
-        assert got == n
-        assert torch.equal(out[:n], x), flag
+    out.fill_(0)
+    torch.cuda.synchronize()
+    got = D.decompress_dev(ctx, tree, dc.data_ptr(), dc.numel() - 64, pad, out.data_ptr(), n + 64)
+    torch.cuda.synchronize()
+    assert got == n
+    assert torch.equal(out[:n], x)

@@ -465,6 +465,11 @@ def test_device_job_full_size_zipf(H, O, ctx):
     x = _device_gen(H, ctx, "zipf", 0x5EED0002, n)
     job = H.EncodeJob(ctx, x.data_ptr(), n)
     w = job.hist()
+    host = x[:n].cpu().numpy()
+    # pass 1 on skewed bytes against an independent host count (the oracle
+    # tree below is built from these weights, so a miscount would otherwise
+    # be self-consistent)
+    assert (w == O.fast_hist(host, 16)).all()
     tree = H.HuffTree.from_weights(H.ByteWeights.from_array(w))
     bits = job.bits(tree)
     assert 5.2 < bits / n < 5.4
@@ -474,7 +479,6 @@ def test_device_job_full_size_zipf(H, O, ctx):
     job.decode(tree, out.data_ptr(), dec.data_ptr())
     torch.cuda.synchronize()
     assert torch.equal(dec[:n], x[:n])
-    host = x[:n].cpu().numpy()
     ot = O.Tree.from_weights(O.weights_from_array(w))
     code, ln = ot.code_table()
     want, wb = O.fast_encode(host, code, ln, threads=16)
