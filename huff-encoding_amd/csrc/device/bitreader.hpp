@@ -78,6 +78,36 @@ __device__ __forceinline__ void st_nt(uint4* p, uint4 v) {
     __builtin_nontemporal_store(w, reinterpret_cast<u32x4_t*>(p));
 }
 
+// Phase stamps of a timing build (-DHUFF_STAMPS, tools/build_variant.sh; never
+// in the product library): a wave keeps s_memtime at up to 8 phase
+// boundaries in SGPRs and writes them, with its hardware id, to a buffer of
+// its own (DecodeArgs/IndexlessArgs::stamps) by ONE vector store (lanes
+// 0..9 each write one word at a lane-indexed address). Slot layout per
+// wave: [0, 8) stamps, [8] HW_ID (CU / SIMD / wave slot), [9] XCC id.
+#ifdef HUFF_STAMPS
+struct WaveStamps {
+    uint64_t t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    __device__ __forceinline__ void mark(int k) { t[k] = __builtin_amdgcn_s_memtime(); }
+    __device__ __forceinline__ void flush(uint64_t* buf, uint64_t wave_slot) const {
+        if (!buf) return;
+        const uint32_t lane = threadIdx.x & 63;
+        uint64_t v = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v = lane == static_cast<uint32_t>(k) ? t[k] : v;
+        if (lane == 8) v = static_cast<uint64_t>(__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11)));  // HW_ID
+        if (lane == 9) v = static_cast<uint64_t>(__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11)));  // XCC_ID
+        if (lane < 10) buf[wave_slot * 10 + lane] = v;
+    }
+};
+#define HUFF_STAMP(ws, k) (ws).mark(k)
+#else
+struct WaveStamps {
+    __device__ __forceinline__ void mark(int) {}
+    __device__ __forceinline__ void flush(uint64_t*, uint64_t) const {}
+};
+#define HUFF_STAMP(ws, k) ((void)0)
+#endif
+
 struct BitSrc {
     const uint32_t* w;
     const uint8_t* b;

@@ -181,7 +181,7 @@ template <bool SLOW, bool SKIP, class Words>
 __device__ __forceinline__ void decode_fixed64(const Words& src, uint32_t rel, uint32_t (&o)[16],
                                                const uint16_t* __restrict__ stab, uint32_t K,
                                                const uint32_t* __restrict__ glut, uint32_t Ks, uint32_t* end_rel,
-                                               uint32_t skip) {
+                                               uint32_t skip, WaveStamps* ws) {
     uint32_t rp = rel >> 5;
     const uint32_t sh = rel & 31;
     uint64_t buf = static_cast<uint64_t>(src(rp) << sh) << 32;
@@ -259,6 +259,7 @@ __device__ __forceinline__ void decode_fixed64(const Words& src, uint32_t rel, u
             FX_STEP();
         }
     }
+    if (ws) HUFF_STAMP(*ws, 3);
 #pragma unroll
     for (int i = 0; i < 64; i += 2) {
         FX_REFILL();
@@ -275,11 +276,12 @@ template <bool SLOW, bool PAD, bool SKIP = false>
 __device__ __forceinline__ void decode_fixed64_stage(const uint32_t* stage, uint32_t rel, uint32_t (&o)[16],
                                                      const uint16_t* __restrict__ stab, uint32_t K,
                                                      const uint32_t* __restrict__ glut, uint32_t Ks,
-                                                     uint32_t* end_rel, uint32_t skip = 0) {
+                                                     uint32_t* end_rel, uint32_t skip = 0,
+                                                     WaveStamps* ws = nullptr) {
     if constexpr (PAD)
-        decode_fixed64<SLOW, SKIP>(PaddedLdsWords{stage}, rel, o, stab, K, glut, Ks, end_rel, skip);
+        decode_fixed64<SLOW, SKIP>(PaddedLdsWords{stage}, rel, o, stab, K, glut, Ks, end_rel, skip, ws);
     else
-        decode_fixed64<SLOW, SKIP>(LdsWords{stage}, rel, o, stab, K, glut, Ks, end_rel, skip);
+        decode_fixed64<SLOW, SKIP>(LdsWords{stage}, rel, o, stab, K, glut, Ks, end_rel, skip, ws);
 }
 
 // fallback for a task whose compressed range exceeds the stage: a compact
@@ -371,6 +373,10 @@ __device__ __forceinline__ void decode_fixed_body(const DecodeArgs& a) {
     uint64_t task = static_cast<uint64_t>(blockIdx.x) * kWaves + wave;
     Task cur{};
     uint4 pre[kLoadRounds];
+    // timing builds: 0 entry, 1 table staged, 2 input staged, 3 skips done,
+    // 4 letters done, 5 transposed, 6 stores issued (one-shot grid: a task per wave)
+    WaveStamps ws;
+    HUFF_STAMP(ws, 0);
     if constexpr (kEarlyLoads) {
         // the first task's index and input loads go out before the table is
         // staged (they hide the table copy of the one-shot grid), joined by a
@@ -390,6 +396,7 @@ __device__ __forceinline__ void decode_fixed_body(const DecodeArgs& a) {
             if (t + kThreads * i < tab_pieces) st_stage16(lds + 4 * (t + kThreads * i), tp[i]);
         __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): table stores done; the input loads stay in flight
         __builtin_amdgcn_s_barrier();
+        HUFF_STAMP(ws, 1);
         if (!have) return;
     } else {
         for (uint32_t i = t; i < tab_words; i += kThreads) lds[i] = reinterpret_cast<const uint32_t*>(a.stab)[i];
@@ -420,6 +427,7 @@ __device__ __forceinline__ void decode_fixed_body(const DecodeArgs& a) {
         const uint64_t nxt_task = task + step;
         const bool more = nxt_task < ntasks;
         wave_sync();
+        HUFF_STAMP(ws, 2);
 
         const uint32_t rel = static_cast<uint32_t>(cur.lane_bit - cur.b0 * 8);
         uint8_t* dst = a.out + cur.sym0 + lane * kLaneSym;
@@ -431,8 +439,9 @@ __device__ __forceinline__ void decode_fixed_body(const DecodeArgs& a) {
         } else if (cur.nsym == kTaskSym) {  // wave-uniform: every lane has 64 letters
             uint32_t o[16];
             uint32_t e = 0;
-            decode_fixed64_stage<SLOW, PAD, SKIP>(stage, rel, o, stab, K, a.lut, a.lut_bits, &e, cur.skip);
+            decode_fixed64_stage<SLOW, PAD, SKIP>(stage, rel, o, stab, K, a.lut, a.lut_bits, &e, cur.skip, &ws);
             fx_check<CHECK>(a, cur, task, lane, cur.b0 * 8 + e, true);
+            HUFF_STAMP(ws, 4);
             // transpose through the stage so every store instruction writes
             // 1 KiB contiguous (16 B per lane): lane-strided 16-B pieces cost
             // 4x the L2 write requests and stalled the TA (PMC)
@@ -441,11 +450,13 @@ __device__ __forceinline__ void decode_fixed_body(const DecodeArgs& a) {
             for (int q = 0; q < 4; ++q)
                 st_stage16(sb + row_piece(lane, q), make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]));
             wave_sync();
+            HUFF_STAMP(ws, 5);
             // nontemporal: the letters are written once and not read back here
             // (-2 % decode time against default-policy stores, same box)
             uint4* d4 = reinterpret_cast<uint4*>(a.out + cur.sym0) + lane;
 #pragma unroll
             for (int q = 0; q < 4; ++q) st_nt(d4 + 64 * q, ld_stage16(sb + row_piece(16 * q + (lane >> 2), lane & 3)));
+            HUFF_STAMP(ws, 6);
         } else if (cur.cnt) {
             uint32_t o[16];
             uint32_t e = 0;
@@ -464,6 +475,7 @@ __device__ __forceinline__ void decode_fixed_body(const DecodeArgs& a) {
         } else {
             fx_check<CHECK>(a, cur, task, lane, 0, false);  // keeps the shuffles wave-uniform
         }
+        ws.flush(a.stamps, task);
         if (!more) break;
         wave_sync();  // the input stage is reused by the next task
         task = nxt_task;

@@ -261,12 +261,15 @@ __device__ __forceinline__ void samp_pick(const uint32_t (&sv)[kSampMax], uint32
 template <bool SLOW>
 __global__ __launch_bounds__(kThreads) void k_spec_lds(IndexlessArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    WaveStamps ws;  // timing builds: 0 entry, 1 staged, 2 multi-code walk, 3 exit walk, 4 fix-up start, 5 fix-up end
+    HUFF_STAMP(ws, 0);
     TabLoad tl;
     issue_tables(a, tl);
     const Staged st = with_l2(stage_block(a, lds + tables_words(a)), a, lds);
     const uint16_t* stab = store_tables(a, tl, lds);
     const uint16_t* wtab = a.wtab ? stab : nullptr;  // one table serves single and multi-code steps
     __syncthreads();
+    HUFF_STAMP(ws, 1);
     const uint64_t i0 = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
     const bool live = i0 < a.nseg;  // no early return: the fix-up below has a barrier
     const uint64_t i = live ? i0 : a.nseg - 1;
@@ -313,6 +316,7 @@ __global__ __launch_bounds__(kThreads) void k_spec_lds(IndexlessArgs a) {
             note_sample();
         }
     }
+    HUFF_STAMP(ws, 2);
     for (;;) {
         uint32_t L[kChunkSteps];
         c.chunk<SLOW>(L, stab, K, a.lut, Kg);
@@ -339,6 +343,7 @@ __global__ __launch_bounds__(kThreads) void k_spec_lds(IndexlessArgs a) {
         cnt += kChunkSteps;
         note_sample();
     }
+    HUFF_STAMP(ws, 3);
     if (live)
         for (; next_k <= a.nsamp; ++next_k) smp[next_k - 1] = ~0u;
 
@@ -356,6 +361,7 @@ __global__ __launch_bounds__(kThreads) void k_spec_lds(IndexlessArgs a) {
     uint64_t s_out = start;
     uint32_t tm_out = 0;
     int32_t dl_out = 0;
+    HUFF_STAMP(ws, 4);
     const uint64_t ns = threadIdx.x ? ex_l[threadIdx.x - 1] : start;
     if (ns != start) {
         Cursor ca_;
@@ -410,6 +416,8 @@ __global__ __launch_bounds__(kThreads) void k_spec_lds(IndexlessArgs a) {
             ((i + 1) % kThreads) != 0 && a.fixlist)
             a.fixlist[atomicAdd(a.flags + kFixRounds, 1u)] = static_cast<uint32_t>(i + 1);
     }
+    HUFF_STAMP(ws, 5);
+    ws.flush(a.stamps, static_cast<uint64_t>(blockIdx.x) * (kThreads / 64) + (threadIdx.x >> 6));
     if (!live) return;
     a.s[i] = s_out;
     a.x[i] = cur;

@@ -107,6 +107,7 @@ struct DecodeArgs {
     // err: u32[8] mismatch count + first (task, lane, want, got)
     uint32_t check_mode;
     uint32_t* err;
+    uint64_t* stamps;             // timing builds (-DHUFF_STAMPS) only: per-wave phase stamps
 };
 // whether k_decode_fixed should swizzle its stage for this mean code
 // length: the stride bands where a bank model of the 32-lane refill reads
@@ -163,6 +164,7 @@ struct IndexlessArgs {
     // the global multi-level table `lut`
     const uint32_t* l2;
     uint32_t l2_words;
+    uint64_t* stamps;             // timing builds (-DHUFF_STAMPS) only: per-wave phase stamps
 };
 constexpr uint32_t kSampBits = 128;
 constexpr uint32_t kSampMax = 8;  // samples kept per segment (nsamp <= kSampMax)

@@ -69,9 +69,26 @@ uint32_t decode_check_mode() {
     return std::atoi(e) == static_cast<int>(dev::kDecodeFixedCheck) ? 1u : 0u;
 }
 
+#ifdef HUFF_STAMPS
+// Timing builds only (tools/build_variant.sh -DHUFF_STAMPS): per-wave phase
+// stamps of the index-free speculative pass (region 0), the skip decoder
+// (region 1) and the indexed decoder (region 2), 10 words per wave
+// (bitreader.hpp WaveStamps); huff_diag_stamps copies a region out.
+constexpr size_t kStampRegionWords = 8u << 20;  // 64 MiB per region: >= 800 K waves
+static uint64_t* g_stamps = nullptr;
+uint64_t* stamp_region(int r) {
+    if (!g_stamps && hipMalloc(&g_stamps, 3 * kStampRegionWords * 8) != hipSuccess) g_stamps = nullptr;
+    if (!g_stamps) return nullptr;
+    return g_stamps + r * kStampRegionWords;
+}
+#endif
+
 // a checked k_decode_fixed launch: zero the mismatch record before, read it
 // after (a host wait: test builds only)
 Status run_checked_decode(huff_ctx* ctx, dev::DecodeArgs& a, const std::function<hipError_t()>& launch) {
+#ifdef HUFF_STAMPS
+    a.stamps = stamp_region(a.skip_packed ? 1 : 2);
+#endif
     if (!a.check_mode) return hip_status(launch(), "decode");
     HUFF_TRY(ctx->d_err.ensure(32));
     a.err = static_cast<uint32_t*>(ctx->d_err.p);
@@ -1086,6 +1103,9 @@ Status indexless_sync(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_bytes,
     a.tm = static_cast<uint32_t*>(st.tm.p);
     a.dl = static_cast<int32_t*>(st.dl.p);
     a.flags = static_cast<unsigned int*>(st.flag.p);
+#ifdef HUFF_STAMPS
+    a.stamps = stamp_region(0);
+#endif
     hipStream_t strm = ctx->stream;
     if (dev::indexless_staged(a)) {  // speculative samples for the marking pass
         a.nsamp = std::min<uint32_t>(dev::kSampMax, static_cast<uint32_t>((S - 1) / dev::kSampBits));
@@ -1272,3 +1292,12 @@ Status decode_indexless_host(huff_ctx* ctx, const uint8_t* comp, size_t len, uin
 }
 
 }  // namespace huff
+
+#ifdef HUFF_STAMPS
+// timing builds only: region r's first `words` stamp words into host memory
+extern "C" int huff_diag_stamps(int r, uint64_t* host, size_t words) {
+    uint64_t* p = huff::stamp_region(r);
+    if (!p || words > huff::kStampRegionWords) return -1;
+    return hipMemcpy(host, p, words * 8, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif
