@@ -11,7 +11,7 @@ cd $root
 for rep in $(seq 1 ${REPS:-3}); do
   for l in new ${LIBS:-}; do
     if [ $l = new ]; then unset HUFF_LIB_AB; else export HUFF_LIB_AB=$l; fi
-    timeout -k 10 200 python -u bench.py --no-cpu-baseline --file-path none --side none --steps 40 ${BENCH_ARGS:-} > $out/bench_${l}_$rep.json 2> $out/bench_${l}_$rep.err || { echo "bench $l failed"; tail -5 $out/bench_${l}_$rep.err; exit 1; }
+    timeout -k 10 200 python -u bench.py --no-cpu-baseline --file-path none --side none --no-general --no-other-scaling --steps 40 ${BENCH_ARGS:-} > $out/bench_${l}_$rep.json 2> $out/bench_${l}_$rep.err || { echo "bench $l failed"; tail -5 $out/bench_${l}_$rep.err; exit 1; }
     python3 -c "import json; d=json.loads(open('$out/bench_${l}_$rep.json').read().strip().splitlines()[-1]); print('$l $rep', d['value'], {k: v['avg_ms'] for k, v in d['kernels'].items()})"
   done
 done
