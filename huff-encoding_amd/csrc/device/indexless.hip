@@ -304,16 +304,43 @@ __global__ __launch_bounds__(kThreads) void k_spec_lds(IndexlessArgs a) {
         pc = cur;
         pcn = cnt;
     };
+    // the first multi-code chunk's window ends (bits | codes << 16 from
+    // start; ~0u: none), boundaries of this path that the fix-up below can
+    // merge on long before the first sample
+    uint32_t cq[kChunkSteps];
+#pragma unroll
+    for (int k = 0; k < kChunkSteps; ++k) cq[k] = ~0u;
     if (wtab) {
-        // multi-code chunks while the chunk's last boundary stays below `end`
-        // (so no boundary inside it can be the exit); single codes after
-        const uint64_t span = static_cast<uint64_t>(kChunkSteps) * (a.max_len > K ? a.max_len : K);
-        while (cur + span < end) {
-            uint32_t U, N;
-            c.multi_chunk<SLOW>(U, N, wtab, stab, K, a.lut, Kg);
-            cur += U;
-            cnt += N;
+        // multi-code chunks (window ends: boundaries of this path) while every
+        // window ends below `end`; the chunk whose windows reach `end` is cut
+        // back to the start of its first such window (the exit lies in it or
+        // at its end) and the cursor re-seated there for the single steps
+        // below (walking the last ~8 K bits in single steps cost a tenth of
+        // the pass: phase stamps)
+        bool first = true;
+        for (;;) {
+            uint32_t U, N, q[kChunkSteps];
+            c.multi_chunk<SLOW>(U, N, q, wtab, stab, K, a.lut, Kg);
+            const bool below = cur + U < end;
+            uint32_t base = 0;
+#pragma unroll
+            for (int k = 0; k < kChunkSteps; ++k) {
+                const bool in = cur + (q[k] & 0xFFFFu) < end;
+                base = in ? q[k] : base;
+                if (first) cq[k] = in ? q[k] : ~0u;
+            }
+            first = false;
+            if (below) {
+                cur += U;
+                cnt += N;
+                note_sample();
+                continue;
+            }
+            cur += base & 0xFFFFu;
+            cnt += base >> 16;
+            c.init(st, cur);
             note_sample();
+            break;
         }
     }
     HUFF_STAMP(ws, 2);
@@ -367,9 +394,50 @@ __global__ __launch_bounds__(kThreads) void k_spec_lds(IndexlessArgs a) {
         Cursor ca_;
         ca_.init(st, ns);
         uint64_t pa = ns, na = 0;
-        uint64_t pk = sp1;        // current sample: position, spec-local index
-        uint32_t ik = si1, k = 1;
-        for (;;) {
+        // merge candidates in ascending order: the first chunk's window ends
+        // (cq), then the samples; pk / ik = the current one (position,
+        // spec-local index), the first at or after the walk's position
+        uint64_t pk = ~0ull;
+        uint32_t ik = 0, k = 0;
+        auto next_candidate = [&](uint64_t at) {
+            uint64_t best = ~0ull;
+            uint32_t bi = 0;
+#pragma unroll
+            for (int j = kChunkSteps - 1; j >= 0; --j) {  // the first window end >= at
+                const uint64_t pj = cq[j] == ~0u ? ~0ull : start + (cq[j] & 0xFFFFu);
+                const bool ok = pj >= at;
+                best = ok ? pj : best;
+                bi = ok ? (cq[j] >> 16) : bi;
+            }
+            if (best == ~0ull) {  // past the window ends: the samples
+                while (true) {
+                    uint32_t sv;
+                    uint64_t ps;
+                    if (k == 0) {
+                        ps = sp1;
+                        sv = 0;
+                        bi = si1;
+                    } else {
+                        sv = k < a.nsamp ? smp[k] : ~0u;
+                        ps = sv == ~0u ? ~0ull : start + samp_off(sv);
+                        bi = samp_idx(sv);
+                    }
+                    if (ps >= at || ps == ~0ull) {
+                        best = ps;
+                        break;
+                    }
+                    ++k;
+                }
+            }
+            pk = best;
+            ik = bi;
+        };
+        next_candidate(ns);
+        if (pk == ns) {  // the predecessor's exit is a boundary of this path: merged at once
+            tm_out = 0;
+            dl_out = -static_cast<int32_t>(ik);
+            cnt = static_cast<uint64_t>(static_cast<int64_t>(cnt) + dl_out);
+        } else for (;;) {
             uint32_t L[kChunkSteps];
             ca_.chunk<SLOW>(L, stab, K, a.lut, Kg);
             uint64_t p = pa;
@@ -402,11 +470,14 @@ __global__ __launch_bounds__(kThreads) void k_spec_lds(IndexlessArgs a) {
             }
             pa = p;
             na += kChunkSteps;
-            while (pa > pk) {  // passed the sample without landing on it: the next one
-                const uint32_t sv = k < a.nsamp ? smp[k] : ~0u;
-                ++k;
-                pk = sv == ~0u ? ~0ull : start + samp_off(sv);
-                ik = samp_idx(sv);
+            if (pa > pk) {  // passed it without landing on it: the next one
+                next_candidate(pa);
+                if (pk == pa) {  // the chunk's last boundary is that one: merged there
+                    tm_out = static_cast<uint32_t>(na);
+                    dl_out = static_cast<int32_t>(static_cast<int64_t>(na) - static_cast<int64_t>(ik));
+                    cnt = static_cast<uint64_t>(static_cast<int64_t>(cnt) + dl_out);
+                    break;
+                }
             }
         }
         s_out = ns;

@@ -107,6 +107,9 @@ struct DecodeArgs {
     // err: u32[8] mismatch count + first (task, lane, want, got)
     uint32_t check_mode;
     uint32_t* err;
+    // skip build (skip_packed): the walk table over the same stab_bits-bit
+    // windows (IndexlessArgs::wtab), so the skip codes go ~2 per lookup
+    const uint16_t* wtab;
     uint64_t* stamps;             // timing builds (-DHUFF_STAMPS) only: per-wave phase stamps
 };
 // whether k_decode_fixed should swizzle its stage for this mean code

@@ -820,6 +820,9 @@ huff::Status huff_enc::decode(const huff_tree* t, const uint8_t* d_comp, uint64_
     a.stab_bits = dt->sbits;
     a.n = n;
     a.out = dst;
+#ifdef HUFF_STAMPS
+    a.stamps = huff::stamp_region(2);
+#endif
     if (a.check_mode) {
         HUFF_TRY(huff::run_checked_decode(ctx, a, [&] { return huff::dev::launch_decode(a, ctx->stream); }));
         HUFF_TRY(check_sums(dst));
@@ -1057,7 +1060,10 @@ Status indexless_sync(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_bytes,
     // codes <= 32 bits take the LDS-staged kernels, longer codes 2048-bit segments
     // (~992 bits: with the one 8 KiB walk table a workgroup's LDS stays under
     // 40 KiB, 4 workgroups per CU; 1024-bit segments measured ~1.5 % slower)
-    const uint64_t seg_target = dt->maxdepth <= 32 ? 992 : 2048;
+#ifndef HUFF_SEG_TARGET
+#define HUFF_SEG_TARGET 992
+#endif
+    const uint64_t seg_target = dt->maxdepth <= 32 ? HUFF_SEG_TARGET : 2048;
     uint64_t S = static_cast<uint64_t>(g) * ((seg_target + g - 1) / g);
     // the LDS-staged kernels read lane i's bits from dword ~S/32 * i: with an
     // even dword stride every lane starts on the same few banks (1024 bits: all
@@ -1255,6 +1261,10 @@ Status decode_indexless_dev(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_
         d.lut_words = static_cast<uint32_t>(dt->lut.size());
         d.sub_abs64 = static_cast<const uint64_t*>(sub_abs.p);
         d.skip_packed = check ? 0u : 1u;
+        // the skip codes through the walk table (HUFF_SKIP_WALK=0: one code per lookup, A/B)
+        const char* sw = std::getenv("HUFF_SKIP_WALK");
+        if (!check && dt->sbits <= 15 && !(sw && *sw == '0'))
+            d.wtab = reinterpret_cast<const uint16_t*>(static_cast<const uint32_t*>(ctx->d_lut.p) + dt->woff);
         d.end_bit = valid_bits;
         d.nchunks = static_cast<uint32_t>((total + dev::kChunk - 1) / dev::kChunk);
         d.max_len = dt->maxdepth;

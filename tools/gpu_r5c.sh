@@ -1,0 +1,24 @@
+#!/usr/bin/env bash
+# Round 5: GPU suite on the reworked speculative pass and the walk-table skip,
+# their phase stamps, index-free timing (with A/B: HUFF_SKIP_WALK=0, 512-thread
+# skip workgroups), then the byte map's pieces-per-lane A/B in the bench step.
+set -uo pipefail
+root=${GRAFT_REPO_ROOT:-$(pwd)}
+tag=${1:-r5c}
+out=$root/gpurun_out/$tag; mkdir -p $out
+cd $root
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 200 --timeout-method thread > $out/gpu_tests.log 2>&1 || { tail -30 $out/gpu_tests.log; exit 1; }
+tail -1 $out/gpu_tests.log
+for wl in zipf text; do
+  HUFF_LIB_AB=stamps timeout -k 10 200 python -u tools/stamps.py --workload $wl > $out/stamps_$wl.json 2> $out/stamps_$wl.err || { tail -20 $out/stamps_$wl.err; exit 1; }
+  for rep in 1 2; do
+    timeout -k 10 200 python -u tools/kbench.py --phase indexless --workload $wl --iters 20 > $out/idx_${wl}_$rep.json 2> $out/idx_$wl.err || { tail -20 $out/idx_$wl.err; exit 1; }
+    HUFF_SKIP_WALK=0 timeout -k 10 200 python -u tools/kbench.py --phase indexless --workload $wl --iters 20 > $out/idx_${wl}_nowalk_$rep.json 2> $out/idx_$wl.err || { tail -20 $out/idx_$wl.err; exit 1; }
+    for v in st512 seg480 seg736; do HUFF_LIB_AB=$v timeout -k 10 200 python -u tools/kbench.py --phase indexless --workload $wl --iters 20 > $out/idx_${wl}_${v}_$rep.json 2> $out/idx_$wl.err || { tail -20 $out/idx_$wl.err; exit 1; }; done
+  done
+  grep -h -o '"wall_ms_per_iter": [0-9.]*' $out/idx_${wl}_*.json
+done
+LIBS="bm8 bm2" REPS=3 bash tools/gpu_benchab.sh $tag/benchab
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $out/idx_trace -o run --output-format csv -- python3 $root/tools/kbench.py --phase indexless --workload zipf --iters 5 > $out/idx_trace.log 2>&1 || { tail -20 $out/idx_trace.log; exit 1; }
+echo "trace done"

@@ -41,6 +41,8 @@ def summarize(name, arr):
     """arr: (waves, 10) u64; stamps 0..7 (0 = not reached), [8] HW_ID, [9] XCC"""
     t = arr[:, :8].astype(np.int64)
     live = t[:, 0] > 0
+    if not live.any():
+        return {"waves": 0, "nonzero_words": int((arr != 0).sum()), "first_rows": arr[:3].tolist()}
     t = t[live]
     hw, xcc = arr[live, 8], arr[live, 9]
     nph = len(PHASES[name])
@@ -58,13 +60,20 @@ def summarize(name, arr):
                           "p90": float(np.percentile(d[ok], 90)), "waves": int(ok.sum())}
         prev = np.where(ok, t[:, k], prev)
     life = last - t[:, 0]
-    span = int(last.max() - t[:, 0].min())
+    # s_memtime counters are per XCD (not synchronised): spans per XCC
+    spans, resid = [], []
+    for x in np.unique(xcc):
+        m = xcc == x
+        sp = int(last[m].max() - t[m, 0].min())
+        ncu_x = len(np.unique((hw[m].astype(np.int64) >> 8) & 0xFF))
+        spans.append(sp)
+        resid.append(float(life[m].sum()) / max(sp, 1) / max(ncu_x, 1))
     cu = (xcc.astype(np.int64) << 16) | ((hw.astype(np.int64) >> 8) & 0xFF)
     ncu = len(np.unique(cu))
     res.update({"phases": phases, "lifetime": {"mean": round(float(life.mean()), 1),
                                                "median": float(np.median(life))},
-                "span_cycles": span, "cus_seen": ncu,
-                "resident_waves_per_cu": round(float(life.sum()) / span / max(ncu, 1), 2)})
+                "span_cycles_per_xcc": {"mean": round(float(np.mean(spans)), 0), "max": int(max(spans))},
+                "cus_seen": ncu, "resident_waves_per_cu": round(float(np.mean(resid)), 2)})
     return res
 
 
