@@ -181,8 +181,7 @@ template <bool SLOW, bool SKIP, class Words>
 __device__ __forceinline__ void decode_fixed64(const Words& src, uint32_t rel, uint32_t (&o)[16],
                                                const uint16_t* __restrict__ stab, uint32_t K,
                                                const uint32_t* __restrict__ glut, uint32_t Ks, uint32_t* end_rel,
-                                               uint32_t skip, WaveStamps* ws,
-                                               const uint16_t* __restrict__ wtab = nullptr) {
+                                               uint32_t skip, WaveStamps* ws) {
     uint32_t rp = rel >> 5;
     const uint32_t sh = rel & 31;
     uint64_t buf = static_cast<uint64_t>(src(rp) << sh) << 32;
@@ -246,48 +245,18 @@ __device__ __forceinline__ void decode_fixed64(const Words& src, uint32_t rel, u
         X -= e;                                                                               \
     } while (0)
 
-// one walk-table step of the skip: all the window's complete codes when they
-// are no more than the codes left to skip, else its first code (the entry's
-// low bits are stab's length and kSsSlow); nothing once none are left
-#define FX_WSTEP()                                                                            \
-    do {                                                                                      \
-        const uint32_t e = wtab[static_cast<uint32_t>(buf >> 32) >> (32 - K)];                \
-        if (SLOW && (e & kSsSlow)) {                                                          \
-            if (rem) {                                                                        \
-                FX_STEP();                                                                    \
-                rem -= 1;                                                                     \
-            }                                                                                 \
-        } else {                                                                              \
-            const uint32_t n = e >> 12;                                                       \
-            const bool mult = n <= rem;                                                       \
-            const uint32_t tu = mult ? ((e >> 8) & 15u) : (rem ? (e & 63u) : 0u);             \
-            rem -= mult ? n : (rem ? 1u : 0u);                                                \
-            buf <<= tu;                                                                       \
-            X -= tu;                                                                          \
-        }                                                                                     \
-    } while (0)
-
 #ifdef HUFF_SKIP_EXPERIMENT  // timing only (wrong letters): 1 = no skip codes, 2 = the wave's max for all lanes
     if constexpr (SKIP) skip = HUFF_SKIP_EXPERIMENT == 1 ? 0u : __reduce_max_sync(~0ull, skip);
 #endif
     if constexpr (SKIP) {  // codes before this lane's first letter: decoded, not kept
-        if (wtab) {  // ~2 codes per lookup (two steps <= 2 K <= 24 bits per refill)
-            uint32_t rem = skip;
-            while (rem) {
-                FX_REFILL();
-                FX_WSTEP();
-                FX_WSTEP();
-            }
-        } else {
-            for (uint32_t j = skip; j >= 2; j -= 2) {
-                FX_REFILL();
-                FX_STEP();
-                FX_STEP();
-            }
-            if (skip & 1u) {
-                FX_REFILL();
-                FX_STEP();
-            }
+        for (uint32_t j = skip; j >= 2; j -= 2) {
+            FX_REFILL();
+            FX_STEP();
+            FX_STEP();
+        }
+        if (skip & 1u) {
+            FX_REFILL();
+            FX_STEP();
         }
     }
     if (ws) HUFF_STAMP(*ws, 3);
@@ -298,7 +267,6 @@ __device__ __forceinline__ void decode_fixed64(const Words& src, uint32_t rel, u
         FX_LOOKUP(i + 1);
     }
     *end_rel = 32 * rp - (X & 63u);
-#undef FX_WSTEP
 #undef FX_STEP
 #undef FX_LOOKUP
 #undef FX_REFILL
@@ -309,11 +277,11 @@ __device__ __forceinline__ void decode_fixed64_stage(const uint32_t* stage, uint
                                                      const uint16_t* __restrict__ stab, uint32_t K,
                                                      const uint32_t* __restrict__ glut, uint32_t Ks,
                                                      uint32_t* end_rel, uint32_t skip = 0,
-                                                     WaveStamps* ws = nullptr, const uint16_t* wtab = nullptr) {
+                                                     WaveStamps* ws = nullptr) {
     if constexpr (PAD)
-        decode_fixed64<SLOW, SKIP>(PaddedLdsWords{stage}, rel, o, stab, K, glut, Ks, end_rel, skip, ws, wtab);
+        decode_fixed64<SLOW, SKIP>(PaddedLdsWords{stage}, rel, o, stab, K, glut, Ks, end_rel, skip, ws);
     else
-        decode_fixed64<SLOW, SKIP>(LdsWords{stage}, rel, o, stab, K, glut, Ks, end_rel, skip, ws, wtab);
+        decode_fixed64<SLOW, SKIP>(LdsWords{stage}, rel, o, stab, K, glut, Ks, end_rel, skip, ws);
 }
 
 // fallback for a task whose compressed range exceeds the stage: a compact
@@ -387,8 +355,7 @@ __device__ __forceinline__ void fx_check(const DecodeArgs& a, const Task& k, uin
     }
 }
 
-// NT threads per workgroup (the skip build: 512, so that 8 waves share the
-// single-symbol and walk tables at the occupancy 4 waves had with one)
+// NT threads per workgroup (HUFF_SKIP_THREADS for the skip build)
 template <bool SLOW, bool PAD, bool CHECK, bool SKIP = false, int NT = kThreads>
 __device__ __forceinline__ void decode_fixed_body(const DecodeArgs& a) {
     static_assert(!(CHECK && SKIP), "the self-check needs exact lane starts");
@@ -400,12 +367,9 @@ __device__ __forceinline__ void decode_fixed_body(const DecodeArgs& a) {
     uint16_t* stab = reinterpret_cast<uint16_t*>(lds);
     const uint32_t tab_words = (nent + 1) / 2;
     const uint32_t tab_rw = (tab_words + 3) & ~3u;
-    // the skip build's walk table follows the single-symbol table
-    const bool walk = SKIP && a.wtab;
-    const uint16_t* wtab = walk ? reinterpret_cast<const uint16_t*>(lds + tab_rw) : nullptr;
     // the wave's stage: dword view for the lane decoders, byte view for the
     // 16-B pieces (all 16-B accesses through u32x4_alias)
-    uint32_t* stage = lds + (walk ? 2 * tab_rw : tab_rw) + wave * (fx_stage_bytes<PAD>() / 4);
+    uint32_t* stage = lds + tab_rw + wave * (fx_stage_bytes<PAD>() / 4);
     uint8_t* sb = reinterpret_cast<uint8_t*>(stage);
     const uint64_t ntasks = (a.n + kTaskSym - 1) / kTaskSym;
     const uint64_t step = static_cast<uint64_t>(gridDim.x) * NW;
@@ -424,14 +388,9 @@ __device__ __forceinline__ void decode_fixed_body(const DecodeArgs& a) {
         const uint32_t tab_pieces = (tab_words + 3) / 4;
         const auto rtab = buf_rsrc(a.stab, tab_words * 4);
         constexpr int TP = (512 + NT - 1) / NT;  // 16-B pieces per thread: a table is <= 8 KiB
-        uint4 tp[TP], tw[TP];
+        uint4 tp[TP];
 #pragma unroll
         for (int i = 0; i < TP; ++i) tp[i] = buf_ld16(rtab, (t + NT * i) * 16);
-        if (walk) {
-            const auto rw = buf_rsrc(a.wtab, tab_words * 4);
-#pragma unroll
-            for (int i = 0; i < TP; ++i) tw[i] = buf_ld16(rw, (t + NT * i) * 16);
-        }
         if (have) {
             cur = task_info<SKIP>(a, task, lane);
             issue_task_loads(a, cur, lane, pre);
@@ -439,19 +398,12 @@ __device__ __forceinline__ void decode_fixed_body(const DecodeArgs& a) {
 #pragma unroll
         for (int i = 0; i < TP; ++i)
             if (t + NT * i < tab_pieces) st_stage16(lds + 4 * (t + NT * i), tp[i]);
-        if (walk) {
-#pragma unroll
-            for (int i = 0; i < TP; ++i)
-                if (t + NT * i < tab_pieces) st_stage16(lds + tab_rw + 4 * (t + NT * i), tw[i]);
-        }
         __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): table stores done; the input loads stay in flight
         __builtin_amdgcn_s_barrier();
         HUFF_STAMP(ws, 1);
         if (!have) return;
     } else {
         for (uint32_t i = t; i < tab_words; i += NT) lds[i] = reinterpret_cast<const uint32_t*>(a.stab)[i];
-        if (walk)
-            for (uint32_t i = t; i < tab_words; i += NT) lds[tab_rw + i] = reinterpret_cast<const uint32_t*>(a.wtab)[i];
         __syncthreads();
         if (task >= ntasks) return;
         cur = task_info<SKIP>(a, task, lane);
@@ -491,7 +443,7 @@ __device__ __forceinline__ void decode_fixed_body(const DecodeArgs& a) {
         } else if (cur.nsym == kTaskSym) {  // wave-uniform: every lane has 64 letters
             uint32_t o[16];
             uint32_t e = 0;
-            decode_fixed64_stage<SLOW, PAD, SKIP>(stage, rel, o, stab, K, a.lut, a.lut_bits, &e, cur.skip, &ws, wtab);
+            decode_fixed64_stage<SLOW, PAD, SKIP>(stage, rel, o, stab, K, a.lut, a.lut_bits, &e, cur.skip, &ws);
             fx_check<CHECK>(a, cur, task, lane, cur.b0 * 8 + e, true);
             HUFF_STAMP(ws, 4);
             // transpose through the stage so every store instruction writes
@@ -512,8 +464,7 @@ __device__ __forceinline__ void decode_fixed_body(const DecodeArgs& a) {
         } else if (cur.cnt) {
             uint32_t o[16];
             uint32_t e = 0;
-            decode_fixed64_stage<SLOW, PAD, SKIP>(stage, rel, o, stab, K, a.lut, a.lut_bits, &e, cur.skip, nullptr,
-                                                  wtab);
+            decode_fixed64_stage<SLOW, PAD, SKIP>(stage, rel, o, stab, K, a.lut, a.lut_bits, &e, cur.skip);
             // a lane with fewer than 64 letters decodes past its end: only full lanes are checked
             fx_check<CHECK>(a, cur, task, lane, cur.b0 * 8 + e, cur.cnt == kLaneSym);
             if (cur.cnt == kLaneSym) {
@@ -557,12 +508,9 @@ template <bool SLOW, bool PAD>
 __global__ __launch_bounds__(kThreads) void k_decode_fixed_chk(DecodeArgs a) { decode_fixed_body<SLOW, PAD, true>(a); }
 // index-free streams with k_mark_lite's entries: each lane first decodes and
 // drops its skip codes
-// The skip build's workgroup: 10 waves (640 threads) share the two tables
-// (16 KiB) beside their stages (45 KiB): two workgroups per CU hold the 20
-// waves the registers allow (5 per SIMD), as five 4-wave workgroups with one
-// table did (HUFF_SKIP_THREADS / HUFF_SKIP_WAVES: A/B builds)
+// The skip build's workgroup (HUFF_SKIP_THREADS / HUFF_SKIP_WAVES: A/B builds)
 #ifndef HUFF_SKIP_THREADS
-#define HUFF_SKIP_THREADS 640
+#define HUFF_SKIP_THREADS 256
 #endif
 #ifndef HUFF_SKIP_WAVES
 #define HUFF_SKIP_WAVES kPadWaves
@@ -580,18 +528,17 @@ __global__ __launch_bounds__(kSkipThreads) __attribute__((amdgpu_waves_per_eu(PA
 
 namespace huff::dev {
 
-size_t decode_fixed_lds_bytes(uint32_t stab_bits, bool pad, bool skip, bool walk) {
+size_t decode_fixed_lds_bytes(uint32_t stab_bits, bool pad, bool skip) {
     const size_t tab_words = ((1u << stab_bits) + 1) / 2;
     const size_t waves = skip ? kSkipThreads / 64 : kWaves;
-    return ((tab_words + 3) & ~size_t(3)) * 4 * (skip && walk ? 2 : 1) +
+    return ((tab_words + 3) & ~size_t(3)) * 4 +
            waves * (pad ? fx_stage_bytes<true>() : fx_stage_bytes<false>());
 }
 
 hipError_t launch_decode_fixed(const DecodeArgs& a, hipStream_t s) {
     if (a.n == 0) return hipSuccess;
-    if (a.wtab && a.stab_bits > 15) return hipErrorInvalidValue;  // walk entries: 4-bit bit counts
     const bool skip = a.skip_packed != 0;
-    const size_t lds = decode_fixed_lds_bytes(a.stab_bits, a.pad_stage != 0, skip, a.wtab != nullptr);
+    const size_t lds = decode_fixed_lds_bytes(a.stab_bits, a.pad_stage != 0, skip);
     const int threads = skip ? kSkipThreads : kThreads;
     const int waves = threads / 64;
     const uint64_t ntasks = (a.n + kTaskSym - 1) / kTaskSym;

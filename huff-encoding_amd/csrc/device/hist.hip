@@ -310,9 +310,17 @@ __global__ __launch_bounds__(1024) void k_scan_tsum(uint32_t tiles, uint64_t* __
 // k_scan_fix_small (<= 64 tiles, the encoder's case: one launch less): add
 // base + the totals of the tiles before, summed by one wave per tile; the
 // last tile also writes start[nchunks]
+// host: when non-null, the grand total also goes to pinned host memory as
+// (tag << 48) | total (one 8-byte store), so the host polls for it instead of
+// a device-to-host copy and a stream synchronisation
+__device__ __forceinline__ void publish_total(unsigned long long* host, uint64_t tag, uint64_t total) {
+    if (host) __hip_atomic_store(host, (tag << 48) | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 __global__ __launch_bounds__(1024) void k_scan_fix_small(uint32_t nchunks, uint64_t base,
                                                          const uint64_t* __restrict__ tsum,
-                                                         uint64_t* __restrict__ start) {
+                                                         uint64_t* __restrict__ start,
+                                                         unsigned long long* host, uint64_t tag) {
     __shared__ uint64_t off;
     const uint32_t t = threadIdx.x;
     if (t < 64) {
@@ -324,18 +332,26 @@ __global__ __launch_bounds__(1024) void k_scan_fix_small(uint32_t nchunks, uint6
     __syncthreads();
     const uint32_t i = blockIdx.x * 1024 + t;
     if (i < nchunks) start[i] += off;
-    if (blockIdx.x == gridDim.x - 1 && t == 0) start[nchunks] = off + tsum[blockIdx.x];
+    if (blockIdx.x == gridDim.x - 1 && t == 0) {
+        const uint64_t end = off + tsum[blockIdx.x];
+        start[nchunks] = end;
+        publish_total(host, tag, end - base);
+    }
 }
 
 // k_scan_fix: add base + the exclusive prefix of the tile totals; the last
 // tile also writes start[nchunks]
 __global__ __launch_bounds__(1024) void k_scan_fix(uint32_t nchunks, uint64_t base, const uint64_t* __restrict__ tsum,
-                                                   uint64_t* __restrict__ start) {
+                                                   uint64_t* __restrict__ start, unsigned long long* host,
+                                                   uint64_t tag) {
     const uint32_t t = threadIdx.x;
     const uint64_t off = base + tsum[blockIdx.x];
     const uint32_t i = blockIdx.x * 1024 + t;
     if (i < nchunks) start[i] += off;
-    if (blockIdx.x == gridDim.x - 1 && t == 0) start[nchunks] = base + tsum[gridDim.x];
+    if (blockIdx.x == gridDim.x - 1 && t == 0) {
+        start[nchunks] = base + tsum[gridDim.x];
+        publish_total(host, tag, tsum[gridDim.x]);
+    }
 }
 
 // lowest index i with missing_mask[in[i]] != 0 (error path of compress_with_tree)
@@ -389,14 +405,16 @@ hipError_t launch_chunk_bits(const uint32_t* chunk_hist, uint32_t nchunks, const
 }
 
 hipError_t launch_scan(const uint64_t* bits, uint32_t nchunks, uint64_t base, uint64_t* start, uint64_t* tsum,
-                       hipStream_t s) {
+                       hipStream_t s, HistDone done) {
     const uint32_t tiles = nchunks ? (nchunks + 1023) / 1024 : 1;
     hipLaunchKernelGGL(k_scan_tiles, dim3(tiles), dim3(1024), 0, s, bits, nchunks, start, tsum);
     if (tiles <= 64) {
-        hipLaunchKernelGGL(k_scan_fix_small, dim3(tiles), dim3(1024), 0, s, nchunks, base, tsum, start);
+        hipLaunchKernelGGL(k_scan_fix_small, dim3(tiles), dim3(1024), 0, s, nchunks, base, tsum, start, done.host,
+                           done.tag);
     } else {
         hipLaunchKernelGGL(k_scan_tsum, dim3(1), dim3(1024), 0, s, tiles, tsum);
-        hipLaunchKernelGGL(k_scan_fix, dim3(tiles), dim3(1024), 0, s, nchunks, base, tsum, start);
+        hipLaunchKernelGGL(k_scan_fix, dim3(tiles), dim3(1024), 0, s, nchunks, base, tsum, start, done.host,
+                           done.tag);
     }
     return hipGetLastError();
 }

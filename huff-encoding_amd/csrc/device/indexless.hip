@@ -48,6 +48,7 @@ struct Seg {
     uint64_t nseg;
     const uint32_t* lut;
     uint32_t K;
+    unsigned long long* wtot;  // per-workgroup code counts of the staged pass (256 segments each), or null
 };
 
 __device__ __forceinline__ void load_prim(uint32_t* plut, const Seg& g) {
@@ -110,6 +111,7 @@ __device__ __forceinline__ void fix_one(const Seg& g, uint64_t* __restrict__ s, 
         if (a.pos == b.pos) {  // merged: same exit, count corrected
             s[i] = ns;
             c[i] = c[i] - cb + ca;
+            if (g.wtot && ca != cb) atomicAdd(g.wtot + i / kThreads, static_cast<unsigned long long>(ca - cb));
             // the old path met the speculative one at old-local tm1 with shift
             // dl1; the new path meets the old one at (ca, cb)
             const uint32_t tm1 = tm[i];
@@ -123,6 +125,7 @@ __device__ __forceinline__ void fix_one(const Seg& g, uint64_t* __restrict__ s, 
         }
         if (a.pos >= end || !a_alive) {  // new exit
             s[i] = ns;
+            if (g.wtot && ca != c[i]) atomicAdd(g.wtot + i / kThreads, static_cast<unsigned long long>(ca - c[i]));
             c[i] = ca;
             tm[i] = kNoMerge;
             if (a.pos != x[i]) {
@@ -196,6 +199,7 @@ __global__ void k_settle(Seg g, uint64_t* __restrict__ s, uint64_t* __restrict__
         }
         s[i] = ns;
         x[i] = rd.pos;
+        if (g.wtot) g.wtot[i / kThreads] += cnt - c[i];  // one lane: no other writer
         c[i] = cnt;
         tm[i] = kNoMerge;
     }
@@ -223,7 +227,7 @@ __global__ __launch_bounds__(kThreads) void k_emit(Seg g, const uint64_t* __rest
 }
 
 Seg make_seg(const IndexlessArgs& a) {
-    return Seg{a.comp, a.comp_bytes, a.valid_bits, a.seg_bits, a.nseg, a.lut, a.lut_bits};
+    return Seg{a.comp, a.comp_bytes, a.valid_bits, a.seg_bits, a.nseg, a.lut, a.lut_bits, a.wtot};
 }
 
 // ---- LDS-staged variants (every code <= 32 bits; segwalk.hpp) -------------
@@ -304,43 +308,20 @@ __global__ __launch_bounds__(kThreads) void k_spec_lds(IndexlessArgs a) {
         pc = cur;
         pcn = cnt;
     };
-    // the first multi-code chunk's window ends (bits | codes << 16 from
-    // start; ~0u: none), boundaries of this path that the fix-up below can
-    // merge on long before the first sample
-    uint32_t cq[kChunkSteps];
-#pragma unroll
-    for (int k = 0; k < kChunkSteps; ++k) cq[k] = ~0u;
     if (wtab) {
-        // multi-code chunks (window ends: boundaries of this path) while every
-        // window ends below `end`; the chunk whose windows reach `end` is cut
-        // back to the start of its first such window (the exit lies in it or
-        // at its end) and the cursor re-seated there for the single steps
-        // below (walking the last ~8 K bits in single steps cost a tenth of
-        // the pass: phase stamps)
-        bool first = true;
-        for (;;) {
-            uint32_t U, N, q[kChunkSteps];
-            c.multi_chunk<SLOW>(U, N, q, wtab, stab, K, a.lut, Kg);
-            const bool below = cur + U < end;
-            uint32_t base = 0;
-#pragma unroll
-            for (int k = 0; k < kChunkSteps; ++k) {
-                const bool in = cur + (q[k] & 0xFFFFu) < end;
-                base = in ? q[k] : base;
-                if (first) cq[k] = in ? q[k] : ~0u;
-            }
-            first = false;
-            if (below) {
-                cur += U;
-                cnt += N;
-                note_sample();
-                continue;
-            }
-            cur += base & 0xFFFFu;
-            cnt += base >> 16;
-            c.init(st, cur);
+        // multi-code chunks while the chunk's last boundary stays below `end`
+        // (so no boundary inside it can be the exit); single codes after.
+        // (Cutting the chunk that reaches `end` back to its window, so the
+        // single codes walk one window instead of ~8 K bits: exit walk 3.8 K
+        // -> 1.2 K cycles per wave, the multi-code walk 18.0 K -> 21.1 K for
+        // the running totals it needs; phase stamps, DESIGN §11. Not kept.)
+        const uint64_t span = static_cast<uint64_t>(kChunkSteps) * (a.max_len > K ? a.max_len : K);
+        while (cur + span < end) {
+            uint32_t U, N;
+            c.multi_chunk<SLOW>(U, N, wtab, stab, K, a.lut, Kg);
+            cur += U;
+            cnt += N;
             note_sample();
-            break;
         }
     }
     HUFF_STAMP(ws, 2);
@@ -394,50 +375,9 @@ __global__ __launch_bounds__(kThreads) void k_spec_lds(IndexlessArgs a) {
         Cursor ca_;
         ca_.init(st, ns);
         uint64_t pa = ns, na = 0;
-        // merge candidates in ascending order: the first chunk's window ends
-        // (cq), then the samples; pk / ik = the current one (position,
-        // spec-local index), the first at or after the walk's position
-        uint64_t pk = ~0ull;
-        uint32_t ik = 0, k = 0;
-        auto next_candidate = [&](uint64_t at) {
-            uint64_t best = ~0ull;
-            uint32_t bi = 0;
-#pragma unroll
-            for (int j = kChunkSteps - 1; j >= 0; --j) {  // the first window end >= at
-                const uint64_t pj = cq[j] == ~0u ? ~0ull : start + (cq[j] & 0xFFFFu);
-                const bool ok = pj >= at;
-                best = ok ? pj : best;
-                bi = ok ? (cq[j] >> 16) : bi;
-            }
-            if (best == ~0ull) {  // past the window ends: the samples
-                while (true) {
-                    uint32_t sv;
-                    uint64_t ps;
-                    if (k == 0) {
-                        ps = sp1;
-                        sv = 0;
-                        bi = si1;
-                    } else {
-                        sv = k < a.nsamp ? smp[k] : ~0u;
-                        ps = sv == ~0u ? ~0ull : start + samp_off(sv);
-                        bi = samp_idx(sv);
-                    }
-                    if (ps >= at || ps == ~0ull) {
-                        best = ps;
-                        break;
-                    }
-                    ++k;
-                }
-            }
-            pk = best;
-            ik = bi;
-        };
-        next_candidate(ns);
-        if (pk == ns) {  // the predecessor's exit is a boundary of this path: merged at once
-            tm_out = 0;
-            dl_out = -static_cast<int32_t>(ik);
-            cnt = static_cast<uint64_t>(static_cast<int64_t>(cnt) + dl_out);
-        } else for (;;) {
+        uint64_t pk = sp1;        // current sample: position, spec-local index
+        uint32_t ik = si1, k = 1;
+        for (;;) {
             uint32_t L[kChunkSteps];
             ca_.chunk<SLOW>(L, stab, K, a.lut, Kg);
             uint64_t p = pa;
@@ -470,14 +410,11 @@ __global__ __launch_bounds__(kThreads) void k_spec_lds(IndexlessArgs a) {
             }
             pa = p;
             na += kChunkSteps;
-            if (pa > pk) {  // passed it without landing on it: the next one
-                next_candidate(pa);
-                if (pk == pa) {  // the chunk's last boundary is that one: merged there
-                    tm_out = static_cast<uint32_t>(na);
-                    dl_out = static_cast<int32_t>(static_cast<int64_t>(na) - static_cast<int64_t>(ik));
-                    cnt = static_cast<uint64_t>(static_cast<int64_t>(cnt) + dl_out);
-                    break;
-                }
+            while (pa > pk) {  // passed the sample without landing on it: the next one
+                const uint32_t sv = k < a.nsamp ? smp[k] : ~0u;
+                ++k;
+                pk = sv == ~0u ? ~0ull : start + samp_off(sv);
+                ik = samp_idx(sv);
             }
         }
         s_out = ns;
@@ -489,6 +426,18 @@ __global__ __launch_bounds__(kThreads) void k_spec_lds(IndexlessArgs a) {
     }
     HUFF_STAMP(ws, 5);
     ws.flush(a.stamps, static_cast<uint64_t>(blockIdx.x) * (kThreads / 64) + (threadIdx.x >> 6));
+    if (a.wtot) {  // the workgroup's code count, for the scan over workgroups (k_mark_lite scans inside)
+        __shared__ uint32_t wsum[kThreads / 64];
+        const uint32_t incl = wave_scan_incl(live ? static_cast<uint32_t>(cnt) : 0u);
+        if ((threadIdx.x & 63) == 63) wsum[threadIdx.x >> 6] = incl;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint64_t tot = 0;
+#pragma unroll
+            for (int w = 0; w < kThreads / 64; ++w) tot += wsum[w];
+            a.wtot[blockIdx.x] = tot;
+        }
+    }
     if (!live) return;
     a.s[i] = s_out;
     a.x[i] = cur;
@@ -563,12 +512,32 @@ __global__ __launch_bounds__(kThreads) void k_mark_lds(IndexlessArgs a, const ui
 // boundary it would walk from and the number of codes to walk, and the
 // fixed-count decoder (skip build) decodes those codes without storing them.
 // No staging and no table: only the segment records and its samples.
+// Segment offsets: off[i] (the scan over segments), or, with woff (the scan
+// over the speculative pass's workgroups, 256 segments each), the
+// workgroup's offset plus the exclusive scan of its segments' counts done
+// here (DPP wave scans + 4 wave totals): the segment-wide scan kernels and
+// the off[] round trip are not run.
 __global__ __launch_bounds__(kThreads) void k_mark_lite(IndexlessArgs a, const uint64_t* __restrict__ off,
+                                                        const unsigned long long* __restrict__ woff,
                                                         uint64_t* __restrict__ sub_abs) {
     const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-    if (i >= a.nseg) return;
-    const uint64_t j0 = off[i];
-    const uint64_t cnt = a.c[i];
+    uint64_t j0, cnt;
+    if (woff) {
+        __shared__ uint32_t wsum[kThreads / 64];
+        cnt = i < a.nseg ? a.c[i] : 0;
+        const uint32_t incl = wave_scan_incl(static_cast<uint32_t>(cnt));  // a workgroup's counts sum < 2^32
+        if ((threadIdx.x & 63) == 63) wsum[threadIdx.x >> 6] = incl;
+        __syncthreads();
+        uint32_t pre = 0;
+#pragma unroll
+        for (uint32_t w = 0; w < kThreads / 64; ++w) pre += w < (threadIdx.x >> 6) ? wsum[w] : 0u;
+        j0 = woff[blockIdx.x] + pre + incl - static_cast<uint32_t>(cnt);
+        if (i >= a.nseg) return;
+    } else {
+        if (i >= a.nseg) return;
+        j0 = off[i];
+        cnt = a.c[i];
+    }
     uint64_t m = (j0 + kIdx - 1) & ~static_cast<uint64_t>(kIdx - 1);
     if (m >= j0 + cnt) return;
     const uint64_t s_true = a.s[i];
@@ -598,22 +567,24 @@ __global__ __launch_bounds__(kThreads) void k_mark_lite(IndexlessArgs a, const u
 
 }  // namespace
 
-hipError_t launch_indexless_mark_lite(const IndexlessArgs& a, const uint64_t* off, uint64_t* sub_abs,
-                                      hipStream_t st) {
+hipError_t launch_indexless_mark_lite(const IndexlessArgs& a, const uint64_t* off, const unsigned long long* woff,
+                                      uint64_t* sub_abs, hipStream_t st) {
     if (a.nseg == 0) return hipSuccess;
-    if (!a.samp) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_mark_lite, dim3((a.nseg + kThreads - 1) / kThreads), dim3(kThreads), 0, st, a, off, sub_abs);
+    if (!a.samp || (!off && !woff)) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_mark_lite, dim3((a.nseg + kThreads - 1) / kThreads), dim3(kThreads), 0, st, a, off, woff,
+                       sub_abs);
     return hipGetLastError();
 }
 
-static size_t lds_staged_bytes(const IndexlessArgs& a) {
+static size_t lds_staged_bytes(const IndexlessArgs& a, uint32_t segs) {
     return static_cast<size_t>((((((1u << a.stab_bits) + 1) / 2) + 3) & ~3u) + a.l2_words) * 4 +
-           ((kThreads * a.seg_bits + 7) / 8 + 128 + 15) / 16 * 16;
+           ((segs * a.seg_bits + 7) / 8 + 128 + 15) / 16 * 16;
 }
 
 static bool use_staged(const IndexlessArgs& a) {
     // (the sample words hold 10-bit offsets and counts: segments < 1024 bits)
-    return a.stab && a.stab_bits && a.max_len <= 32 && a.seg_bits < 1024 && lds_staged_bytes(a) <= 160 * 1024;
+    return a.stab && a.stab_bits && a.max_len <= 32 && a.seg_bits < 1024 &&
+           lds_staged_bytes(a, kThreads) <= 160 * 1024;
 }
 
 hipError_t launch_indexless_mark(const IndexlessArgs& a, const uint64_t* off, uint64_t* sub_abs, uint32_t shift,
@@ -624,7 +595,7 @@ hipError_t launch_indexless_mark(const IndexlessArgs& a, const uint64_t* off, ui
     IndexlessArgs m = a;
     m.wtab = nullptr;  // single steps: the walks stop at exact counts
     hipLaunchKernelGGL(slow ? k_mark_lds<true> : k_mark_lds<false>, dim3((m.nseg + kThreads - 1) / kThreads),
-                       dim3(kThreads), lds_staged_bytes(m), st, m, off, sub_abs, shift);
+                       dim3(kThreads), lds_staged_bytes(m, kThreads), st, m, off, sub_abs, shift);
     return hipGetLastError();
 }
 
@@ -636,7 +607,7 @@ hipError_t launch_indexless_spec(const IndexlessArgs& a, hipStream_t st) {
         if (!a.samp) return hipErrorInvalidValue;
         const bool slow = a.max_len > a.stab_bits;
         hipLaunchKernelGGL(slow ? k_spec_lds<true> : k_spec_lds<false>, dim3((a.nseg + kThreads - 1) / kThreads),
-                           dim3(kThreads), lds_staged_bytes(a), st, a);
+                           dim3(kThreads), lds_staged_bytes(a, kThreads), st, a);
         return hipGetLastError();
     }
     const Seg g = make_seg(a);

@@ -107,9 +107,6 @@ struct DecodeArgs {
     // err: u32[8] mismatch count + first (task, lane, want, got)
     uint32_t check_mode;
     uint32_t* err;
-    // skip build (skip_packed): the walk table over the same stab_bits-bit
-    // windows (IndexlessArgs::wtab), so the skip codes go ~2 per lookup
-    const uint16_t* wtab;
     uint64_t* stamps;             // timing builds (-DHUFF_STAMPS) only: per-wave phase stamps
 };
 // whether k_decode_fixed should swizzle its stage for this mean code
@@ -167,6 +164,10 @@ struct IndexlessArgs {
     // the global multi-level table `lut`
     const uint32_t* l2;
     uint32_t l2_words;
+    // (LDS-staged path) the code count of each workgroup's 256 segments,
+    // written by the speculative pass and kept by the fix-up kernels (atomic
+    // deltas): the scan runs over workgroups, k_mark_lite scans inside one
+    unsigned long long* wtot;
     uint64_t* stamps;             // timing builds (-DHUFF_STAMPS) only: per-wave phase stamps
 };
 constexpr uint32_t kSampBits = 128;
@@ -274,6 +275,7 @@ struct WCountArgs {
     unsigned long long *keys_lo, *keys_hi, *counts, *sent;
     unsigned int* state;
     unsigned long long *out_lo, *out_hi, *out_c, *nout;
+    uint64_t out_cap;             // k_wextract stores only indices < out_cap (it counts them all in *nout)
     unsigned long long* used;
     unsigned int* overflow;
     uint32_t unbounded;
@@ -345,6 +347,8 @@ constexpr uint32_t kDecodeFixedCheck = 11;
 
 // Pass 1's totals straight to pinned host memory (device-visible pointer):
 // host[b] = (tag << 48) | total_b. host == nullptr: the totals stay in gw.
+// a result published straight to pinned host memory: (tag << 48) | value
+// in one 8-byte store (pass 1's weights, a scan's grand total)
 struct HistDone {
     unsigned long long* host = nullptr;
     uint64_t tag = 0;  // 16 bits
@@ -372,7 +376,7 @@ hipError_t launch_chunk_bits(const uint32_t* chunk_hist, uint32_t nchunks, const
                              hipStream_t s);
 // tsum: scratch of ceil(nchunks / 1024) (>= 1) u64
 hipError_t launch_scan(const uint64_t* bits, uint32_t nchunks, uint64_t base, uint64_t* start, uint64_t* tsum,
-                       hipStream_t s);
+                       hipStream_t s, HistDone done = HistDone{});
 hipError_t launch_pack(bool long_codes, const PackArgs& a, hipStream_t s);
 hipError_t launch_decode(const DecodeArgs& a, hipStream_t s);
 hipError_t launch_decode_fixed(const DecodeArgs& a, hipStream_t s);
@@ -387,7 +391,10 @@ hipError_t launch_indexless_emit(const IndexlessArgs& a, const uint64_t* off, ui
 // decoders' 256-symbol runs; 6: k_decode_fixed's kIdx = 64)
 // sub_abs[g] = (a boundary at or before symbol 64 g) | (codes from it to the
 // symbol) << 48, without walking: the decoder skips the codes (k_mark_lite)
-hipError_t launch_indexless_mark_lite(const IndexlessArgs& a, const uint64_t* off, uint64_t* sub_abs, hipStream_t st);
+// off: per-segment offsets, or null and woff: per-workgroup offsets (the
+// scan of IndexlessArgs::wtot; k_mark_lite scans inside each workgroup)
+hipError_t launch_indexless_mark_lite(const IndexlessArgs& a, const uint64_t* off, const unsigned long long* woff,
+                                      uint64_t* sub_abs, hipStream_t st);
 constexpr uint64_t kSkipPosMask = (1ull << 48) - 1;
 hipError_t launch_indexless_mark(const IndexlessArgs& a, const uint64_t* off, uint64_t* sub_abs, uint32_t shift,
                                  hipStream_t s);

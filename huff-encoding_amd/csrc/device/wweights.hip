@@ -211,12 +211,13 @@ __global__ __launch_bounds__(kT) void k_wextract(const unsigned long long* __res
                                                  unsigned long long* __restrict__ out_lo,
                                                  unsigned long long* __restrict__ out_hi,
                                                  unsigned long long* __restrict__ out_c,
-                                                 unsigned long long* __restrict__ nout) {
+                                                 unsigned long long* __restrict__ nout, uint64_t cap) {
     const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kT;
     for (uint64_t s = static_cast<uint64_t>(blockIdx.x) * kT + threadIdx.x; s < slots; s += stride) {
         const uint64_t c = counts[s];
         if (!c) continue;
         const uint64_t j = atomicAdd(nout, 1ull);
+        if (j >= cap) continue;  // counted, not stored: the host reports more used slots than claims
         out_lo[j] = klo[s];
         if (khi) out_hi[j] = khi[s];
         out_c[j] = c;
@@ -277,7 +278,7 @@ hipError_t wcount_launch(const WCountArgs& a, hipStream_t st) {
 hipError_t wextract_launch(const WCountArgs& a, hipStream_t st) {
     if (a.n == 0 || a.width <= 2) return hipSuccess;
     hipLaunchKernelGGL(k_wextract, dim3(grid_for(a.slots, 16, 8192)), dim3(kT), 0, st, a.keys_lo,
-                       a.width == 16 ? a.keys_hi : nullptr, a.counts, a.slots, a.out_lo, a.out_hi, a.out_c, a.nout);
+                       a.width == 16 ? a.keys_hi : nullptr, a.counts, a.slots, a.out_lo, a.out_hi, a.out_c, a.nout, a.out_cap);
     return hipGetLastError();
 }
 

@@ -1051,7 +1051,7 @@ huff::IndexlessSync& huff_ctx::indexless_ws() {
 namespace huff {
 
 Status indexless_sync(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_bytes, uint64_t valid_bits,
-                      const huff_tree* t, IndexlessSync& st) {
+                      const huff_tree* t, IndexlessSync& st, bool need_off) {
     const DecTables* dt = st.dt;
     // segment length: a multiple of the gcd of all code lengths
     uint32_t g = 0;
@@ -1083,7 +1083,10 @@ Status indexless_sync(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_bytes,
     HUFF_TRY(st.off.ensure((nseg + 1) * 8));
     HUFF_TRY(st.tm.ensure(nseg * 4));
     HUFF_TRY(st.dl.ensure(nseg * 4));
-    HUFF_TRY(st.flag.ensure((dev::kFixRounds + 1) * 4));
+    HUFF_TRY(st.flag.ensure(32));  // kFixRounds + 1 words, zeroed by one aligned fill
+    const uint64_t nwg = (nseg + 255) / 256;  // workgroups of the staged speculative pass
+    HUFF_TRY(st.wtot.ensure(nwg * 8));
+    HUFF_TRY(st.woff.ensure((nwg + 1) * 8));
     dev::IndexlessArgs& a = st.a;
     a = dev::IndexlessArgs{};
     a.comp = d_comp;
@@ -1119,21 +1122,56 @@ Status indexless_sync(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_bytes,
         a.samp = static_cast<uint32_t*>(st.samp.p);
         HUFF_TRY(st.fixlist.ensure(nseg * 4 + 4));
         a.fixlist = static_cast<uint32_t*>(st.fixlist.p);
+        a.wtot = static_cast<unsigned long long*>(st.wtot.p);
     } else {  // k_spec leaves the merge record to the fix-up rounds
         HIP_TRY(hipMemsetAsync(st.tm.p, 0, nseg * 4, strm));
         HIP_TRY(hipMemsetAsync(st.dl.p, 0, nseg * 4, strm));
     }
-    HIP_TRY(hipMemsetAsync(st.flag.p, 0, (dev::kFixRounds + 1) * 4, strm));
+    static_assert((dev::kFixRounds + 1) * 4 <= 32, "the flags fit the zeroed 32 bytes");
+    HIP_TRY(hipMemsetAsync(st.flag.p, 0, 32, strm));
     HIP_TRY(dev::launch_indexless_spec(a, strm));
     // fix-up rounds and the sequential fallback decide on the device whether
     // they have work (no host wait between rounds)
     HIP_TRY(dev::launch_indexless_settle_all(a, strm));
     HUFF_TRY(st.tsum.ensure((nseg / 1024 + 2) * 8));
-    HIP_TRY(dev::launch_scan(static_cast<const uint64_t*>(st.c.p), static_cast<uint32_t>(nseg), 0,
-                             static_cast<uint64_t*>(st.off.p), static_cast<uint64_t*>(st.tsum.p), strm));
     st.total = 0;
-    HIP_TRY(hipMemcpyAsync(&st.total, static_cast<uint64_t*>(st.off.p) + nseg, 8, hipMemcpyDeviceToHost, strm));
-    return ctx->sync();
+    // the staged pass keeps per-workgroup counts: only they are scanned
+    // (k_mark_lite scans inside a workgroup), unless a consumer needs every
+    // segment's offset (the walked marks, k_emit)
+    st.block_off = a.wtot && !need_off;
+    // the total goes from the scan's last kernel straight to pinned host
+    // memory, tagged; the host polls it (a copy and a stream
+    // synchronisation here cost ~40 us between the sync and the decode)
+    HUFF_TRY(ctx->pin_total.ensure(8));
+    if (!ctx->pin_total_dev) {
+        std::memset(ctx->pin_total.p, 0, 8);
+        HIP_TRY(hipHostGetDevicePointer(&ctx->pin_total_dev, ctx->pin_total.p, 0));
+    }
+    dev::HistDone done;
+    done.host = static_cast<unsigned long long*>(ctx->pin_total_dev);
+    ctx->total_seq = (ctx->total_seq % 0xFFFF) + 1;  // 1..65535: never the zeroed word's tag
+    done.tag = ctx->total_seq;
+    if (st.block_off) {
+        HIP_TRY(dev::launch_scan(static_cast<const uint64_t*>(st.wtot.p), static_cast<uint32_t>(nwg), 0,
+                                 static_cast<uint64_t*>(st.woff.p), static_cast<uint64_t*>(st.tsum.p), strm, done));
+    } else {
+        HIP_TRY(dev::launch_scan(static_cast<const uint64_t*>(st.c.p), static_cast<uint32_t>(nseg), 0,
+                                 static_cast<uint64_t*>(st.off.p), static_cast<uint64_t*>(st.tsum.p), strm, done));
+    }
+    const uint64_t* hw = static_cast<const uint64_t*>(ctx->pin_total.p);
+    for (uint64_t spin = 0;; ++spin) {
+        const uint64_t v = __atomic_load_n(hw, __ATOMIC_ACQUIRE);
+        if ((v >> 48) == done.tag) {
+            st.total = v & ((1ull << 48) - 1);
+            return Status::ok();
+        }
+        if ((spin & 1023) == 1023) {
+            const hipError_t q = hipStreamQuery(strm);
+            if (q == hipSuccess && (__atomic_load_n(hw, __ATOMIC_ACQUIRE) >> 48) != done.tag)
+                return Status::err(HUFF_E_HIP, "the index-free scan finished without publishing its total");
+            if (q != hipSuccess && q != hipErrorNotReady) HIP_TRY(q);
+        }
+    }
 }
 
 Status indexless_mark(huff_ctx* ctx, IndexlessSync& st, DevBuf& sub_abs, uint32_t shift) {
@@ -1228,7 +1266,8 @@ Status decode_indexless_dev(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_
     }
     IndexlessSync& st = ctx->indexless_ws();
     st.dt = dt;
-    HUFF_TRY(indexless_sync(ctx, d_comp, comp_bytes, valid_bits, t, st));
+    // k_emit (codes > 32 bits) and the walked marks of the check build read every segment's offset
+    HUFF_TRY(indexless_sync(ctx, d_comp, comp_bytes, valid_bits, t, st, decode_check_mode() != 0));
     const uint64_t total = st.total;
     *nsym = total;
     if (total == 0) HUFF_TRY(walk_end(nullptr, 0, nullptr, 0));
@@ -1248,8 +1287,10 @@ Status decode_indexless_dev(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_
             HUFF_TRY(indexless_mark(ctx, st, sub_abs, 6));
         } else {
             HUFF_TRY(sub_abs.ensure(((total + 63) >> 6) * 8 + 8));
-            HIP_TRY(dev::launch_indexless_mark_lite(st.a, static_cast<const uint64_t*>(st.off.p),
-                                                    static_cast<uint64_t*>(sub_abs.p), strm));
+            HIP_TRY(dev::launch_indexless_mark_lite(
+                st.a, st.block_off ? nullptr : static_cast<const uint64_t*>(st.off.p),
+                st.block_off ? static_cast<const unsigned long long*>(st.woff.p) : nullptr,
+                static_cast<uint64_t*>(sub_abs.p), strm));
         }
         const uint64_t m = ((total - 1) >> 6) << 6;  // the last mark: symbol m
         HUFF_TRY(walk_end(static_cast<const uint64_t*>(sub_abs.p) + (m >> 6), 0, nullptr, total - m, !check));
@@ -1261,10 +1302,6 @@ Status decode_indexless_dev(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_
         d.lut_words = static_cast<uint32_t>(dt->lut.size());
         d.sub_abs64 = static_cast<const uint64_t*>(sub_abs.p);
         d.skip_packed = check ? 0u : 1u;
-        // the skip codes through the walk table (HUFF_SKIP_WALK=0: one code per lookup, A/B)
-        const char* sw = std::getenv("HUFF_SKIP_WALK");
-        if (!check && dt->sbits <= 15 && !(sw && *sw == '0'))
-            d.wtab = reinterpret_cast<const uint16_t*>(static_cast<const uint32_t*>(ctx->d_lut.p) + dt->woff);
         d.end_bit = valid_bits;
         d.nchunks = static_cast<uint32_t>((total + dev::kChunk - 1) / dev::kChunk);
         d.max_len = dt->maxdepth;

@@ -135,6 +135,9 @@ struct huff_ctx {
     PinnedBuf pin_w;     // weights readback: 256 tagged totals written by pass 1
     void* pin_w_dev = nullptr;
     uint64_t hist_seq = 0;
+    PinnedBuf pin_total;  // the index-free decode's symbol count, tagged, written by its scan
+    void* pin_total_dev = nullptr;
+    uint64_t total_seq = 0;
     PinnedBuf pin_lut;   // decode table upload
     DevBuf d_in, d_out;  // staging of the host-pointer API
     DevBuf d_lut;
@@ -247,11 +250,15 @@ Status decode_indexless_dev(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_
 struct IndexlessSync {
     const DecTables* dt = nullptr;  // tables of the tree, uploaded to ctx->d_lut
     DevBuf s, x0, c, off, flag, tsum, samp, tm, dl, fixlist;
+    DevBuf wtot, woff;  // per-workgroup code counts of the staged pass and their exclusive scan
     dev::IndexlessArgs a{};
     uint64_t total = 0;
+    bool block_off = false;  // offsets per workgroup (woff) only; off[] not written
 };
+// need_off: every segment's offset in `off` (else, on the staged path, only
+// the per-workgroup offsets in `woff`: k_mark_lite's form)
 Status indexless_sync(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_bytes, uint64_t valid_bits,
-                      const huff_tree* t, IndexlessSync& st);
+                      const huff_tree* t, IndexlessSync& st, bool need_off = true);
 // sub_abs[g] = first bit of symbol g << shift (needs dev::indexless_staged(st.a))
 Status indexless_mark(huff_ctx* ctx, IndexlessSync& st, DevBuf& sub_abs, uint32_t shift = 8);
 Status decode_indexless_host(huff_ctx* ctx, const uint8_t* comp, size_t len, uint64_t valid_bits,

@@ -302,6 +302,7 @@ Status wweights_map_host(huff_ctx* ctx, uint32_t width, const uint8_t* letters, 
     a.out_lo = static_cast<unsigned long long*>(olo.p);
     a.out_c = static_cast<unsigned long long*>(oc.p);
     a.out_hi = width == 16 ? static_cast<unsigned long long*>(ohi.p) : nullptr;
+    a.out_cap = cap;  // a guard the kernel enforces, so the check below comes before any overrun
     HIP_TRY(dev::wextract_launch(a, s));
     HIP_TRY(hipMemcpyAsync(m, misc.p, 8, hipMemcpyDeviceToHost, s));
     HUFF_TRY(ctx->sync());
@@ -382,7 +383,10 @@ Status wdecode_indexless_dev(huff_ctx* ctx, const huff_wtree* t, const uint8_t* 
     HUFF_TRY(ctx->upload_dec_tables(shape, &dt));
     IndexlessSync& st = ctx->indexless_ws();
     st.dt = dt;
-    HUFF_TRY(indexless_sync(ctx, d_comp, comp_bytes, valid_bits, shape, st));
+    const WideDecTables* wdt = nullptr;
+    HUFF_TRY(t->dec_tables(&wdt));
+    const bool skip = !wdt->stab.empty() && !std::getenv("HUFF_WIDE_MARK_WALK");
+    HUFF_TRY(indexless_sync(ctx, d_comp, comp_bytes, valid_bits, shape, st, !skip));
     *n_out = st.total;
     if (!d_out) return Status::err(HUFF_E_BUFFER_TOO_SMALL, "output buffer too small");
     if (st.total > cap_letters) return Status::err(HUFF_E_BUFFER_TOO_SMALL, "output buffer too small");
@@ -393,13 +397,12 @@ Status wdecode_indexless_dev(huff_ctx* ctx, const huff_wtree* t, const uint8_t* 
     // takes k_mark_lite's marks (a boundary and the codes to skip from it, as
     // the byte path's skip build); HUFF_WIDE_MARK_WALK=1 or the long-code
     // decoder: exact points walked by k_mark_lds
-    const WideDecTables* wdt = nullptr;
-    HUFF_TRY(t->dec_tables(&wdt));
-    const bool skip = !wdt->stab.empty() && !std::getenv("HUFF_WIDE_MARK_WALK");
     if (skip) {
         HUFF_TRY(sub_abs.ensure(((st.total + 63) >> 6) * 8 + 8));
-        HIP_TRY(dev::launch_indexless_mark_lite(st.a, static_cast<const uint64_t*>(st.off.p),
-                                                static_cast<uint64_t*>(sub_abs.p), ctx->stream));
+        HIP_TRY(dev::launch_indexless_mark_lite(
+            st.a, st.block_off ? nullptr : static_cast<const uint64_t*>(st.off.p),
+            st.block_off ? static_cast<const unsigned long long*>(st.woff.p) : nullptr,
+            static_cast<uint64_t*>(sub_abs.p), ctx->stream));
     } else {
         HUFF_TRY(indexless_mark(ctx, st, sub_abs, 6));
     }

@@ -145,7 +145,11 @@ def test_batch_limits(H, O, ctx):
     ot = O.Tree.from_weights(O.weights_from_array(rows[1].astype(np.uint64)))
     assert t.tree_nbits.cpu().numpy()[1] == len(ot.as_bin())
     data = torch.zeros(100, dtype=torch.uint8, device="cuda")
+    data[40:50] = 7
+    # a descending pair is an empty stream, in the C API and the wrapper alike
+    h = batch.batch_hist(ctx, data, torch.tensor([0, 50, 40, 60], dtype=torch.int64, device="cuda")).cpu().numpy()
+    assert h[0, 0] == 40 and h[0, 7] == 10 and h[1].sum() == 0 and h[2, 0] == 10 and h[2, 7] == 10
     with pytest.raises(ValueError):
-        batch.batch_hist(ctx, data, torch.tensor([0, 50, 40], dtype=torch.int64, device="cuda"))
+        batch.batch_hist(ctx, data, torch.tensor([0, -1], dtype=torch.int64, device="cuda"))
     with pytest.raises(ValueError):
         batch.batch_hist(ctx, data, torch.tensor([0, 101], dtype=torch.int64, device="cuda"))

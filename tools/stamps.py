@@ -9,9 +9,10 @@ Runs the indexed decode and the index-free decode of a 1 GiB stream once
 each (after warm-up calls), reads the stamp regions the timing build wrote
 (runtime.cpp huff_diag_stamps; 10 words per wave, bitreader.hpp WaveStamps)
 and prints one JSON line: per kernel, the mean / median cycles of every
-phase of a wave, the wave lifetime, the kernel's span in cycles (first
-entry to last stamp), and the mean number of waves resident per CU over the
-span (sum of lifetimes / span / CUs). s_memtime ticks at the shader clock.
+phase of a wave, the wave lifetime, the kernel's span in cycles per
+XCC (first entry to last stamp; s_memtime counters are per XCD) and the mean
+number of waves resident per CU over it (sum of lifetimes / span / CUs).
+s_memtime ticks at the shader clock.
 """
 import argparse
 import ctypes as C
@@ -81,6 +82,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--workload", default="zipf", choices=sorted(SEEDS))
     ap.add_argument("--bytes", type=int, default=1 << 30)
+    ap.add_argument("--seg", type=int, default=992, help="segment bits of the build (runtime.cpp HUFF_SEG_TARGET)")
+    ap.add_argument("--walks", type=int, default=1, help="segments per thread of k_spec_lds")
     args = ap.parse_args()
     torch.cuda.set_device(0)
     L = C.CDLL(_lib.LIB_PATH)
@@ -110,10 +113,10 @@ def main():
     # the last index-free call left regions 0 and 1; the indexed decode region 2
     job.decode(tree, out.data_ptr(), dec.data_ptr())
     torch.cuda.synchronize()
-    # segments of the speculative pass: runtime.cpp indexless_sync (992 bits for these trees)
-    seg = 992
-    nseg = (bits + seg - 1) // seg
-    for name, r, waves in (("k_spec_lds", 0, (nseg + 255) // 256 * 4), ("k_decode_fixed_skip", 1, ntasks),
+    # segments of the speculative pass: runtime.cpp indexless_sync (args.seg bits for these trees)
+    nseg = (bits + args.seg - 1) // args.seg
+    per_wg = 256 * args.walks
+    for name, r, waves in (("k_spec_lds", 0, (nseg + per_wg - 1) // per_wg * 4), ("k_decode_fixed_skip", 1, ntasks),
                            ("k_decode_fixed", 2, ntasks)):
         buf = np.zeros((waves, 10), np.uint64)
         assert L.huff_diag_stamps(r, buf.ctypes.data, buf.size) == 0
