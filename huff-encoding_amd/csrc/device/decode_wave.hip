@@ -27,16 +27,21 @@ constexpr int kThreads = 256;
 constexpr int kWaves = kThreads / 64;
 constexpr uint32_t kLaneSym = kIdx;              // symbols per lane per task
 static_assert(kTaskSym == 64 * kLaneSym, "4,096 symbols per wave task");
-constexpr uint32_t kInCap = 4608;                // input stage bytes per wave (9 bits per symbol)
 // k_decode_fixed's per-wave stage: the task's input, then (after the decode)
-// its 64 output rows of 64 B
+// its 64 output rows of 64 B. Two sizes: 4,608 B (9 bits per symbol), or, for
+// the index-free skip build of streams of <= 5.6 bits per symbol
+// (fixed_decode_small), 3,072 B: 20 KiB per workgroup with the table, so 8
+// workgroups share a CU instead of 5-6, the rows leaving in two halves. A
+// task whose range exceeds its stage decodes from global memory.
+constexpr uint32_t kInCap = 4608;
+constexpr uint32_t kInCapSmall = 3072;
 constexpr uint32_t kRowBytes = 64;  // 16-B pieces XOR-swizzled by (row >> 1) & 3: conflict-free ds_write_b128
-template <bool PAD>
-constexpr uint32_t fx_stage_bytes() { return kInCap; }  // PAD (swizzled) or not: a permutation of the same bytes
-static_assert(64 * kRowBytes <= kInCap, "the output rows fit the stage");
+template <bool SMALL>
+constexpr uint32_t fx_stage_bytes() { return SMALL ? kInCapSmall : kInCap; }
+static_assert(64 * kRowBytes <= kInCap && 32 * kRowBytes <= kInCapSmall, "the output rows (or half) fit the stage");
 __device__ __forceinline__ uint32_t row_piece(uint32_t row, uint32_t q) { return row * kRowBytes + 16 * (q ^ ((row >> 1) & 3)); }
-constexpr uint32_t kInPieces = kInCap / 16;      // 288 16-B pieces
-constexpr uint32_t kLoadRounds = (kInPieces + 63) / 64;  // 5
+template <bool SMALL>
+constexpr uint32_t load_rounds() { return (fx_stage_bytes<SMALL>() / 16 + 63) / 64; }  // 5 or 3
 static_assert(kChunk % kTaskSym == 0, "a task never straddles a chunk");
 // The first task's loads issued before the table copy (HUFF_DEC_EARLY_LOADS=0
 // for the A/B build without), and the minimum waves per SIMD of the PAD
@@ -114,9 +119,9 @@ __device__ __forceinline__ Task task_info(const DecodeArgs& a, uint64_t t, uint3
 // unconditional loads (pieces past the range read zero), so they stay in
 // flight while the current task decodes — a bounds-checked load with a
 // byte-wise fallback made the compiler wait for them right after issue.
-template <uint32_t R>
+template <uint32_t CAP, uint32_t R>
 __device__ __forceinline__ void issue_task_loads(const DecodeArgs& a, const Task& k, uint32_t lane, uint4 (&pre)[R]) {
-    const uint32_t np = k.len <= kInCap ? k.len / 16 : 0u;
+    const uint32_t np = k.len <= CAP ? k.len / 16 : 0u;
     // the stream is only 4-B aligned: the readable range ends at the dword
     // holding its last byte (the buffer range check is per dword, so a 16-B
     // piece straddling the end returns its readable dwords and zeros)
@@ -355,9 +360,11 @@ __device__ __forceinline__ void fx_check(const DecodeArgs& a, const Task& k, uin
     }
 }
 
-// NT threads per workgroup (HUFF_SKIP_THREADS for the skip build)
-template <bool SLOW, bool PAD, bool CHECK, bool SKIP = false, int NT = kThreads>
+template <bool SLOW, bool PAD, bool CHECK, bool SKIP = false, bool SMALL = false>
 __device__ __forceinline__ void decode_fixed_body(const DecodeArgs& a) {
+    constexpr uint32_t CAP = fx_stage_bytes<SMALL>();
+    constexpr uint32_t kLoadRounds = load_rounds<SMALL>();
+    constexpr int NT = kThreads;
     static_assert(!(CHECK && SKIP), "the self-check needs exact lane starts");
     constexpr int NW = NT / 64;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -369,7 +376,7 @@ __device__ __forceinline__ void decode_fixed_body(const DecodeArgs& a) {
     const uint32_t tab_rw = (tab_words + 3) & ~3u;
     // the wave's stage: dword view for the lane decoders, byte view for the
     // 16-B pieces (all 16-B accesses through u32x4_alias)
-    uint32_t* stage = lds + tab_rw + wave * (fx_stage_bytes<PAD>() / 4);
+    uint32_t* stage = lds + tab_rw + wave * (CAP / 4);
     uint8_t* sb = reinterpret_cast<uint8_t*>(stage);
     const uint64_t ntasks = (a.n + kTaskSym - 1) / kTaskSym;
     const uint64_t step = static_cast<uint64_t>(gridDim.x) * NW;
@@ -393,7 +400,7 @@ __device__ __forceinline__ void decode_fixed_body(const DecodeArgs& a) {
         for (int i = 0; i < TP; ++i) tp[i] = buf_ld16(rtab, (t + NT * i) * 16);
         if (have) {
             cur = task_info<SKIP>(a, task, lane);
-            issue_task_loads(a, cur, lane, pre);
+            issue_task_loads<CAP>(a, cur, lane, pre);
         }
 #pragma unroll
         for (int i = 0; i < TP; ++i)
@@ -416,8 +423,8 @@ __device__ __forceinline__ void decode_fixed_body(const DecodeArgs& a) {
     //   stage writes (input) -> sync -> lane reads -> sync -> row writes
     //   (output transpose) -> sync -> row reads -> sync -> next task's writes
     while (true) {
-        if constexpr (!kEarlyLoads) issue_task_loads(a, cur, lane, pre);
-        const uint32_t np = cur.len <= kInCap ? cur.len / 16 : 0u;
+        if constexpr (!kEarlyLoads) issue_task_loads<CAP>(a, cur, lane, pre);
+        const uint32_t np = cur.len <= CAP ? cur.len / 16 : 0u;
 #pragma unroll
         for (uint32_t r = 0; r < kLoadRounds; ++r) {
             const uint32_t p = lane + 64 * r;
@@ -435,7 +442,7 @@ __device__ __forceinline__ void decode_fixed_body(const DecodeArgs& a) {
 
         const uint32_t rel = static_cast<uint32_t>(cur.lane_bit - cur.b0 * 8);
         uint8_t* dst = a.out + cur.sym0 + lane * kLaneSym;
-        if (cur.len > kInCap) {
+        if (cur.len > CAP) {
             uint32_t e = 0;
             if (cur.cnt) e = decode_fixed_global(GlobalWords{a.comp, a.comp_bytes, cur.b0 / 4}, rel, cur.cnt, dst,
                                                  a.lut, a.lut_bits, SKIP ? cur.skip : 0u);
@@ -450,16 +457,35 @@ __device__ __forceinline__ void decode_fixed_body(const DecodeArgs& a) {
             // 1 KiB contiguous (16 B per lane): lane-strided 16-B pieces cost
             // 4x the L2 write requests and stalled the TA (PMC)
             wave_sync();  // the wave's stage reads are done
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-                st_stage16(sb + row_piece(lane, q), make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]));
-            wave_sync();
-            HUFF_STAMP(ws, 5);
-            // nontemporal: the letters are written once and not read back here
-            // (-2 % decode time against default-policy stores, same box)
+            // nontemporal stores: the letters are written once and not read
+            // back here (-2 % decode time against default-policy stores, same box)
             uint4* d4 = reinterpret_cast<uint4*>(a.out + cur.sym0) + lane;
+            if constexpr (!SMALL) {
 #pragma unroll
-            for (int q = 0; q < 4; ++q) st_nt(d4 + 64 * q, ld_stage16(sb + row_piece(16 * q + (lane >> 2), lane & 3)));
+                for (int q = 0; q < 4; ++q)
+                    st_stage16(sb + row_piece(lane, q), make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]));
+                wave_sync();
+                HUFF_STAMP(ws, 5);
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    st_nt(d4 + 64 * q, ld_stage16(sb + row_piece(16 * q + (lane >> 2), lane & 3)));
+            } else {  // rows 0-31, then rows 32-63, through the 2 KiB they need
+#pragma unroll
+                for (uint32_t h = 0; h < 2; ++h) {
+                    if ((lane >> 5) == h) {
+#pragma unroll
+                        for (int q = 0; q < 4; ++q)
+                            st_stage16(sb + row_piece(lane & 31, q),
+                                       make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]));
+                    }
+                    wave_sync();
+#pragma unroll
+                    for (int q = 0; q < 2; ++q)
+                        st_nt(d4 + 64 * (2 * h + q), ld_stage16(sb + row_piece(16 * q + (lane >> 2), lane & 3)));
+                    wave_sync();  // the half's rows are read before the next half overwrites them
+                }
+                HUFF_STAMP(ws, 5);
+            }
             HUFF_STAMP(ws, 6);
         } else if (cur.cnt) {
             uint32_t o[16];
@@ -484,7 +510,7 @@ __device__ __forceinline__ void decode_fixed_body(const DecodeArgs& a) {
         wave_sync();  // the input stage is reused by the next task
         task = nxt_task;
         cur = task_info<SKIP>(a, task, lane);
-        if constexpr (kEarlyLoads) issue_task_loads(a, cur, lane, pre);
+        if constexpr (kEarlyLoads) issue_task_loads<CAP>(a, cur, lane, pre);
     }
 }
 
@@ -508,18 +534,9 @@ template <bool SLOW, bool PAD>
 __global__ __launch_bounds__(kThreads) void k_decode_fixed_chk(DecodeArgs a) { decode_fixed_body<SLOW, PAD, true>(a); }
 // index-free streams with k_mark_lite's entries: each lane first decodes and
 // drops its skip codes
-// The skip build's workgroup (HUFF_SKIP_THREADS / HUFF_SKIP_WAVES: A/B builds)
-#ifndef HUFF_SKIP_THREADS
-#define HUFF_SKIP_THREADS 256
-#endif
-#ifndef HUFF_SKIP_WAVES
-#define HUFF_SKIP_WAVES kPadWaves
-#endif
-constexpr int kSkipThreads = HUFF_SKIP_THREADS;
-static_assert(kSkipThreads % 64 == 0 && kSkipThreads <= 1024, "whole waves");
-template <bool SLOW, bool PAD>
-__global__ __launch_bounds__(kSkipThreads) __attribute__((amdgpu_waves_per_eu(PAD && !SLOW ? HUFF_SKIP_WAVES : 1, 8))) void k_decode_fixed_skip(DecodeArgs a) {
-    decode_fixed_body<SLOW, PAD, false, true, kSkipThreads>(a);
+template <bool SLOW, bool PAD, bool SMALL>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(PAD && !SLOW ? kPadWaves : 1, 8))) void k_decode_fixed_skip(DecodeArgs a) {
+    decode_fixed_body<SLOW, PAD, false, true, SMALL>(a);
 }
 
 }  // namespace
@@ -528,39 +545,46 @@ __global__ __launch_bounds__(kSkipThreads) __attribute__((amdgpu_waves_per_eu(PA
 
 namespace huff::dev {
 
-size_t decode_fixed_lds_bytes(uint32_t stab_bits, bool pad, bool skip) {
+size_t decode_fixed_lds_bytes(uint32_t stab_bits, bool small) {
     const size_t tab_words = ((1u << stab_bits) + 1) / 2;
-    const size_t waves = skip ? kSkipThreads / 64 : kWaves;
     return ((tab_words + 3) & ~size_t(3)) * 4 +
-           waves * (pad ? fx_stage_bytes<true>() : fx_stage_bytes<false>());
+           static_cast<size_t>(kWaves) * (small ? fx_stage_bytes<true>() : fx_stage_bytes<false>());
 }
 
 hipError_t launch_decode_fixed(const DecodeArgs& a, hipStream_t s) {
     if (a.n == 0) return hipSuccess;
-    const bool skip = a.skip_packed != 0;
-    const size_t lds = decode_fixed_lds_bytes(a.stab_bits, a.pad_stage != 0, skip);
-    const int threads = skip ? kSkipThreads : kThreads;
-    const int waves = threads / 64;
+    // the small stage: the skip build with every code in the table (same-box
+    // A/B, 1 GiB: index-free Zipf 1.153 vs 1.183 ms, text 1.055 vs 1.067; the
+    // indexed decoder lost with it: Zipf 0.498 vs 0.478, text 0.416 vs 0.408,
+    // its swizzled 4.5 KiB stage at 6 waves per SIMD beats the unswizzled
+    // 3 KiB one at 8; profiles/r05/decode_stage/)
+    const bool small = a.small_stage && a.skip_packed && a.max_len <= a.stab_bits;
+    const size_t lds = decode_fixed_lds_bytes(a.stab_bits, small);
     const uint64_t ntasks = (a.n + kTaskSym - 1) / kTaskSym;
     const bool slow = a.max_len > a.stab_bits;
     const bool pad = a.pad_stage != 0;
     using K = void (*)(DecodeArgs);
     // [check mode][slow][pad]
     static const K table[2][2][2] = {
-        {{k_decode_fixed<false>, k_decode_fixed<true>}, {k_decode_fixed_slow<false>, k_decode_fixed_slow<true>}},
+        {{k_decode_fixed<false>, k_decode_fixed<true>},
+         {k_decode_fixed_slow<false>, k_decode_fixed_slow<true>}},
         {{k_decode_fixed_chk<false, false>, k_decode_fixed_chk<false, true>},
          {k_decode_fixed_chk<true, false>, k_decode_fixed_chk<true, true>}},
     };
-    static const K skip_table[2][2] = {{k_decode_fixed_skip<false, false>, k_decode_fixed_skip<false, true>},
-                                       {k_decode_fixed_skip<true, false>, k_decode_fixed_skip<true, true>}};
+    static const K skip_table[2][2] = {{k_decode_fixed_skip<false, false, false>, k_decode_fixed_skip<false, true, false>},
+                                       {k_decode_fixed_skip<true, false, false>, k_decode_fixed_skip<true, true, false>}};
+    // the small stage unswizzled: 79 VGPRs keep 6 waves per SIMD (the
+    // swizzled body needs 81: 5)
+    const K small_kern = k_decode_fixed_skip<false, false, true>;
     if (a.check_mode > 1 || (a.check_mode && !a.err)) return hipErrorInvalidValue;
     if (a.skip_packed && (a.check_mode || !a.sub_abs64)) return hipErrorInvalidValue;
-    K kern = a.skip_packed ? skip_table[slow][pad] : table[a.check_mode][slow][pad];
+    K kern = small ? small_kern
+                   : (a.skip_packed ? skip_table[slow][pad] : table[a.check_mode][slow][pad]);
     // persistent grid = resident workgroups (registers and LDS both limit)
     int per_cu = 0;
-    hipError_t err = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, threads, lds);
+    hipError_t err = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kThreads, lds);
     if (err != hipSuccess || per_cu < 1) per_cu = 1;
-    const uint64_t want = (ntasks + waves - 1) / waves;
+    const uint64_t want = (ntasks + kWaves - 1) / kWaves;
     uint64_t cap = uint64_t(a.cu_count ? a.cu_count : 256) * per_cu;
     // production: one task per wave (a one-shot grid, as the byte map's): the
     // dispatcher refills the CUs as waves finish — same-box A/B against the
@@ -575,7 +599,7 @@ hipError_t launch_decode_fixed(const DecodeArgs& a, hipStream_t s) {
 #endif
     if (!a.check_mode && oneshot) cap = want;
     const uint32_t grid = static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>(want, cap)));
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(threads), lds, s, a);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), lds, s, a);
     return hipGetLastError();
 }
 

@@ -103,6 +103,9 @@ struct DecodeArgs {
     // where the lanes' streams start ~32 m / k dwords apart every refill
     // would hit the same few LDS banks
     uint32_t pad_stage;
+    // k_decode_fixed: the 3 KiB per-wave stage (8 workgroups per CU instead of
+    // 6) for streams of at most kSmallStageBits bits per symbol (fixed_decode_small)
+    uint32_t small_stage;
     // k_decode_fixed self-check build (0: production kernel; 1: checked).
     // err: u32[8] mismatch count + first (task, lane, want, got)
     uint32_t check_mode;
@@ -113,6 +116,14 @@ struct DecodeArgs {
 // length: the stride bands where a bank model of the 32-lane refill reads
 // (lane starts jittered 0.6 dwords per 64 symbols; tools/stage_banks.py)
 // gives the swizzled stage >= 1 LDS cycle fewer per read than the plain one
+// A 4,096-symbol task in the 3 KiB stage: its bits plus the 32-B lookahead
+// (and, index-free, the skip codes) within 3,072 B: 5.9 bits per symbol at
+// most; a mean of up to 5.6 leaves ~20 standard deviations of a task's sum on
+// the workloads measured (tasks that do not fit decode from global memory)
+constexpr double kSmallStageBits = 5.6;
+inline bool fixed_decode_small(uint64_t bits, uint64_t nsym) {
+    return nsym && static_cast<double>(bits) <= kSmallStageBits * static_cast<double>(nsym);
+}
 inline bool fixed_decode_pad(uint64_t bits, uint64_t nsym) {
     if (nsym == 0) return false;
     const double s = 2.0 * static_cast<double>(bits) / static_cast<double>(nsym);  // dwords per 64 symbols

@@ -61,6 +61,12 @@ bool fixed8_disabled() {
     return e && *e && *e != '0';
 }
 
+// HUFF_SMALL_STAGE=0: the decoders keep the 4.5 KiB stage for every stream (A/B)
+bool small_stage_enabled() {
+    const char* e = std::getenv("HUFF_SMALL_STAGE");  // read per call: tests flip it
+    return !(e && *e == '0');
+}
+
 uint32_t decode_check_mode() {
     const char* e = std::getenv("HUFF_DEC_VARIANT");  // read per call: tests flip it
     if (!e) return 0;
@@ -816,6 +822,7 @@ huff::Status huff_enc::decode(const huff_tree* t, const uint8_t* d_comp, uint64_
     }
     a.cu_count = static_cast<uint32_t>(ctx->cu_count);
     a.pad_stage = huff::dev::fixed_decode_pad(total_bits, n);
+    a.small_stage = huff::small_stage_enabled() && huff::dev::fixed_decode_small(total_bits, n);
     a.stab = reinterpret_cast<const uint16_t*>(static_cast<const uint32_t*>(ctx->d_lut.p) + dt->soff);
     a.stab_bits = dt->sbits;
     a.n = n;
@@ -1309,6 +1316,7 @@ Status decode_indexless_dev(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_
         d.stab_bits = dt->sbits;
         d.cu_count = static_cast<uint32_t>(ctx->cu_count);
         d.pad_stage = dev::fixed_decode_pad(valid_bits, total);
+        d.small_stage = small_stage_enabled() && dev::fixed_decode_small(valid_bits, total);
         d.n = total;
         d.out = bounce ? static_cast<uint8_t*>(ctx->d_align.p) : out_at();
         d.check_mode = check;

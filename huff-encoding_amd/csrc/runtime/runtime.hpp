@@ -67,6 +67,8 @@ void build_multi_table(const HuffTree& t, uint32_t mbits, DecTables& out);
 
 // HUFF_DISABLE_FIXED8=1 forces the general kernels even for all-8-bit codes
 bool fixed8_disabled();
+// HUFF_SMALL_STAGE=0 keeps the decoders' 4.5 KiB stage for every stream
+bool small_stage_enabled();
 // HUFF_DEC_VARIANT=11 -> k_decode_fixed's self-checking build (mode 1; else 0)
 uint32_t decode_check_mode();
 

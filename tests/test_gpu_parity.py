@@ -425,6 +425,45 @@ def test_device_job_long_tail_codes(H, O, ctx, dec, monkeypatch):
     assert torch.equal(dec_t[:n], x[:n])
 
 
+@pytest.mark.parametrize("small", ["1", "0"], ids=["small-stage", "large-stage"])
+def test_decode_stage_overflow(H, O, ctx, small, monkeypatch):
+    """a stream whose mean code length picks the decoders' 3 KiB stage
+    (<= 5.6 bits per symbol) but with a stretch of ~8-bit codes: those tasks
+    exceed the stage and decode from global memory. Indexed decode and the
+    index-free decode (the skip build), against the input and the oracle's
+    stream; and with HUFF_SMALL_STAGE=0 (the 4.5 KiB stage)."""
+    import torch
+    from huff_coding import device as D
+
+    monkeypatch.setenv("HUFF_SMALL_STAGE", small)
+    rng = np.random.default_rng(404)
+    n = (1 << 22) + 4321
+    host = np.minimum(rng.geometric(0.5, n) - 1, 255).astype(np.uint8)  # ~2 bits per symbol
+    host[n // 3: n // 3 + 300_000] = rng.integers(0, 256, 300_000, dtype=np.uint8)  # a dense stretch
+    x = torch.from_numpy(np.concatenate([host, np.zeros(64, np.uint8)])).cuda()
+    job = H.EncodeJob(ctx, x.data_ptr(), n)
+    w = job.hist()
+    tree = H.HuffTree.from_weights(H.ByteWeights.from_array(w))
+    bits = job.bits(tree)
+    assert bits / n <= 5.6  # the small stage is chosen when enabled
+    ot = O.Tree.from_weights(O.weights_from_array(w))
+    code, ln = ot.code_table()
+    assert ln[host[n // 3: n // 3 + 300_000]].mean() > 6  # the stretch's tasks exceed 3 KiB
+    out = torch.zeros((bits + 7) // 8 + 64, dtype=torch.uint8, device="cuda")
+    assert job.pack(tree, out.data_ptr(), out.numel()) == bits
+    want, wbits = O.fast_encode(host, code, ln, threads=8)
+    torch.cuda.synchronize()
+    assert wbits == bits and (out[: (bits + 7) // 8].cpu().numpy() == want).all()
+    dec = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
+    job.decode(tree, out.data_ptr(), dec.data_ptr())
+    torch.cuda.synchronize()
+    assert torch.equal(dec[:n], x[:n])
+    dec.fill_(0)
+    got = D.decompress_dev(ctx, tree, out.data_ptr(), (bits + 7) // 8, (8 - bits % 8) % 8, dec.data_ptr(), n + 64)
+    torch.cuda.synchronize()
+    assert got == n and torch.equal(dec[:n], x[:n])
+
+
 @pytest.mark.parametrize("general", [False, True], ids=["fixed8", "general"])
 def test_device_job_full_size_uniform(H, O, ctx, general, monkeypatch):
     """BASELINE config 2: 1 GiB uniform, bit-exact vs the checker + round trip.
