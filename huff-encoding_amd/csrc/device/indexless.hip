@@ -262,6 +262,20 @@ __device__ __forceinline__ void samp_pick(const uint32_t (&sv)[kSampMax], uint32
     }
 }
 
+// Lead-in: a lane starts its walk kLeadBits before its segment and takes the
+// first boundary at or after the segment start as its entry. Huffman codes
+// resynchronise within a few codes (1 GiB Zipf: half of all walks from an
+// arbitrary bit within 11 bits, 0.4 % beyond 96; tools/sync_stats.py), so the
+// entry is nearly always the true boundary, the predecessor's exit: the
+// in-workgroup fix-up below and k_fix_list's check of every workgroup's first
+// segment then find nothing to walk. Without it every lane walked from its
+// predecessor's exit to its first sample (>= 128 bits) and each wave waited
+// for its slowest lane.
+#ifndef HUFF_LEAD_BITS
+#define HUFF_LEAD_BITS 128
+#endif
+constexpr uint32_t kLeadBits = HUFF_LEAD_BITS;
+
 template <bool SLOW>
 __global__ __launch_bounds__(kThreads) void k_spec_lds(IndexlessArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -269,7 +283,7 @@ __global__ __launch_bounds__(kThreads) void k_spec_lds(IndexlessArgs a) {
     HUFF_STAMP(ws, 0);
     TabLoad tl;
     issue_tables(a, tl);
-    const Staged st = with_l2(stage_block(a, lds + tables_words(a)), a, lds);
+    const Staged st = with_l2(stage_block(a, lds + tables_words(a), kLeadBits), a, lds);
     const uint16_t* stab = store_tables(a, tl, lds);
     const uint16_t* wtab = a.wtab ? stab : nullptr;  // one table serves single and multi-code steps
     __syncthreads();
@@ -282,8 +296,26 @@ __global__ __launch_bounds__(kThreads) void k_spec_lds(IndexlessArgs a) {
     const uint64_t start = i * a.seg_bits;
     const uint64_t end = (i + 1 == a.nseg) ? B : (start + a.seg_bits < B ? start + a.seg_bits : B);
     Cursor c;
-    c.init(st, start);
     uint64_t cur = start, cnt = 0;
+    if (kLeadBits && start) {  // the entry: the lead-in walk's first boundary >= start
+        uint64_t p = start > kLeadBits ? start - kLeadBits : 0;
+        c.init(st, p);
+        for (;;) {
+            uint32_t L[kChunkSteps];
+            c.chunk<SLOW>(L, stab, K, a.lut, Kg);
+            uint64_t ex = ~0ull;
+#pragma unroll
+            for (int k = 0; k < kChunkSteps; ++k) {
+                p += L[k];
+                ex = (ex == ~0ull && p >= start) ? p : ex;
+            }
+            if (ex != ~0ull) {
+                cur = ex < B ? ex : B;  // a code crossing B: no code starts in the segment
+                break;
+            }
+        }
+    }
+    c.init(st, cur);
     // samples: a boundary of this path at or after every kSampBits bits past
     // start (a chunk spans < kSampBits bits: at most one per chunk)
     uint32_t* smp = a.samp + i * a.nsamp;
@@ -291,7 +323,8 @@ __global__ __launch_bounds__(kThreads) void k_spec_lds(IndexlessArgs a) {
     uint64_t next_bit = (a.nsamp && live) ? start + kSampBits : ~0ull;
     uint64_t sp1 = ~0ull;  // the first sample (position, spec-local index)
     uint32_t si1 = 0;
-    uint64_t pc = start, pcn = 0, last_main = start;  // the previous chunk end, the last sample
+    const uint64_t entry = cur;
+    uint64_t pc = entry, pcn = 0, last_main = entry;  // the previous chunk end, the last sample
     auto note_sample = [&]() {
         if (cur >= next_bit) {
             const uint64_t db = cur - pc, dc = cnt - pcn;
@@ -366,12 +399,12 @@ __global__ __launch_bounds__(kThreads) void k_spec_lds(IndexlessArgs a) {
     __shared__ uint64_t ex_l[kThreads];
     ex_l[threadIdx.x] = cur;
     __syncthreads();
-    uint64_t s_out = start;
+    uint64_t s_out = entry;
     uint32_t tm_out = 0;
     int32_t dl_out = 0;
     HUFF_STAMP(ws, 4);
-    const uint64_t ns = threadIdx.x ? ex_l[threadIdx.x - 1] : start;
-    if (ns != start) {
+    const uint64_t ns = threadIdx.x ? ex_l[threadIdx.x - 1] : entry;
+    if (ns != entry) {
         Cursor ca_;
         ca_.init(st, ns);
         uint64_t pa = ns, na = 0;
@@ -502,7 +535,10 @@ __global__ __launch_bounds__(kThreads) void k_mark_lds(IndexlessArgs a, const ui
             const uint32_t u = static_cast<uint32_t>(static_cast<int64_t>(t) - dl);
             uint32_t idx, rel;
             samp_pick(sv, u, idx, rel);
-            pos = walk<SLOW>(st, s_spec + rel, u - idx, stab, K, a.lut, Kg);
+            // no sample at or before u: the speculative path's origin is its
+            // entry (lead-in), not recorded; the true path from its start is
+            pos = rel ? walk<SLOW>(st, s_spec + rel, u - idx, stab, K, a.lut, Kg)
+                      : walk<SLOW>(st, s_true, static_cast<uint32_t>(t), stab, K, a.lut, Kg);
         }
         sub_abs[m >> shift] = pos;
     }
@@ -558,8 +594,10 @@ __global__ __launch_bounds__(kThreads) void k_mark_lite(IndexlessArgs a, const u
             const uint32_t u = static_cast<uint32_t>(static_cast<int64_t>(t) - dl);
             uint32_t idx, rel;
             samp_pick(sv, u, idx, rel);
-            pos = s_spec + rel;
-            skip = u - idx;
+            // no sample at or before u: the speculative path's origin is its
+            // entry (lead-in), not recorded; the true path from its start is
+            pos = rel ? s_spec + rel : s_true;
+            skip = rel ? u - idx : t;
         }
         sub_abs[m / kIdx] = pos | (static_cast<uint64_t>(skip) << 48);
     }
@@ -578,7 +616,7 @@ hipError_t launch_indexless_mark_lite(const IndexlessArgs& a, const uint64_t* of
 
 static size_t lds_staged_bytes(const IndexlessArgs& a, uint32_t segs) {
     return static_cast<size_t>((((((1u << a.stab_bits) + 1) / 2) + 3) & ~3u) + a.l2_words) * 4 +
-           ((segs * a.seg_bits + 7) / 8 + 128 + 15) / 16 * 16;
+           ((segs * a.seg_bits + 7) / 8 + (kLeadBits + 7) / 8 + 128 + 15) / 16 * 16;
 }
 
 static bool use_staged(const IndexlessArgs& a) {

@@ -38,11 +38,13 @@ __device__ __forceinline__ void keep_loads(uint4 (&v)[N]) {
     for (int k = 0; k < N; ++k) asm volatile("" : "+v"(v[k].x), "+v"(v[k].y), "+v"(v[k].z), "+v"(v[k].w));
 }
 
+// lead: bits staged before the block's first segment (its first lane's
+// lead-in walk, indexless.hip k_spec_lds)
 template <uint32_t NSEG = 256, class A>
-__device__ __forceinline__ Staged stage_block(const A& a, uint32_t* w) {
+__device__ __forceinline__ Staged stage_block(const A& a, uint32_t* w, uint32_t lead = 0) {
     constexpr uint32_t kT = 256;  // threads
     const uint64_t seg0 = static_cast<uint64_t>(blockIdx.x) * NSEG;
-    const uint64_t bit_lo = seg0 * a.seg_bits;
+    const uint64_t bit_lo = seg0 * a.seg_bits - (seg0 * a.seg_bits < lead ? seg0 * a.seg_bits : lead);
     const uint64_t seg_end = seg0 + NSEG < a.nseg ? seg0 + NSEG : a.nseg;
     const uint64_t bit_hi = seg_end * a.seg_bits < a.valid_bits ? seg_end * a.seg_bits : a.valid_bits;
     const uint64_t byte_lo = (bit_lo >> 3) & ~15ull;
