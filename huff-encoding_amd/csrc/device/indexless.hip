@@ -6,7 +6,8 @@
 // segment start has the residue of a true codeword boundary).
 //  k_spec : lane i decodes speculatively from bit i*S until the first codeword
 //           boundary >= (i+1)*S: exit x[i] and symbol count c[i].
-//  k_fix  : (kFixRounds launches, each a no-op once the previous round
+//  k_fix  : (staged path: k_fix_list + k_fix_chain, below; else
+//           kFixRounds launches, each a no-op once the previous round
 //           changed nothing) lane i restarts from its predecessor's exit
 //           x[i-1] with a second cursor on its old path; the cursor that is
 //           behind advances; when both sit on the same boundary the paths have
@@ -93,9 +94,11 @@ __global__ __launch_bounds__(kThreads) void k_spec(Seg g, uint64_t* __restrict__
 // round r of the fix-up, in place on x (a lane may read its predecessor's exit
 // from this round or the last: either is a boundary of a valid path, and a
 // changed exit sets flags[r], so the next round looks again)
+// nl / ncnt: a list the successor of a changed exit is appended to (the chain)
 __device__ __forceinline__ void fix_one(const Seg& g, uint64_t* __restrict__ s, uint64_t* __restrict__ x,
                                         uint64_t* __restrict__ c, uint32_t* __restrict__ tm, int32_t* __restrict__ dl,
-                                        unsigned int* __restrict__ flags, int r, uint64_t i, const uint32_t* plut) {
+                                        unsigned int* __restrict__ flags, int r, uint64_t i, const uint32_t* plut,
+                                        uint32_t* nl = nullptr, unsigned int* ncnt = nullptr) {
     const uint64_t ns = x[i - 1];
     const uint64_t old_s = s[i];
     if (ns == old_s) return;
@@ -131,6 +134,7 @@ __device__ __forceinline__ void fix_one(const Seg& g, uint64_t* __restrict__ s, 
             if (a.pos != x[i]) {
                 x[i] = a.pos;
                 atomicOr(flags + r, 1u);
+                if (nl && i + 1 < g.nseg) nl[atomicAdd(ncnt, 1u)] = static_cast<uint32_t>(i + 1);
             }
             return;
         }
@@ -164,7 +168,7 @@ __global__ __launch_bounds__(kThreads) void k_fix(Seg g, uint64_t* __restrict__ 
 __global__ __launch_bounds__(kThreads) void k_fix_list(Seg g, uint64_t* __restrict__ s, uint64_t* __restrict__ x,
                                                        uint64_t* __restrict__ c, uint32_t* __restrict__ tm,
                                                        int32_t* __restrict__ dl, unsigned int* __restrict__ flags,
-                                                       const uint32_t* __restrict__ list) {
+                                                       const uint32_t* __restrict__ list, uint32_t* __restrict__ chain) {
     extern __shared__ uint32_t plut[];
     load_prim(plut, g);
     const uint64_t firsts = (g.nseg - 1) / kThreads;  // segments 256, 512, ...
@@ -172,7 +176,45 @@ __global__ __launch_bounds__(kThreads) void k_fix_list(Seg g, uint64_t* __restri
     for (uint64_t j = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; j < n;
          j += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
         const uint64_t i = j < firsts ? (j + 1) * kThreads : list[j - firsts];
-        fix_one(g, s, x, c, tm, dl, flags, 0, i, plut);
+        fix_one(g, s, x, c, tm, dl, flags, 0, i, plut, chain, flags + kFixRounds + 1);
+    }
+}
+
+// The rest of the fix-up in one workgroup: round after round over only the
+// successors of the exits the previous round changed (two lists in turn),
+// until a round changes none. Segments resynchronise within a few codes, so
+// after round 0 the list is nearly always empty and this is a no-op; the
+// three no-op k_fix launches and the k_settle launch it replaced cost ~20 us.
+// Each segment is listed at most once per round (only its predecessor's fix
+// appends it); a lane reading an exit its predecessor changes in the same
+// round gets the successor listed again for the next round.
+constexpr int kChainThreads = 1024;
+__global__ __launch_bounds__(kChainThreads) void k_fix_chain(Seg g, uint64_t* __restrict__ s,
+                                                             uint64_t* __restrict__ x, uint64_t* __restrict__ c,
+                                                             uint32_t* __restrict__ tm, int32_t* __restrict__ dl,
+                                                             unsigned int* __restrict__ flags,
+                                                             uint32_t* __restrict__ chain) {
+    if (__builtin_nontemporal_load(flags + kFixRounds + 1) == 0) return;  // round 0 changed no exit
+    extern __shared__ uint32_t plut[];
+    load_prim(plut, g);
+    __shared__ uint32_t n_sh;
+    uint32_t cur = 0;
+    for (;;) {
+        unsigned int* cnt = flags + kFixRounds + 1 + cur;
+        unsigned int* ncnt = flags + kFixRounds + 2 - cur;
+        if (threadIdx.x == 0) n_sh = atomicAdd(cnt, 0u);
+        __syncthreads();
+        const uint32_t n = n_sh;
+        if (n == 0) break;
+        const uint32_t* list = chain + static_cast<uint64_t>(cur) * g.nseg;
+        uint32_t* nl = chain + static_cast<uint64_t>(cur ^ 1u) * g.nseg;
+        for (uint32_t j = threadIdx.x; j < n; j += blockDim.x) fix_one(g, s, x, c, tm, dl, flags, 0, list[j], plut, nl, ncnt);
+        __syncthreads();  // every fix of the round done (and n_sh read by every lane)
+        if (threadIdx.x == 0) {
+            atomicExch(cnt, 0u);
+            atomicAdd(flags + kFixRounds + 3, n);  // the chain's fixes in all (diagnostics: HUFF_FIX_STATS)
+        }
+        cur ^= 1u;
     }
 }
 
@@ -271,10 +313,11 @@ __device__ __forceinline__ void samp_pick(const uint32_t (&sv)[kSampMax], uint32
 // segment then find nothing to walk. Without it every lane walked from its
 // predecessor's exit to its first sample (>= 128 bits) and each wave waited
 // for its slowest lane.
-#ifndef HUFF_LEAD_BITS
-#define HUFF_LEAD_BITS 128
-#endif
-constexpr uint32_t kLeadBits = HUFF_LEAD_BITS;
+// The lead (IndexlessArgs::lead_bits) is kLeadBits rounded down to a multiple
+// of the gcd of the code lengths, like the segment starts, so a lane never
+// starts out of phase: with all codes 6 bits long a 128-bit lead-in walked a
+// path that never met the true one and the fix-up chained through every
+// segment.
 
 template <bool SLOW>
 __global__ __launch_bounds__(kThreads) void k_spec_lds(IndexlessArgs a) {
@@ -283,7 +326,7 @@ __global__ __launch_bounds__(kThreads) void k_spec_lds(IndexlessArgs a) {
     HUFF_STAMP(ws, 0);
     TabLoad tl;
     issue_tables(a, tl);
-    const Staged st = with_l2(stage_block(a, lds + tables_words(a), kLeadBits), a, lds);
+    const Staged st = with_l2(stage_block(a, lds + tables_words(a), a.lead_bits), a, lds);
     const uint16_t* stab = store_tables(a, tl, lds);
     const uint16_t* wtab = a.wtab ? stab : nullptr;  // one table serves single and multi-code steps
     __syncthreads();
@@ -297,8 +340,8 @@ __global__ __launch_bounds__(kThreads) void k_spec_lds(IndexlessArgs a) {
     const uint64_t end = (i + 1 == a.nseg) ? B : (start + a.seg_bits < B ? start + a.seg_bits : B);
     Cursor c;
     uint64_t cur = start, cnt = 0;
-    if (kLeadBits && start) {  // the entry: the lead-in walk's first boundary >= start
-        uint64_t p = start > kLeadBits ? start - kLeadBits : 0;
+    if (a.lead_bits && start) {  // the entry: the lead-in walk's first boundary >= start
+        uint64_t p = start > a.lead_bits ? start - a.lead_bits : 0;
         c.init(st, p);
 #ifndef HUFF_LEAD_MULTI
 #define HUFF_LEAD_MULTI 1
@@ -589,7 +632,7 @@ __global__ __launch_bounds__(kThreads) void k_mark_lds(IndexlessArgs a, const ui
 // the off[] round trip are not run.
 __global__ __launch_bounds__(kThreads) void k_mark_lite(IndexlessArgs a, const uint64_t* __restrict__ off,
                                                         const unsigned long long* __restrict__ woff,
-                                                        uint64_t* __restrict__ sub_abs) {
+                                                        uint64_t* __restrict__ sub_abs, uint64_t sub_cap) {
     const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
     uint64_t j0, cnt;
     if (woff) {
@@ -609,7 +652,8 @@ __global__ __launch_bounds__(kThreads) void k_mark_lite(IndexlessArgs a, const u
         cnt = a.c[i];
     }
     uint64_t m = (j0 + kIdx - 1) & ~static_cast<uint64_t>(kIdx - 1);
-    if (m >= j0 + cnt) return;
+    const uint64_t m_end = j0 + cnt < sub_cap * kIdx ? j0 + cnt : sub_cap * kIdx;
+    if (m >= m_end) return;
     const uint64_t s_true = a.s[i];
     const uint64_t s_spec = i * a.seg_bits;
     const uint32_t tm = a.tm[i];
@@ -617,7 +661,7 @@ __global__ __launch_bounds__(kThreads) void k_mark_lite(IndexlessArgs a, const u
     uint32_t sv[kSampMax];
 #pragma unroll
     for (uint32_t k = 0; k < kSampMax; ++k) sv[k] = k < a.nsamp ? a.samp[i * a.nsamp + k] : ~0u;
-    for (; m < j0 + cnt; m += kIdx) {
+    for (; m < m_end; m += kIdx) {
         const uint32_t t = static_cast<uint32_t>(m - j0);
         uint64_t pos;
         uint32_t skip;
@@ -640,11 +684,11 @@ __global__ __launch_bounds__(kThreads) void k_mark_lite(IndexlessArgs a, const u
 }  // namespace
 
 hipError_t launch_indexless_mark_lite(const IndexlessArgs& a, const uint64_t* off, const unsigned long long* woff,
-                                      uint64_t* sub_abs, hipStream_t st) {
+                                      uint64_t* sub_abs, uint64_t sub_cap, hipStream_t st) {
     if (a.nseg == 0) return hipSuccess;
     if (!a.samp || (!off && !woff)) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_mark_lite, dim3((a.nseg + kThreads - 1) / kThreads), dim3(kThreads), 0, st, a, off, woff,
-                       sub_abs);
+                       sub_abs, sub_cap < (~0ull / kIdx) ? sub_cap : (~0ull / kIdx));
     return hipGetLastError();
 }
 
@@ -695,14 +739,15 @@ hipError_t launch_indexless_settle_all(const IndexlessArgs& a, hipStream_t st) {
     const size_t lds = (1u << a.lut_bits) * 4;
     // grid-stride rounds: a few resident workgroups per CU cover the segments
     const uint32_t grid = static_cast<uint32_t>(std::min<uint64_t>((a.nseg + kThreads - 1) / kThreads, 2048));
-    int r0 = 0;
-    if (a.fixlist && use_staged(a)) {  // the staged pass listed what round 0 must look at
+    if (a.fixlist && a.chain && use_staged(a)) {  // the staged pass listed what round 0 must look at
         const uint32_t lgrid = static_cast<uint32_t>(std::min<uint64_t>(((a.nseg / kThreads) + kThreads) / kThreads, 256));
         hipLaunchKernelGGL(k_fix_list, dim3(std::max<uint32_t>(lgrid, 1)), dim3(kThreads), lds, st, g, a.s, a.x, a.c,
-                           a.tm, a.dl, a.flags, a.fixlist);
-        r0 = 1;
+                           a.tm, a.dl, a.flags, a.fixlist, a.chain);
+        hipLaunchKernelGGL(k_fix_chain, dim3(1), dim3(kChainThreads), lds, st, g, a.s, a.x, a.c, a.tm, a.dl, a.flags,
+                           a.chain);
+        return hipGetLastError();
     }
-    for (int r = r0; r < kFixRounds; ++r)
+    for (int r = 0; r < kFixRounds; ++r)
         hipLaunchKernelGGL(k_fix, dim3(grid), dim3(kThreads), lds, st, g, a.s, a.x, a.c, a.tm, a.dl, a.flags, r);
     hipLaunchKernelGGL(k_settle, dim3(1), dim3(64), lds, st, g, a.s, a.x, a.c, a.tm, a.flags);
     return hipGetLastError();

@@ -138,6 +138,7 @@ struct IndexlessArgs {
     uint64_t comp_bytes;
     uint64_t valid_bits;          // B
     uint64_t seg_bits;            // S (multiple of the gcd of code lengths)
+    uint32_t lead_bits;           // the staged pass's lead-in (<= kLeadBits, a multiple of the gcd; 0: none)
     uint64_t nseg;
     const uint32_t* lut;
     uint32_t lut_bits;
@@ -157,11 +158,16 @@ struct IndexlessArgs {
     // (tm = kNoMerge: never within the segment)
     uint32_t* tm;
     int32_t* dl;
-    unsigned int* flags;          // [kFixRounds + 1]: round r found a changed exit; [kFixRounds]: fixlist count
+    // [0, kFixRounds): round r found a changed exit; [kFixRounds]: fixlist
+    // count; [kFixRounds + 1, +2]: the counts of the chain's two lists;
+    // [kFixRounds + 3]: the chain's fixes in all
+    unsigned int* flags;
     // (LDS-staged path) segments whose start may not be their predecessor's
     // exit after the speculative pass, besides every workgroup's first one:
     // the successors of segments the in-workgroup fix-up gave a new exit
     uint32_t* fixlist;
+    // (LDS-staged path) 2 x nseg: the fix-up chain's lists (k_fix_chain)
+    uint32_t* chain;
     const uint16_t* stab;         // single-symbol table (k_decode_fixed's): the LDS-staged kernels
     uint32_t stab_bits;
     // walk table over the same stab_bits-bit windows, for the speculative
@@ -181,6 +187,12 @@ struct IndexlessArgs {
     unsigned long long* wtot;
     uint64_t* stamps;             // timing builds (-DHUFF_STAMPS) only: per-wave phase stamps
 };
+// the staged speculative pass starts each lane up to kLeadBits before its
+// segment (indexless.hip k_spec_lds)
+#ifndef HUFF_LEAD_BITS
+#define HUFF_LEAD_BITS 128
+#endif
+constexpr uint32_t kLeadBits = HUFF_LEAD_BITS;
 constexpr uint32_t kSampBits = 128;
 constexpr uint32_t kSampMax = 8;  // samples kept per segment (nsamp <= kSampMax)
 constexpr uint32_t kNoMerge = 0xFFFFFFFFu;
@@ -392,9 +404,11 @@ hipError_t launch_pack(bool long_codes, const PackArgs& a, hipStream_t s);
 hipError_t launch_decode(const DecodeArgs& a, hipStream_t s);
 hipError_t launch_decode_fixed(const DecodeArgs& a, hipStream_t s);
 hipError_t launch_indexless_spec(const IndexlessArgs& a, hipStream_t s);
-// kFixRounds fix-up rounds (each a no-op once the previous one changed
-// nothing), then the sequential sweep only if the last round still changed an
-// exit: no host round trip
+// LDS-staged path: k_fix_list (round 0 over the segments that can differ)
+// then k_fix_chain (one workgroup following the changed exits, a no-op when
+// round 0 changed none). Else kFixRounds fix-up rounds (each a no-op once the
+// previous one changed nothing), then the sequential sweep only if the last
+// round still changed an exit. No host round trip either way.
 hipError_t launch_indexless_settle_all(const IndexlessArgs& a, hipStream_t s);
 hipError_t launch_indexless_emit(const IndexlessArgs& a, const uint64_t* off, uint8_t* out, hipStream_t s);
 // restart index for the ring decoder: sub_abs[g] = start bit of symbol 256 g
@@ -404,8 +418,10 @@ hipError_t launch_indexless_emit(const IndexlessArgs& a, const uint64_t* off, ui
 // symbol) << 48, without walking: the decoder skips the codes (k_mark_lite)
 // off: per-segment offsets, or null and woff: per-workgroup offsets (the
 // scan of IndexlessArgs::wtot; k_mark_lite scans inside each workgroup)
+// sub_cap: entries of sub_abs that may be written (the marks past it are not;
+// the caller sized sub_abs before the symbol count was known)
 hipError_t launch_indexless_mark_lite(const IndexlessArgs& a, const uint64_t* off, const unsigned long long* woff,
-                                      uint64_t* sub_abs, hipStream_t st);
+                                      uint64_t* sub_abs, uint64_t sub_cap, hipStream_t st);
 constexpr uint64_t kSkipPosMask = (1ull << 48) - 1;
 hipError_t launch_indexless_mark(const IndexlessArgs& a, const uint64_t* off, uint64_t* sub_abs, uint32_t shift,
                                  hipStream_t s);

@@ -1058,7 +1058,8 @@ huff::IndexlessSync& huff_ctx::indexless_ws() {
 namespace huff {
 
 Status indexless_sync(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_bytes, uint64_t valid_bits,
-                      const huff_tree* t, IndexlessSync& st, bool need_off) {
+                      const huff_tree* t, IndexlessSync& st, bool need_off,
+                      const std::function<Status()>& before_wait) {
     const DecTables* dt = st.dt;
     // segment length: a multiple of the gcd of all code lengths
     uint32_t g = 0;
@@ -1090,7 +1091,7 @@ Status indexless_sync(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_bytes,
     HUFF_TRY(st.off.ensure((nseg + 1) * 8));
     HUFF_TRY(st.tm.ensure(nseg * 4));
     HUFF_TRY(st.dl.ensure(nseg * 4));
-    HUFF_TRY(st.flag.ensure(32));  // kFixRounds + 1 words, zeroed by one aligned fill
+    HUFF_TRY(st.flag.ensure(32));  // kFixRounds + 4 words, zeroed by one aligned fill
     const uint64_t nwg = (nseg + 255) / 256;  // workgroups of the staged speculative pass
     HUFF_TRY(st.wtot.ensure(nwg * 8));
     HUFF_TRY(st.woff.ensure((nwg + 1) * 8));
@@ -1100,6 +1101,7 @@ Status indexless_sync(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_bytes,
     a.comp_bytes = comp_bytes;
     a.valid_bits = valid_bits;
     a.seg_bits = S;
+    a.lead_bits = dev::kLeadBits / g * g;  // in phase with the segment starts
     a.nseg = nseg;
     a.lut = static_cast<const uint32_t*>(ctx->d_lut.p);
     a.lut_bits = dt->bits;
@@ -1129,12 +1131,14 @@ Status indexless_sync(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_bytes,
         a.samp = static_cast<uint32_t*>(st.samp.p);
         HUFF_TRY(st.fixlist.ensure(nseg * 4 + 4));
         a.fixlist = static_cast<uint32_t*>(st.fixlist.p);
+        HUFF_TRY(st.chain.ensure(nseg * 8 + 8));
+        a.chain = static_cast<uint32_t*>(st.chain.p);
         a.wtot = static_cast<unsigned long long*>(st.wtot.p);
     } else {  // k_spec leaves the merge record to the fix-up rounds
         HIP_TRY(hipMemsetAsync(st.tm.p, 0, nseg * 4, strm));
         HIP_TRY(hipMemsetAsync(st.dl.p, 0, nseg * 4, strm));
     }
-    static_assert((dev::kFixRounds + 1) * 4 <= 32, "the flags fit the zeroed 32 bytes");
+    static_assert((dev::kFixRounds + 4) * 4 <= 32, "the flags fit the zeroed 32 bytes");
     HIP_TRY(hipMemsetAsync(st.flag.p, 0, 32, strm));
     HIP_TRY(dev::launch_indexless_spec(a, strm));
     // fix-up rounds and the sequential fallback decide on the device whether
@@ -1165,11 +1169,19 @@ Status indexless_sync(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_bytes,
         HIP_TRY(dev::launch_scan(static_cast<const uint64_t*>(st.c.p), static_cast<uint32_t>(nseg), 0,
                                  static_cast<uint64_t*>(st.off.p), static_cast<uint64_t*>(st.tsum.p), strm, done));
     }
+    if (before_wait) HUFF_TRY(before_wait());
     const uint64_t* hw = static_cast<const uint64_t*>(ctx->pin_total.p);
     for (uint64_t spin = 0;; ++spin) {
         const uint64_t v = __atomic_load_n(hw, __ATOMIC_ACQUIRE);
         if ((v >> 48) == done.tag) {
             st.total = v & ((1ull << 48) - 1);
+            if (std::getenv("HUFF_FIX_STATS")) {  // diagnostics: how much the fix-up did (a synchronising copy)
+                unsigned int f[8];
+                HIP_TRY(hipMemcpyAsync(f, st.flag.p, sizeof f, hipMemcpyDeviceToHost, strm));
+                HIP_TRY(hipStreamSynchronize(strm));
+                std::fprintf(stderr, "huff fix-up: segments %llu, listed by the speculative pass %u, chain fixes %u\n",
+                             static_cast<unsigned long long>(nseg), f[dev::kFixRounds], f[dev::kFixRounds + 3]);
+            }
             return Status::ok();
         }
         if ((spin & 1023) == 1023) {
@@ -1273,8 +1285,27 @@ Status decode_indexless_dev(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_
     }
     IndexlessSync& st = ctx->indexless_ws();
     st.dt = dt;
+    const uint32_t check = decode_check_mode();
+    // with a caller's buffer, the marks go out before the host waits for the
+    // count: sub_abs sized for the most symbols the stream or the buffer can
+    // hold (shortest code), k_mark_lite bounded to it (22 us of idle stream
+    // between the scan and k_mark_lite otherwise)
+    bool marked = false;
+    auto mark_early = [&]() -> Status {
+        if (!d_user || check || d_end || !st.block_off || !dev::indexless_staged(st.a)) return Status::ok();
+        uint32_t min_len = 64;
+        for (const LeafCode& lc : t->t.leaves()) min_len = std::min<uint32_t>(min_len, std::max<uint32_t>(lc.len, 1));
+        const uint64_t most = std::min<uint64_t>(user_cap, valid_bits / min_len);
+        const uint64_t runs = (most + 63) >> 6;
+        DevBuf& sub_abs = ctx->idx_sub_abs;
+        HUFF_TRY(sub_abs.ensure(runs * 8 + 8));
+        HIP_TRY(dev::launch_indexless_mark_lite(st.a, nullptr, static_cast<const unsigned long long*>(st.woff.p),
+                                                static_cast<uint64_t*>(sub_abs.p), runs, ctx->stream));
+        marked = true;
+        return Status::ok();
+    };
     // k_emit (codes > 32 bits) and the walked marks of the check build read every segment's offset
-    HUFF_TRY(indexless_sync(ctx, d_comp, comp_bytes, valid_bits, t, st, decode_check_mode() != 0));
+    HUFF_TRY(indexless_sync(ctx, d_comp, comp_bytes, valid_bits, t, st, check != 0, mark_early));
     const uint64_t total = st.total;
     *nsym = total;
     if (total == 0) HUFF_TRY(walk_end(nullptr, 0, nullptr, 0));
@@ -1289,15 +1320,14 @@ Status decode_indexless_dev(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_
         // decoder's lanes walk those codes themselves; the self-check builds,
         // HUFF_DEC_VARIANT=11, needs exact lane starts: k_mark_lds walks)
         DevBuf& sub_abs = ctx->idx_sub_abs;
-        const uint32_t check = decode_check_mode();
         if (check) {
             HUFF_TRY(indexless_mark(ctx, st, sub_abs, 6));
-        } else {
+        } else if (!marked) {
             HUFF_TRY(sub_abs.ensure(((total + 63) >> 6) * 8 + 8));
             HIP_TRY(dev::launch_indexless_mark_lite(
                 st.a, st.block_off ? nullptr : static_cast<const uint64_t*>(st.off.p),
                 st.block_off ? static_cast<const unsigned long long*>(st.woff.p) : nullptr,
-                static_cast<uint64_t*>(sub_abs.p), strm));
+                static_cast<uint64_t*>(sub_abs.p), ~0ull, strm));
         }
         const uint64_t m = ((total - 1) >> 6) << 6;  // the last mark: symbol m
         HUFF_TRY(walk_end(static_cast<const uint64_t*>(sub_abs.p) + (m >> 6), 0, nullptr, total - m, !check));

@@ -251,7 +251,7 @@ Status decode_indexless_dev(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_
 // symbol offsets per segment in `off`, the symbol count in `total`
 struct IndexlessSync {
     const DecTables* dt = nullptr;  // tables of the tree, uploaded to ctx->d_lut
-    DevBuf s, x0, c, off, flag, tsum, samp, tm, dl, fixlist;
+    DevBuf s, x0, c, off, flag, tsum, samp, tm, dl, fixlist, chain;
     DevBuf wtot, woff;  // per-workgroup code counts of the staged pass and their exclusive scan
     dev::IndexlessArgs a{};
     uint64_t total = 0;
@@ -259,8 +259,12 @@ struct IndexlessSync {
 };
 // need_off: every segment's offset in `off` (else, on the staged path, only
 // the per-workgroup offsets in `woff`: k_mark_lite's form)
+// before_wait: launched after the scan, before the host waits for the
+// total (work that does not need the count: k_mark_lite, so the host's wait
+// overlaps it instead of stalling the stream)
 Status indexless_sync(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_bytes, uint64_t valid_bits,
-                      const huff_tree* t, IndexlessSync& st, bool need_off = true);
+                      const huff_tree* t, IndexlessSync& st, bool need_off = true,
+                      const std::function<Status()>& before_wait = nullptr);
 // sub_abs[g] = first bit of symbol g << shift (needs dev::indexless_staged(st.a))
 Status indexless_mark(huff_ctx* ctx, IndexlessSync& st, DevBuf& sub_abs, uint32_t shift = 8);
 Status decode_indexless_host(huff_ctx* ctx, const uint8_t* comp, size_t len, uint64_t valid_bits,

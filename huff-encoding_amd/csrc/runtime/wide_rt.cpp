@@ -386,24 +386,38 @@ Status wdecode_indexless_dev(huff_ctx* ctx, const huff_wtree* t, const uint8_t* 
     const WideDecTables* wdt = nullptr;
     HUFF_TRY(t->dec_tables(&wdt));
     const bool skip = !wdt->stab.empty() && !std::getenv("HUFF_WIDE_MARK_WALK");
-    HUFF_TRY(indexless_sync(ctx, d_comp, comp_bytes, valid_bits, shape, st, !skip));
+    DevBuf& sub_abs = ctx->idx_sub_abs;
+    // every kWideRun-th letter: the task decoder (the tree's two-level table)
+    // takes k_mark_lite's marks (a boundary and the codes to skip from it, as
+    // the byte path's skip build), launched before the host waits for the
+    // count (sized for the most letters the buffer or the stream holds);
+    // HUFF_WIDE_MARK_WALK=1 or the long-code decoder: exact points walked by
+    // k_mark_lds
+    bool marked = false;
+    auto mark_early = [&]() -> Status {
+        if (!skip || !d_out || !st.block_off || !dev::indexless_staged(st.a)) return Status::ok();
+        uint32_t min_len = 64;
+        for (const LeafCode& lc : shape->t.leaves()) min_len = std::min<uint32_t>(min_len, std::max<uint32_t>(lc.len, 1));
+        const uint64_t runs = (std::min<uint64_t>(cap_letters, valid_bits / min_len) + 63) >> 6;
+        HUFF_TRY(sub_abs.ensure(runs * 8 + 8));
+        HIP_TRY(dev::launch_indexless_mark_lite(st.a, nullptr, static_cast<const unsigned long long*>(st.woff.p),
+                                                static_cast<uint64_t*>(sub_abs.p), runs, ctx->stream));
+        marked = true;
+        return Status::ok();
+    };
+    HUFF_TRY(indexless_sync(ctx, d_comp, comp_bytes, valid_bits, shape, st, !skip, mark_early));
     *n_out = st.total;
     if (!d_out) return Status::err(HUFF_E_BUFFER_TOO_SMALL, "output buffer too small");
     if (st.total > cap_letters) return Status::err(HUFF_E_BUFFER_TOO_SMALL, "output buffer too small");
     if (!dev::indexless_staged(st.a))
         return Status::err(HUFF_E_CODE_TOO_LONG, "index-free decode of letters wider than a byte needs codes <= 32 bits");
-    DevBuf& sub_abs = ctx->idx_sub_abs;
-    // every kWideRun-th letter: the task decoder (the tree's two-level table)
-    // takes k_mark_lite's marks (a boundary and the codes to skip from it, as
-    // the byte path's skip build); HUFF_WIDE_MARK_WALK=1 or the long-code
-    // decoder: exact points walked by k_mark_lds
-    if (skip) {
+    if (skip && !marked) {
         HUFF_TRY(sub_abs.ensure(((st.total + 63) >> 6) * 8 + 8));
         HIP_TRY(dev::launch_indexless_mark_lite(
             st.a, st.block_off ? nullptr : static_cast<const uint64_t*>(st.off.p),
             st.block_off ? static_cast<const unsigned long long*>(st.woff.p) : nullptr,
-            static_cast<uint64_t*>(sub_abs.p), ctx->stream));
-    } else {
+            static_cast<uint64_t*>(sub_abs.p), ~0ull, ctx->stream));
+    } else if (!skip) {
         HUFF_TRY(indexless_mark(ctx, st, sub_abs, 6));
     }
     HIP_TRY(hipEventRecord(ctx->lut_free, ctx->stream));

@@ -180,3 +180,39 @@ def test_indexfree_full_size_foreign_stream(H, O, ctx, kind, monkeypatch):
     torch.cuda.synchronize()
     assert got == n
     assert torch.equal(out[:n], x)
+
+
+def test_indexfree_fix_chain(H, O, ctx, monkeypatch, capfd):
+    """slowly resynchronising codes (near-fixed lengths): exits that the
+    speculative pass's in-workgroup fix-up and round 0 (k_fix_list) leave
+    changed are followed by the one-workgroup chain (k_fix_chain); the
+    diagnostics (HUFF_FIX_STATS=1) show it ran, and the letters are exact"""
+    import re
+
+    monkeypatch.setenv("HUFF_FIX_STATS", "1")
+    rng = np.random.default_rng(31)
+    chain = 0
+    for k, n in ((160, 4_000_001), (40, 3_000_001), (250, 4_000_003), (129, 3_000_017)):
+        roundtrip(H, O, ctx, rng.integers(0, k, n, dtype=np.uint8).tobytes())
+        err = capfd.readouterr().err
+        got = [int(m) for m in re.findall(r"chain fixes (\d+)", err)]
+        assert got, err
+        chain += sum(got)
+    assert chain > 0
+
+
+def test_indexfree_lead_in_phase(H, O, ctx, monkeypatch, capfd):
+    """codes whose lengths share a factor (all 3 or 6 bits): the speculative
+    pass's lead-in stays a multiple of it, so every lane starts in phase and
+    the fix-up has nothing to do (a 128-bit lead-in with 6-bit codes once sent
+    the fix-up chain through every segment)"""
+    import re
+
+    monkeypatch.setenv("HUFF_FIX_STATS", "1")
+    rng = np.random.default_rng(37)
+    for k in (8, 64):
+        data = rng.permutation(np.tile(np.arange(1, k + 1, dtype=np.uint8), 3_000_000 // k)).tobytes()
+        roundtrip(H, O, ctx, data)
+        err = capfd.readouterr().err
+        stats = re.findall(r"listed by the speculative pass (\d+), chain fixes (\d+)", err)
+        assert stats and all(a == "0" and b == "0" for a, b in stats), err
