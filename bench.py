@@ -158,7 +158,7 @@ PHASE_KERNELS = {  # bench phase -> device kernels (names as in tools/summarize_
 # the index-free decode pipeline of the general path: its
 # kernels' HBM bytes per launch from profiles/traffic_<kind>_indexfree.json
 # (tools/make_traffic.py over a kbench --phase indexless PMC run)
-INDEXFREE_KERNELS = ["k_spec_lds", "k_fix_list", "k_scan_tiles", "k_scan_tsum", "k_scan_fix", "k_mark_lite",
+INDEXFREE_KERNELS = ["k_spec_lds", "k_fix_list", "k_fix_chain", "k_scan_tiles", "k_scan_fix_small", "k_mark_lite",
                      "k_decode_fixed_skip"]
 
 

@@ -131,11 +131,14 @@ __device__ __forceinline__ void fix_one(const Seg& g, uint64_t* __restrict__ s, 
             if (g.wtot && ca != c[i]) atomicAdd(g.wtot + i / kThreads, static_cast<unsigned long long>(ca - c[i]));
             c[i] = ca;
             tm[i] = kNoMerge;
-            if (a.pos != x[i]) {
-                x[i] = a.pos;
-                atomicOr(flags + r, 1u);
-                if (nl && i + 1 < g.nseg) nl[atomicAdd(ncnt, 1u)] = static_cast<uint32_t>(i + 1);
-            }
+            x[i] = a.pos;
+            // the successor looks again: a new exit is rare, and comparing
+            // with the old one is not possible (the staged pass writes x only
+            // where a fix-up reads it), nor with the successor's start (its
+            // own fix may be rewriting it in this round). A successor whose
+            // start already is this exit returns at once.
+            atomicOr(flags + r, 1u);
+            if (nl && i + 1 < g.nseg) nl[atomicAdd(ncnt, 1u)] = static_cast<uint32_t>(i + 1);
             return;
         }
         if (a.pos < b.pos || !b_alive) {
@@ -274,33 +277,43 @@ Seg make_seg(const IndexlessArgs& a) {
 
 // ---- LDS-staged variants (every code <= 32 bits; segwalk.hpp) -------------
 
-// A sample word (segments of < 1024 bits): bits [0, 10) = offset of a
-// boundary of the speculative path from the segment start, [10, 20) = its
-// spec-local code index, [20, 27) / [27, 32) = how far back (bits / codes)
-// the chunk end before it lies, a second boundary between two samples (0
-// codes: none). k_mark_lite starts a mark from the nearest of both, so the
-// fixed-count decoder's lanes skip ~half as many codes; ~0u: no sample.
-#ifndef HUFF_HALF_SAMPLES
-#define HUFF_HALF_SAMPLES 1
-#endif
-__device__ __forceinline__ uint32_t samp_off(uint32_t v) { return v & 1023u; }
-__device__ __forceinline__ uint32_t samp_idx(uint32_t v) { return (v >> 10) & 1023u; }
-// the nearest boundary at or before spec-local code u among a segment's
-// samples (main and half): (code index, bit offset); (0, 0) = the segment start
-__device__ __forceinline__ void samp_pick(const uint32_t (&sv)[kSampMax], uint32_t u, uint32_t& idx, uint32_t& rel) {
+// Samples: slot k of a segment (k = 0 .. nsamp-1) is the first chunk end of
+// the speculative path at or after start + kSampBits (k + 1), as a u16: bits
+// [0, 8) = how far past that threshold it lies, [8, 16) = the codes since
+// the previous recorded slot (or since the entry); 0xFFFF = none (not
+// reached, or a field would overflow). A segment's slots take kSampStride
+// u16 (whole dwords). Round 4's u32 slots every 128 bits (absolute offset and
+// index, plus a "half" boundary between slots) took 28 B per segment.
+constexpr uint32_t kSampStride = (kSampMax + 1) & ~1u;
+constexpr uint32_t kSampNone = 0xFFFFu;
+struct SampWords {
+    uint32_t d[kSampStride / 2];
+};
+__device__ __forceinline__ SampWords samp_load(const uint16_t* samp, uint64_t i) {
+    SampWords w;
+    const uint32_t* p = reinterpret_cast<const uint32_t*>(samp + i * kSampStride);
+#pragma unroll
+    for (uint32_t k = 0; k < kSampStride / 2; ++k) w.d[k] = p[k];
+    return w;
+}
+__device__ __forceinline__ uint32_t samp_slot(const SampWords& w, uint32_t k) {
+    return (w.d[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
+}
+// the nearest recorded slot at or before spec-local code u: (code index, bit
+// offset from the segment start); (0, 0): none
+__device__ __forceinline__ void samp_pick(const SampWords& w, uint32_t nsamp, uint32_t u, uint32_t& idx,
+                                          uint32_t& rel) {
     idx = 0;
     rel = 0;
+    uint32_t cum = 0;
 #pragma unroll
-    for (uint32_t k = 0; k < kSampMax; ++k) {  // ascending: half_k < main_k < half_k+1
-        const uint32_t v = sv[k];
-        const bool valid = v != ~0u;
-        const uint32_t mi = samp_idx(v), mo = samp_off(v), dc = v >> 27, db = (v >> 20) & 127u;
-        const bool okh = valid && dc != 0 && mi - dc <= u;
-        idx = okh ? mi - dc : idx;
-        rel = okh ? mo - db : rel;
-        const bool ok = valid && mi <= u;
-        idx = ok ? mi : idx;
-        rel = ok ? mo : rel;
+    for (uint32_t k = 0; k < kSampMax; ++k) {
+        const uint32_t v = samp_slot(w, k);
+        const bool valid = k < nsamp && v != kSampNone;
+        cum += valid ? v >> 8 : 0u;
+        const bool ok = valid && cum <= u;
+        idx = ok ? cum : idx;
+        rel = ok ? kSampBits * (k + 1) + (v & 0xFFu) : rel;
     }
 }
 
@@ -386,30 +399,21 @@ __global__ __launch_bounds__(kThreads) void k_spec_lds(IndexlessArgs a) {
         }
     }
     c.init(st, cur);
-    // samples: a boundary of this path at or after every kSampBits bits past
-    // start (a chunk spans < kSampBits bits: at most one per chunk)
-    uint32_t* smp = a.samp + i * a.nsamp;
+    // samples: the first chunk end of this path at or after every kSampBits
+    // bits past start (the slots above)
+    uint16_t* smp = a.samp + i * kSampStride;
     uint32_t next_k = 1;
     uint64_t next_bit = (a.nsamp && live) ? start + kSampBits : ~0ull;
-    uint64_t sp1 = ~0ull;  // the first sample (position, spec-local index)
-    uint32_t si1 = 0;
+    uint64_t last_idx = 0;  // the code index of the last recorded slot (the entry: 0)
     const uint64_t entry = cur;
-    uint64_t pc = entry, pcn = 0, last_main = entry;  // the previous chunk end, the last sample
     auto note_sample = [&]() {
         if (cur >= next_bit) {
-            const uint64_t db = cur - pc, dc = cnt - pcn;
-            const bool half = HUFF_HALF_SAMPLES && pc > last_main && db <= 127 && dc <= 31;
-            smp[next_k - 1] = static_cast<uint32_t>(cur - start) | (static_cast<uint32_t>(cnt) << 10) |
-                              (half ? static_cast<uint32_t>((db << 20) | (dc << 27)) : 0u);
-            if (next_k == 1) {  // kept for the fix-up below
-                sp1 = cur;
-                si1 = static_cast<uint32_t>(cnt);
-            }
-            last_main = cur;
+            const uint64_t off = cur - next_bit, didx = cnt - last_idx;
+            const bool ok = off < 256 && didx < 255;
+            smp[next_k - 1] = static_cast<uint16_t>(ok ? off | (didx << 8) : kSampNone);
+            last_idx = ok ? cnt : last_idx;
             next_bit = ++next_k <= a.nsamp ? next_bit + kSampBits : ~0ull;
         }
-        pc = cur;
-        pcn = cnt;
     };
     if (wtab) {
         // multi-code chunks while the chunk's last boundary stays below `end`
@@ -456,7 +460,7 @@ __global__ __launch_bounds__(kThreads) void k_spec_lds(IndexlessArgs a) {
     }
     HUFF_STAMP(ws, 3);
     if (live)
-        for (; next_k <= a.nsamp; ++next_k) smp[next_k - 1] = ~0u;
+        for (; next_k <= a.nsamp; ++next_k) smp[next_k - 1] = static_cast<uint16_t>(kSampNone);
 
     // fix-up inside the workgroup, on the staged bits: lane i restarts from
     // lane i-1's exit (the first lane's predecessor is in another workgroup:
@@ -485,8 +489,23 @@ __global__ __launch_bounds__(kThreads) void k_spec_lds(IndexlessArgs a) {
         Cursor ca_;
         ca_.init(st, ns);
         uint64_t pa = ns, na = 0;
-        uint64_t pk = sp1;        // current sample: position, spec-local index
-        uint32_t ik = si1, k = 1;
+        uint64_t pk = 0;  // current sample: position, spec-local index (read back from the slots)
+        uint32_t ik = 0, cum = 0, k = 0;
+        // passed the sample without landing on it: the next recorded one
+        auto next_sample = [&]() {
+            while (pa > pk) {
+                const uint32_t v = k < a.nsamp ? smp[k] : kSampNone;
+                ++k;
+                if (v != kSampNone) {
+                    cum += v >> 8;
+                    pk = start + kSampBits * k + (v & 0xFFu);
+                    ik = cum;
+                } else if (k >= a.nsamp) {
+                    pk = ~0ull;
+                }
+            }
+        };
+        next_sample();
         for (;;) {
             uint32_t L[kChunkSteps];
             ca_.chunk<SLOW>(L, stab, K, a.lut, Kg);
@@ -520,12 +539,7 @@ __global__ __launch_bounds__(kThreads) void k_spec_lds(IndexlessArgs a) {
             }
             pa = p;
             na += kChunkSteps;
-            while (pa > pk) {  // passed the sample without landing on it: the next one
-                const uint32_t sv = k < a.nsamp ? smp[k] : ~0u;
-                ++k;
-                pk = sv == ~0u ? ~0ull : start + samp_off(sv);
-                ik = samp_idx(sv);
-            }
+            next_sample();
         }
         s_out = ns;
         // a new exit: the successor started from the old one (a workgroup's
@@ -550,7 +564,9 @@ __global__ __launch_bounds__(kThreads) void k_spec_lds(IndexlessArgs a) {
     }
     if (!live) return;
     a.s[i] = s_out;
-    a.x[i] = cur;
+    // the exit only where a fix-up reads it (fix_one reads its predecessor's):
+    // the workgroup's last segment, and a new exit whose successor was listed
+    if (threadIdx.x == kThreads - 1 || i + 1 == a.nseg || (tm_out == kNoMerge && cur != cur0)) a.x[i] = cur;
     a.c[i] = cnt;
     a.tm[i] = tm_out;
     a.dl[i] = dl_out;
@@ -600,9 +616,7 @@ __global__ __launch_bounds__(kThreads) void k_mark_lds(IndexlessArgs a, const ui
     const int64_t dl = a.dl[i];
     // the lane's samples, loaded at once (a dependent load per sample tried
     // cost a memory latency each)
-    uint32_t sv[kSampMax];
-#pragma unroll
-    for (uint32_t k = 0; k < kSampMax; ++k) sv[k] = k < a.nsamp ? a.samp[i * a.nsamp + k] : ~0u;
+    const SampWords sw = samp_load(a.samp, i);
     for (; m < j0 + cnt; m += step) {
         const uint64_t t = m - j0;
         uint64_t pos;
@@ -611,7 +625,7 @@ __global__ __launch_bounds__(kThreads) void k_mark_lds(IndexlessArgs a, const ui
         } else {
             const uint32_t u = static_cast<uint32_t>(static_cast<int64_t>(t) - dl);
             uint32_t idx, rel;
-            samp_pick(sv, u, idx, rel);
+            samp_pick(sw, a.nsamp, u, idx, rel);
             // no sample at or before u: the speculative path's origin is its
             // entry (lead-in), not recorded; the true path from its start is
             pos = rel ? walk<SLOW>(st, s_spec + rel, u - idx, stab, K, a.lut, Kg)
@@ -658,9 +672,7 @@ __global__ __launch_bounds__(kThreads) void k_mark_lite(IndexlessArgs a, const u
     const uint64_t s_spec = i * a.seg_bits;
     const uint32_t tm = a.tm[i];
     const int64_t dl = a.dl[i];
-    uint32_t sv[kSampMax];
-#pragma unroll
-    for (uint32_t k = 0; k < kSampMax; ++k) sv[k] = k < a.nsamp ? a.samp[i * a.nsamp + k] : ~0u;
+    const SampWords sw = samp_load(a.samp, i);
     for (; m < m_end; m += kIdx) {
         const uint32_t t = static_cast<uint32_t>(m - j0);
         uint64_t pos;
@@ -671,7 +683,7 @@ __global__ __launch_bounds__(kThreads) void k_mark_lite(IndexlessArgs a, const u
         } else {
             const uint32_t u = static_cast<uint32_t>(static_cast<int64_t>(t) - dl);
             uint32_t idx, rel;
-            samp_pick(sv, u, idx, rel);
+            samp_pick(sw, a.nsamp, u, idx, rel);
             // no sample at or before u: the speculative path's origin is its
             // entry (lead-in), not recorded; the true path from its start is
             pos = rel ? s_spec + rel : s_true;

@@ -148,10 +148,11 @@ struct IndexlessArgs {
     const uint32_t* mlut;         // multi-symbol table (codes <= 32 bits: the LDS-staged kernels)
     uint32_t mlut_bits;
     uint32_t max_len;
-    // spec samples (LDS-staged path): segment i's slot k-1 (k = 1..nsamp) =
-    // (spec-local symbol index << 16) | (bit offset from i*S) of the first
-    // boundary of its speculative path at or after k*kSampBits; ~0u: none
-    uint32_t* samp;
+    // spec samples (LDS-staged path): segment i's slots at samp + stride i,
+    // slot k the first chunk end of its speculative path at or after
+    // i*S + kSampBits (k + 1) (indexless.hip: u16 offset past that / codes
+    // since the previous slot; 0xFFFF none)
+    uint16_t* samp;
     uint32_t nsamp;
     // how the settled path relates to the speculative one: past true-local
     // symbol tm[i] they coincide, true-local = spec-local + dl[i]
@@ -193,8 +194,12 @@ struct IndexlessArgs {
 #define HUFF_LEAD_BITS 128
 #endif
 constexpr uint32_t kLeadBits = HUFF_LEAD_BITS;
-constexpr uint32_t kSampBits = 128;
-constexpr uint32_t kSampMax = 8;  // samples kept per segment (nsamp <= kSampMax)
+// the speculative pass's sample spacing (indexless.hip); segments < 1024 bits
+#ifndef HUFF_SAMP_BITS
+#define HUFF_SAMP_BITS 96
+#endif
+constexpr uint32_t kSampBits = HUFF_SAMP_BITS;
+constexpr uint32_t kSampMax = 1023 / kSampBits;  // samples kept per segment (nsamp <= kSampMax)
 constexpr uint32_t kNoMerge = 0xFFFFFFFFu;
 constexpr int kFixRounds = 4;     // device-side fix-up rounds before the sequential fallback
 

@@ -1127,8 +1127,8 @@ Status indexless_sync(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_bytes,
     hipStream_t strm = ctx->stream;
     if (dev::indexless_staged(a)) {  // speculative samples for the marking pass
         a.nsamp = std::min<uint32_t>(dev::kSampMax, static_cast<uint32_t>((S - 1) / dev::kSampBits));
-        HUFF_TRY(st.samp.ensure(nseg * a.nsamp * 4 + 4));
-        a.samp = static_cast<uint32_t*>(st.samp.p);
+        HUFF_TRY(st.samp.ensure(nseg * ((dev::kSampMax + 1) & ~1u) * 2 + 16));  // u16 slots, whole dwords per segment
+        a.samp = static_cast<uint16_t*>(st.samp.p);
         HUFF_TRY(st.fixlist.ensure(nseg * 4 + 4));
         a.fixlist = static_cast<uint32_t*>(st.fixlist.p);
         HUFF_TRY(st.chain.ensure(nseg * 8 + 8));
