@@ -28,13 +28,27 @@ namespace huff::dev {
 namespace {
 
 // waves per workgroup: as many as the LDS holds beside one table copy, at
-// most 16 (12 for <= 2-byte letters: their bodies need ~125 registers, more
-// than the 128 of a 16-wave workgroup leave without spills)
+// most 16 (the 2-byte body fits the 128 registers of a 16-wave workgroup
+// since its output stores take 32-bit buffer offsets; round 4 capped it at
+// 12). HUFF_W2_WAVES: the cap for <= 2-byte letters (A/B builds).
+#ifndef HUFF_W2_WAVES
+#define HUFF_W2_WAVES 16
+#endif
 template <uint32_t W>
-constexpr int max_waves() { return W <= 2 ? 12 : 16; }
+constexpr int max_waves() { return W <= 2 ? HUFF_W2_WAVES : 16; }
 constexpr uint32_t kTaskLetters = 64 * kWideRun;  // 4,096
 constexpr uint32_t kSlowFlag = 0x80;              // entry: the first code is longer than K
-constexpr uint32_t kRowBytes = 64 * 64;           // a wave's transpose buffer: 64 rows of 64 B
+// a wave's transpose buffer: for <= 4-byte letters 32 rows of 64 B, the 64
+// lanes' parts in two halves, stored through 32-bit buffer offsets (a 4 KiB
+// buffer for all 64 rows at once held the 2-byte decoder to 13 waves per CU
+// beside its table and stages: W = 2 0.628 -> 0.602 ms, W = 4 0.484 ->
+// 0.474); wider letters (8 parts per lane and more) keep all 64 rows at once
+// and plain stores: the halves' extra wave syncs cost the 8-byte decoder 11 %
+// (0.366 -> 0.405 ms), the buffer stores 2 %
+template <uint32_t W>
+constexpr uint32_t row_halves() { return W <= 4 ? 2u : 1u; }
+template <uint32_t W>
+constexpr uint32_t row_bytes() { return 64 * 64 / row_halves<W>(); }
 
 struct U128 {
     uint64_t lo, hi;
@@ -213,17 +227,43 @@ __device__ __forceinline__ void lane_full(const Words& src, uint32_t rel, uint8_
         uint32_t o[ND];
         decode_part<W, PL, TWO, R1>(s, src, o, tab, K1, letters, leaf4);
         if (rows) {
-            wave_order();  // the previous part's row reads were issued first
+            if constexpr (W >= 8) {
+                wave_order();  // the previous part's row reads were issued first
 #pragma unroll
-            for (uint32_t q = 0; q < 4; ++q)
-                *reinterpret_cast<uint4*>(rows + row_piece(lane, q)) =
-                    make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
-            wave_order();
+                for (uint32_t q = 0; q < 4; ++q)
+                    *reinterpret_cast<uint4*>(rows + row_piece(lane, q)) =
+                        make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
+                wave_order();
 #pragma unroll
-            for (uint32_t j = 0; j < 4; ++j) {
-                const uint32_t r = 16 * j + (lane >> 2), q = lane & 3;
-                const uint4 v = *reinterpret_cast<const uint4*>(rows + row_piece(r, q));
-                *reinterpret_cast<uint4*>(task_out + r * (kWideRun * W) + p * 64 + 16 * q) = v;
+                for (uint32_t j = 0; j < 4; ++j) {
+                    const uint32_t r = 16 * j + (lane >> 2), q = lane & 3;
+                    const uint4 v = *reinterpret_cast<const uint4*>(rows + row_piece(r, q));
+                    *reinterpret_cast<uint4*>(task_out + r * (kWideRun * W) + p * 64 + 16 * q) = v;
+                }
+                continue;
+            }
+            // through a buffer resource over the task's output: 32-bit
+            // offsets (64-bit addresses per store held ~8 more registers)
+            const auto ro = buf_rsrc(task_out, kTaskLetters * W);
+            constexpr uint32_t H = row_halves<W>(), RH = 64 / H;  // halves, rows per half
+#pragma unroll
+            for (uint32_t h = 0; h < H; ++h) {  // lanes [RH h, RH h + RH)
+                wave_order();  // the previous rows were read first
+                if (H == 1 || lane / RH == h) {
+#pragma unroll
+                    for (uint32_t q = 0; q < 4; ++q)
+                        *reinterpret_cast<uint4*>(rows + row_piece(lane % RH, q)) =
+                            make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
+                }
+                wave_order();
+#pragma unroll
+                for (uint32_t j = 0; j < RH / 16; ++j) {
+                    const uint32_t r = 16 * j + (lane >> 2), q = lane & 3;
+                    const uint4 v = *reinterpret_cast<const uint4*>(rows + row_piece(r, q));
+                    u32x4_t w = {v.x, v.y, v.z, v.w};
+                    __builtin_amdgcn_raw_buffer_store_b128(
+                        w, ro, static_cast<int>((RH * h + r) * (kWideRun * W) + p * 64 + 16 * q), 0, 0);
+                }
             }
             continue;
         }
@@ -260,7 +300,7 @@ __device__ __forceinline__ void lane_tail(const Words& src, uint32_t rel, uint32
 }
 
 template <uint32_t W, bool TWO, bool R1, bool LDS>
-__global__ __launch_bounds__(max_waves<W>() * 64) void k_wdec_task(WideDecArgs a) {
+__global__ __launch_bounds__((LDS ? max_waves<W>() : 4) * 64) void k_wdec_task(WideDecArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const uint32_t K1 = a.stab_bits;
     const uint32_t t = threadIdx.x, lane = t & 63, wave = wave_index();
@@ -278,7 +318,7 @@ __global__ __launch_bounds__(max_waves<W>() * 64) void k_wdec_task(WideDecArgs a
     const EntryT<W>* tab = LDS ? reinterpret_cast<const EntryT<W>*>(lds) : static_cast<const EntryT<W>*>(a.stab);
     const uint8_t* letters = LDS && leaf_letters<W>(a) ? lds + tab_bytes : a.letters;
     const bool leaf4 = W == 4 && a.w4_leaf;
-    uint8_t* wave_lds = lds + tab_bytes + let_bytes + wave * (a.stage_bytes + kRowBytes);
+    uint8_t* wave_lds = lds + tab_bytes + let_bytes + wave * (a.stage_bytes + row_bytes<W>());
     uint32_t* stage = reinterpret_cast<uint32_t*>(wave_lds);
     uint8_t* rows = wave_lds + a.stage_bytes;
     const bool aligned = (reinterpret_cast<uintptr_t>(a.out) & 15) == 0;
@@ -353,7 +393,7 @@ hipError_t launch_as(const WideDecArgs& a, size_t shared, uint32_t waves, hipStr
     const bool r1 = a.max_len > 16;
     const Kern k = !two ? k_wdec_task<W, false, false, LDS>
                         : (r1 ? k_wdec_task<W, true, true, LDS> : k_wdec_task<W, true, false, LDS>);
-    const size_t lds = shared + size_t(waves) * (a.stage_bytes + kRowBytes);
+    const size_t lds = shared + size_t(waves) * (a.stage_bytes + row_bytes<W>());
     if (lds > 64 * 1024) {
         const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
                                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -377,7 +417,7 @@ hipError_t by_place(const WideDecArgs& a, hipStream_t s) {
     constexpr size_t kLds = 160 * 1024;
     const size_t tab = a.stab_bytes;
     const size_t let = leaf_letters<W>(a) ? (static_cast<size_t>(a.nleaves) * W + 15) & ~size_t(15) : 0;
-    const size_t per_wave = a.stage_bytes + kRowBytes;
+    const size_t per_wave = a.stage_bytes + row_bytes<W>();
     if (tab + let <= 96 * 1024 && tab + let + 4 * per_wave <= kLds) {
         size_t waves = (kLds - tab - let) / per_wave;
         waves = waves > size_t(max_waves<W>()) ? size_t(max_waves<W>()) : waves;
