@@ -31,7 +31,7 @@ from . import _lib
 from ._lib import load
 
 __all__ = [
-    "ByteWeights", "HuffTree", "CompressData", "compress", "compress_with_tree", "decompress",
+    "ByteWeights", "HuffTree", "HuffBranch", "HuffLeaf", "CompressData", "compress", "compress_with_tree", "decompress",
     "read_compress_write", "read_decompress_write", "parse_block_size", "Context", "EncodeJob",
     "HuffError", "HuffPanic", "CompressError", "FromBinError", "CompressedDataFromBytesError",
 ]
@@ -309,6 +309,70 @@ class HuffTree:
 
     def root_weight(self) -> int:
         return int(load().huff_tree_root_weight(self.h))
+
+    def root(self) -> "HuffBranch":
+        """tree_inner.rs:322-325"""
+        b = C.c_int32()
+        _check(load().huff_tree_root(self.h, C.byref(b)))
+        return HuffBranch(self, b.value)
+
+
+class HuffLeaf:
+    """leaf.rs:25-79 as read from a tree branch: letter (None for a joint
+    branch), weight, code (a '0'/'1' string, None for a joint root)"""
+
+    def __init__(self, letter: Optional[int], weight: int, code: Optional[str]):
+        self._letter, self._weight, self._code = letter, weight, code
+
+    def letter(self) -> Optional[int]:
+        return self._letter
+
+    def weight(self) -> int:
+        return self._weight
+
+    def code(self) -> Optional[str]:
+        return self._code
+
+
+class HuffBranch:
+    """branch.rs:157-279 over the library's tree: a node id valid while the
+    tree lives (the branch keeps the tree alive)"""
+
+    def __init__(self, tree: "HuffTree", node: int):
+        self._tree, self._node = tree, node
+
+    def _children(self):
+        lft, rgt = C.c_int32(), C.c_int32()
+        _check(load().huff_branch_children(self._tree.h, self._node, C.byref(lft), C.byref(rgt)))
+        return lft.value, rgt.value
+
+    def leaf(self) -> HuffLeaf:
+        L = load()
+        has, letter, weight = C.c_int(), C.c_uint8(), C.c_uint64()
+        _check(L.huff_branch_leaf(self._tree.h, self._node, C.byref(has), C.byref(letter), C.byref(weight)))
+        bits = (C.c_uint8 * 512)()
+        n, has_code = C.c_size_t(), C.c_int()
+        _check(L.huff_branch_code(self._tree.h, self._node, bits, 512, C.byref(n), C.byref(has_code)))
+        code = "".join(str(bits[k]) for k in range(n.value)) if has_code.value else None
+        return HuffLeaf(int(letter.value) if has.value else None, int(weight.value), code)
+
+    def left_child(self) -> Optional["HuffBranch"]:
+        lft, _ = self._children()
+        return HuffBranch(self._tree, lft) if lft >= 0 else None
+
+    def right_child(self) -> Optional["HuffBranch"]:
+        _, rgt = self._children()
+        return HuffBranch(self._tree, rgt) if rgt >= 0 else None
+
+    def has_children(self) -> bool:
+        return self._children()[0] >= 0
+
+    def children_iter(self):
+        """branch.rs:247-250: None, or an iterator over (left, right)"""
+        lft, rgt = self._children()
+        if lft < 0:
+            return None
+        return iter((HuffBranch(self._tree, lft), HuffBranch(self._tree, rgt)))
 
 
 def bitvec_str(bits: str) -> str:

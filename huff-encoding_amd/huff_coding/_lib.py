@@ -76,6 +76,10 @@ SIGNATURES = [
     ("huff_tree_code_bits", i, [vp, C.c_uint8, u8p, sz, szp]),
     ("huff_tree_as_bin", i, [vp, u8p, sz, szp]),
     ("huff_tree_try_from_bin", i, [vp, sz, C.POINTER(vp)]),
+    ("huff_tree_root", i, [vp, C.POINTER(C.c_int32)]),
+    ("huff_branch_children", i, [vp, C.c_int32, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
+    ("huff_branch_leaf", i, [vp, C.c_int32, C.POINTER(i), u8p, u64p]),
+    ("huff_branch_code", i, [vp, C.c_int32, u8p, sz, szp, C.POINTER(i)]),
     ("huff_cd_new", i, [vp, sz, C.c_uint8, vp, C.POINTER(vp)]),
     ("huff_cd_free", None, [vp]),
     ("huff_cd_comp_bytes", i, [vp, C.POINTER(u8p), szp]),

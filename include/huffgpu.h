@@ -133,6 +133,26 @@ int huff_tree_as_bin(const huff_tree* t, uint8_t* out, size_t cap, size_t* nbits
 /* try_from_bin (tree_inner.rs:522-604): `bits` packed Msb0, nbits used. */
 int huff_tree_try_from_bin(const uint8_t* bits, size_t nbits, huff_tree** out);
 
+/* Walking the tree: the reference's HuffTree::root (tree_inner.rs:322-325)
+ * and HuffBranch / HuffLeaf accessors. A branch is a node id (>= 0) valid as
+ * long as the tree; -1 stands for None. HUFF_E_INVALID_ARG for a null tree or
+ * an id the tree does not hold. */
+int huff_tree_root(const huff_tree* t, int32_t* branch);
+/* HuffBranch::left_child / right_child (branch.rs:254-268): both -1 when the
+ * branch has no children (has_children, branch.rs:277-279; children_iter
+ * returns None then, else left then right, branch.rs:247-250). */
+int huff_branch_children(const huff_tree* t, int32_t branch, int32_t* left, int32_t* right);
+/* HuffBranch::leaf (branch.rs:207-209) -> HuffLeaf::letter / weight
+ * (leaf.rs:61-68): *has_letter = 1 and *letter for a letter branch, 0 for a
+ * joint branch (letter None). Weights are 0 in a tree read by try_from_bin
+ * (tree_inner.rs:446-447). Any output pointer may be NULL. */
+int huff_branch_leaf(const huff_tree* t, int32_t branch, int* has_letter, uint8_t* letter, uint64_t* weight);
+/* HuffLeaf::code (leaf.rs:70-73): the branch's path from the root, one bit
+ * per byte (tree_inner.rs:422-440 sets it on every branch below the root; a
+ * single-leaf root gets [0], tree_inner.rs:310-315). *has_code = 0 (None) for
+ * the root of a tree with children. HUFF_E_BUFFER_TOO_SMALL if cap < *nbits. */
+int huff_branch_code(const huff_tree* t, int32_t branch, uint8_t* bits, size_t cap, size_t* nbits, int* has_code);
+
 /* ------------------------------------------------------------------------ */
 /* CompressData + compress/decompress — huff_coding/src/comp.rs              */
 /* ------------------------------------------------------------------------ */
