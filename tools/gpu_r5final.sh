@@ -3,13 +3,14 @@
 # kernel trace of the bench, per-workload kernel profiles (trace + PMC
 # passes, tools/profile.sh) for the traffic summaries and the index-free
 # decode, the wide-letter and batch benches. PROFILES=0 stops after the
-# bench trace.
+# bench trace; PART=profiles runs only what follows it.
 #   tools/gpu_r5final.sh <tag>
 set -uo pipefail
 root=${GRAFT_REPO_ROOT:-$(pwd)}
 tag=${1:-r5f}
 out=$root/gpurun_out/$tag; mkdir -p $out
 cd $root
+if [ "${PART:-all}" != profiles ]; then
 timeout -k 10 500 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 --timeout-method thread > $out/gpu_tests.log 2>&1 || { tail -30 $out/gpu_tests.log; exit 1; }
 tail -2 $out/gpu_tests.log
 timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $out/smoke.log 2>&1 || { tail -20 $out/smoke.log; exit 1; }
@@ -19,6 +20,7 @@ echo "bench done"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/bench_trace -o run --output-format csv -- python3 $root/bench.py --steps 5 --warmup 2 --no-cpu-baseline --file-path none > $out/bench_trace.log 2>&1 || { tail -20 $out/bench_trace.log; exit 1; }
 echo "bench trace done"
+fi
 cd $root
 [ "${PROFILES:-1}" = 0 ] && exit 0
 for wl in uniform zipf text; do
