@@ -296,37 +296,11 @@ int huff_branch_leaf(const huff_tree* t, int32_t branch, int* has_letter, uint8_
 
 int huff_branch_code(const huff_tree* t, int32_t branch, uint8_t* bits, size_t cap, size_t* nbits, int* has_code) {
     if (!valid_branch(t, branch) || !nbits) return fail(HUFF_E_INVALID_ARG, "null argument or no such branch");
-    const auto& nodes = t->t.nodes();
-    const int32_t root = t->t.root();
     std::vector<uint8_t> path;
-    bool found = false;
-    if (branch == root) {  // None above a joint root, [0] for a single-leaf root
-        found = nodes[root].is_leaf;
-        if (found) path.push_back(0);
-    } else {
-        // depth-first from the root, left (0) before right (1), keeping the path
-        std::vector<std::pair<int32_t, uint8_t>> stack;  // (node, next child to visit)
-        stack.push_back({root, 0});
-        while (!stack.empty() && !found) {
-            auto& top = stack.back();
-            const huff::HuffNode& n = nodes[top.first];
-            if (n.is_leaf || top.second > 1) {
-                stack.pop_back();
-                if (!path.empty()) path.pop_back();
-                continue;
-            }
-            const uint8_t side = top.second++;
-            const int32_t child = side ? n.right : n.left;
-            path.push_back(side);
-            if (child == branch) {
-                found = true;
-                break;
-            }
-            stack.push_back({child, 0});
-        }
-        if (!found) return fail(HUFF_E_INVALID_ARG, "the branch is not below the root");
-    }
-    if (has_code) *has_code = found ? 1 : 0;
+    bool has = false;
+    if (!huff::capi::branch_path(t->t.nodes(), t->t.root(), branch, path, has))
+        return fail(HUFF_E_INVALID_ARG, "the branch is not below the root");
+    if (has_code) *has_code = has ? 1 : 0;
     *nbits = path.size();
     if (cap < path.size()) return fail(HUFF_E_BUFFER_TOO_SMALL, "bit buffer too small");
     if (bits && !path.empty()) std::memcpy(bits, path.data(), path.size());

@@ -3,6 +3,7 @@
 #include <cstring>
 #include <memory>
 #include <string>
+#include <vector>
 
 #include "capi_util.hpp"
 #include "huffgpu_wide.h"
@@ -93,6 +94,48 @@ int huff_wtree_try_from_bin(uint32_t width, const uint8_t* bits, size_t nbits, h
         *out = t.release();
         return huff::Status::ok();
     });
+}
+
+// tree navigation (tree_inner.rs:322-325, branch.rs:207-279, leaf.rs:61-73)
+static bool valid_wbranch(const huff_wtree* t, int32_t b) {
+    return t && b >= 0 && static_cast<size_t>(b) < t->t.nodes().size();
+}
+
+int huff_wtree_root(const huff_wtree* t, int32_t* branch) {
+    if (!t || !branch) return fail(HUFF_E_INVALID_ARG, "null argument");
+    *branch = t->t.root();
+    return HUFF_OK;
+}
+
+int huff_wbranch_children(const huff_wtree* t, int32_t branch, int32_t* left, int32_t* right) {
+    if (!valid_wbranch(t, branch)) return fail(HUFF_E_INVALID_ARG, "no such branch in the tree");
+    const huff::WideNode& n = t->t.nodes()[branch];
+    if (left) *left = n.is_leaf ? -1 : n.left;
+    if (right) *right = n.is_leaf ? -1 : n.right;
+    return HUFF_OK;
+}
+
+int huff_wbranch_leaf(const huff_wtree* t, int32_t branch, int* has_letter, void* letter, uint64_t* weight) {
+    if (!valid_wbranch(t, branch)) return fail(HUFF_E_INVALID_ARG, "no such branch in the tree");
+    const huff::WideNode& n = t->t.nodes()[branch];
+    if (has_letter) *has_letter = n.is_leaf ? 1 : 0;
+    if (letter) huff::store_letter(static_cast<uint8_t*>(letter), t->t.width(), n.is_leaf ? n.letter : 0);
+    if (weight) *weight = n.weight;
+    return HUFF_OK;
+}
+
+int huff_wbranch_code(const huff_wtree* t, int32_t branch, uint8_t* bits, size_t cap, size_t* nbits,
+                      int* has_code) {
+    if (!valid_wbranch(t, branch) || !nbits) return fail(HUFF_E_INVALID_ARG, "null argument or no such branch");
+    std::vector<uint8_t> path;
+    bool has = false;
+    if (!huff::capi::branch_path(t->t.nodes(), t->t.root(), branch, path, has))
+        return fail(HUFF_E_INVALID_ARG, "the branch is not below the root");
+    if (has_code) *has_code = has ? 1 : 0;
+    *nbits = path.size();
+    if (cap < path.size()) return fail(HUFF_E_BUFFER_TOO_SMALL, "bit buffer too small");
+    if (bits && !path.empty()) std::memcpy(bits, path.data(), path.size());
+    return HUFF_OK;
 }
 
 int huff_wweights_map(huff_ctx* ctx, uint32_t width, const void* letters, size_t n, void* letters_out,

@@ -127,6 +127,10 @@ SIGNATURES = [
     ("huff_wtree_read_codes", i, [vp, vp, vp, vp, sz, szp]),
     ("huff_wtree_as_bin", i, [vp, vp, sz, szp]),
     ("huff_wtree_try_from_bin", i, [C.c_uint32, vp, sz, C.POINTER(vp)]),
+    ("huff_wtree_root", i, [vp, C.POINTER(C.c_int32)]),
+    ("huff_wbranch_children", i, [vp, C.c_int32, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
+    ("huff_wbranch_leaf", i, [vp, C.c_int32, C.POINTER(i), vp, u64p]),
+    ("huff_wbranch_code", i, [vp, C.c_int32, u8p, sz, szp, C.POINTER(i)]),
     ("huff_wweights_map", i, [vp, C.c_uint32, vp, sz, vp, vp, sz, szp]),
     ("huff_wcd_new", i, [vp, sz, C.c_uint8, vp, C.POINTER(vp)]),
     ("huff_wcd_free", None, [vp]),

@@ -162,6 +162,58 @@ class WideTree:
         _check(load().huff_wtree_as_bin(self.h, buf, len(buf), C.byref(n)))
         return "".join("1" if (buf[k // 8] >> (7 - k % 8)) & 1 else "0" for k in range(n.value))
 
+    def root(self) -> "WideBranch":
+        """tree_inner.rs:322-325"""
+        b = C.c_int32()
+        _check(load().huff_wtree_root(self.h, C.byref(b)))
+        return WideBranch(self, b.value)
+
+
+class WideBranch:
+    """HuffBranch<L> (branch.rs:157-279) of a WideTree; leaf() gives a
+    huff_coding.HuffLeaf whose letter is the integer value of L"""
+
+    def __init__(self, tree: WideTree, node: int):
+        self._tree, self._node = tree, node
+
+    def _children(self):
+        lft, rgt = C.c_int32(), C.c_int32()
+        _check(load().huff_wbranch_children(self._tree.h, self._node, C.byref(lft), C.byref(rgt)))
+        return lft.value, rgt.value
+
+    def leaf(self):
+        from . import HuffLeaf
+
+        L = load()
+        lt = self._tree.ltype
+        has, weight = C.c_int(), C.c_uint64()
+        raw = (C.c_uint8 * lt.width)()
+        _check(L.huff_wbranch_leaf(self._tree.h, self._node, C.byref(has), raw, C.byref(weight)))
+        bits = (C.c_uint8 * 4096)()
+        n, has_code = C.c_size_t(), C.c_int()
+        _check(L.huff_wbranch_code(self._tree.h, self._node, bits, 4096, C.byref(n), C.byref(has_code)))
+        code = "".join(str(bits[k]) for k in range(n.value)) if has_code.value else None
+        letter = lt.to_int(bytes(raw)) if has.value else None
+        return HuffLeaf(letter, int(weight.value), code)
+
+    def left_child(self) -> Optional["WideBranch"]:
+        lft, _ = self._children()
+        return WideBranch(self._tree, lft) if lft >= 0 else None
+
+    def right_child(self) -> Optional["WideBranch"]:
+        _, rgt = self._children()
+        return WideBranch(self._tree, rgt) if rgt >= 0 else None
+
+    def has_children(self) -> bool:
+        return self._children()[0] >= 0
+
+    def children_iter(self):
+        """branch.rs:247-250: None, or an iterator over (left, right)"""
+        lft, rgt = self._children()
+        if lft < 0:
+            return None
+        return iter((WideBranch(self._tree, lft), WideBranch(self._tree, rgt)))
+
 
 class WideCompressData:
     """CompressData<L> (comp.rs:40-300)"""

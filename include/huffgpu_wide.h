@@ -51,6 +51,15 @@ int huff_wtree_as_bin(const huff_wtree* t, uint8_t* out, size_t cap, size_t* nbi
 /* HuffTree::<L>::try_from_bin (tree_inner.rs:522-604); FromBinError
  * messages "Provided BitVec is too small/big for an encoded HuffTree". */
 int huff_wtree_try_from_bin(uint32_t width, const uint8_t* bits, size_t nbits, huff_wtree** out);
+/* Walking the tree, as huffgpu.h's huff_tree_root / huff_branch_* for u8
+ * (HuffTree::root tree_inner.rs:322-325, HuffBranch branch.rs:207-279,
+ * HuffLeaf leaf.rs:61-73): node ids >= 0, -1 = None; the letter as W
+ * little-endian bytes. */
+int huff_wtree_root(const huff_wtree* t, int32_t* branch);
+int huff_wbranch_children(const huff_wtree* t, int32_t branch, int32_t* left, int32_t* right);
+int huff_wbranch_leaf(const huff_wtree* t, int32_t branch, int* has_letter, void* letter, uint64_t* weight);
+int huff_wbranch_code(const huff_wtree* t, int32_t branch, uint8_t* bits, size_t cap, size_t* nbits,
+                      int* has_code);
 
 /* ---------------- weights (GPU) ------------------------------------------ */
 /* build_weights_map (weights.rs:82-123) of n host letters: the distinct

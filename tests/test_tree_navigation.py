@@ -121,3 +121,48 @@ def test_bad_branch_ids(H):
     assert len(code) >= 1
     assert L.huff_branch_code(t.h, leaf._node, None, 0, C.byref(n), C.byref(has)) not in (0, 1)
     assert n.value == len(code)
+
+
+def wwalk(b, lt, path, out):
+    """the wide tree's preorder walk: as_bin with W*8 letter bits (big-endian
+    two's complement, letter.rs as_be_bytes)"""
+    leaf = b.leaf()
+    out.append((path, leaf.letter(), leaf.weight(), leaf.code(), b.has_children()))
+    it = b.children_iter()
+    if it is None:
+        raw = int(leaf.letter()).to_bytes(lt.width, "big", signed=lt.signed)
+        return "0" + "".join(format(x, "08b") for x in raw)
+    lft, rgt = list(it)
+    return "1" + wwalk(lft, lt, path + "0", out) + wwalk(rgt, lt, path + "1", out)
+
+
+@pytest.mark.parametrize("dtype,lbits", [(np.int16, 16), (np.uint32, 32), (np.int64, 64)])
+def test_wide_walk_matches_oracle(O, dtype, lbits):
+    """HuffTree<L>::root and its branches for wider letters (letter.rs:41-60)
+    against the oracle's as_bin; leaf weights are the letters' weights, joint
+    weights the sums, codes the paths; a tree read back from bits: weights 0"""
+    import huff_coding.wide as W
+
+    rng = np.random.default_rng(100 + lbits)
+    info = np.iinfo(dtype)
+    for _ in range(15):
+        k = int(rng.integers(1, 300))
+        letters = np.unique(rng.integers(info.min, info.max, k, dtype=dtype, endpoint=True))
+        rng.shuffle(letters)
+        weights = rng.integers(1, 6, letters.size)
+        wmap = dict(zip(letters.tolist(), weights.tolist()))
+        t = W.WideTree.from_weights(list(wmap.items()), dtype)
+        ot = O.Tree.from_leaves(letters.astype(np.int64).view(np.uint64) & np.uint64((1 << lbits) - 1)
+                                if lbits < 64 else letters.view(np.uint64), weights)
+        recs = []
+        assert wwalk(t.root(), t.ltype, "", recs) == ot.as_bin(lbits)
+        assert recs[0][3] == (None if recs[0][4] else "0")
+        by_path = {p: wt for p, _, wt, _, _ in recs}
+        for p, letter, wt, code, kids in recs[1:]:
+            assert code == p
+            assert wt == (by_path[p + "0"] + by_path[p + "1"] if kids else wmap[letter])
+        assert recs[0][2] == int(weights.sum())
+        t2 = W.WideTree.try_from_bin(t.as_bin(), dtype)
+        recs2 = []
+        assert wwalk(t2.root(), t2.ltype, "", recs2) == ot.as_bin(lbits)
+        assert all(r[2] == 0 for r in recs2)
