@@ -75,6 +75,17 @@ def index_free_cases(O, rng):
     # equal counts of 8 / 64 letters: all codes 3 / 6 bits (gcd 3: S = 1023 - ...)
     for k in (8, 64):
         yield f"fixed-{k}", rng.permutation(np.tile(np.arange(1, k + 1, dtype=np.uint8), 600_000 // k)).tobytes()
+    # one letter of 1-bit code beside a Fibonacci tail of codes up to ~30 bits:
+    # multi-code chunks span up to 8 x 30 bits, so more than 255 one-bit codes
+    # can lie between two sample slots — the slot overflows (0xFFFF) and the
+    # marks fall back to the previous slot or the segment's true start
+    fib = [1, 1]
+    while len(fib) < 30:
+        fib.append(fib[-1] + fib[-2])
+    tail = np.repeat(np.arange(1, 31, dtype=np.uint8), np.array(fib))
+    skew = np.full(20_000_000, 255, np.uint8)  # byte 255: ~89 %, a 1-bit code (255: no byte-0 duplicate leaf)
+    skew[rng.choice(skew.size, tail.size, replace=False)] = rng.permutation(tail)
+    yield "one-bit-long-tail", skew.tobytes()
     # codes up to 23 bits (Fibonacci-like counts)
     fib = [1, 1]
     while len(fib) < 24:
