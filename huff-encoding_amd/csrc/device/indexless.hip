@@ -4,31 +4,35 @@
 // Self-synchronising parallel decode. The valid bits [0, B) are cut into
 // segments of S bits (S a multiple of g = gcd of all code lengths, so every
 // segment start has the residue of a true codeword boundary).
-//  k_spec : lane i decodes speculatively from bit i*S until the first codeword
-//           boundary >= (i+1)*S: exit x[i] and symbol count c[i].
-//  k_fix  : (staged path: k_fix_list + k_fix_chain, below; else
-//           kFixRounds launches, each a no-op once the previous round
-//           changed nothing) lane i restarts from its predecessor's exit
-//           x[i-1] with a second cursor on its old path; the cursor that is
-//           behind advances; when both sit on the same boundary the paths have
-//           merged (exit unchanged, count corrected, and the merge point and
-//           index shift against the speculative path recorded), otherwise the
-//           new exit is published and the successor re-checks next round.
-//           Huffman codes resynchronise within a few codewords in practice, so
-//           one or two rounds settle; k_settle (a sequential sweep) runs only
-//           when the last round still changed an exit — decided on the
-//           device, so the host does not wait between rounds.
-//  scan   : exclusive scan of c[] -> output offsets (k_scan, hist.hip).
-//  k_mark : (codes <= 32 bits) the start bit of every symbol whose index is a
-//           multiple of 2^shift: the restart index the fixed-count decoder
-//           then decodes from. k_spec leaves samples on its path (the first
-//           boundary past every kSampBits bits, with its symbol count), so a
-//           mark is found by decoding forward from the nearest sample — about
-//           a quarter of the symbols, where walking the whole segment again
-//           cost more than the speculative pass itself (1.27 vs 0.91 ms per
-//           GiB of Zipf bytes).
+//  k_spec : lane i decodes speculatively from its segment to the first
+//           codeword boundary >= (i+1)*S: exit x[i] and symbol count c[i].
+//           The staged form (k_spec_lds, codes <= 32 bits, the default) first
+//           walks a lead-in of up to kLeadBits before its segment and starts
+//           at the first boundary at or past i*S (nearly always the true
+//           one), keeps a sample slot every kSampBits bits, fixes its
+//           workgroup's segments in place and writes per-workgroup counts.
+//  fix-up : a segment whose start differs from its predecessor's exit is
+//           walked again from that exit with a second cursor on its old path;
+//           the cursor that is behind advances; when both sit on the same
+//           boundary the paths have merged (exit unchanged, count corrected,
+//           merge point and index shift against the speculative path
+//           recorded), otherwise the new exit is published and the successor
+//           looks again. Staged path: k_fix_list (every workgroup's first
+//           segment and the segments the speculative pass listed) then
+//           k_fix_chain (one workgroup following the changed exits, a no-op
+//           when there are none). Otherwise kFixRounds k_fix launches (each a
+//           no-op once the previous round changed nothing) and k_settle (a
+//           sequential sweep, only if the last round still changed an exit).
+//           Decided on the device: the host does not wait between rounds.
+//  scan   : exclusive scan of the counts (per workgroup on the staged path,
+//           k_scan in hist.hip) -> output offsets, the total to the host.
+//  k_mark_lite : (codes <= 32 bits) for every 64th symbol the nearest sample
+//           slot at or before it and the codes to skip from there; the
+//           fixed-count decoder's skip build decodes and drops those codes.
+//           (k_mark_lds walks to the exact boundaries instead: the
+//           self-checking build.)
 //  k_emit : (longer codes) lane i decodes c[i] symbols from its settled start.
-// k_spec and k_mark stage each workgroup's 256 segments in LDS (k_*_lds).
+// The staged kernels read each workgroup's 256 segments from LDS (segwalk.hpp).
 // A codeword that would cross B is dropped, as the reference's walk drops an
 // incomplete final code (comp.rs:493-516).
 #include <algorithm>
