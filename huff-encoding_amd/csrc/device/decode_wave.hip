@@ -80,14 +80,28 @@ __device__ __forceinline__ Task task_info(const DecodeArgs& a, uint64_t t, uint3
     // after the lane's entry it cost a second memory latency per task)
     const uint64_t next = k.sym0 + kTaskSym;
     uint64_t end;
-    if (a.sub_abs64) {
+    if (SKIP && a.mark32) {  // compact marks (k_mark_lite): segment + offset + skip
+        if (next < a.n) {
+            const uint32_t m = a.mark32[next / kIdx];
+            const uint64_t seg = a.task_seg[t + 1];  // the next task's first mark's own segment
+            end = seg * a.seg_bits + mark32_rel(m) + static_cast<uint64_t>(mark32_skip(m)) * a.max_len;
+        } else {
+            end = a.end_bit;
+        }
+        const uint32_t seg0 = a.task_seg[t];
+        const uint32_t m = k.cnt ? a.mark32[k.sym0 / kIdx + lane] : 0u;
+        k.lane_bit = k.cnt ? static_cast<uint64_t>(mark32_seg(m, seg0)) * a.seg_bits + mark32_rel(m) : 0;
+        k.skip = mark32_skip(m);
+    } else if (a.sub_abs64) {
         end = next < a.n ? a.sub_abs64[next / kIdx] : a.end_bit;
     } else if (next < a.n) {
         end = a.sub16 ? a.task_base[t + 1] : a.chunk_start[next / kChunk] + a.sub_bit[next / kIdx];
     } else {
         end = a.chunk_start[a.nchunks];
     }
-    if (a.sub_abs64) {  // index-free streams: absolute start bit of every 64th symbol (k_mark_lds)
+    if (SKIP && a.mark32) {
+        // (read above)
+    } else if (a.sub_abs64) {  // index-free streams: absolute start bit of every 64th symbol (k_mark_lds)
         k.lane_bit = k.cnt ? a.sub_abs64[k.sym0 / kIdx + lane] : 0;
         if constexpr (SKIP) {
             k.skip = static_cast<uint32_t>(k.lane_bit >> 48);
@@ -104,7 +118,7 @@ __device__ __forceinline__ Task task_info(const DecodeArgs& a, uint64_t t, uint3
     const uint32_t f_hi = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(k.lane_bit >> 32)));
     const uint64_t first = (static_cast<uint64_t>(f_hi) << 32) | f_lo;
     if constexpr (SKIP)  // the next task's first bit lies within its skipped codes (used only now)
-        if (a.sub_abs64 && next < a.n) end = (end & kSkipPosMask) + (end >> 48) * a.max_len;
+        if (!a.mark32 && a.sub_abs64 && next < a.n) end = (end & kSkipPosMask) + (end >> 48) * a.max_len;
     k.end = end;
     k.b0 = (first >> 3) & ~15ull;
     uint64_t b1 = ((end + 7) >> 3) + 32;  // lookahead: window + the dword read ahead
@@ -577,7 +591,8 @@ hipError_t launch_decode_fixed(const DecodeArgs& a, hipStream_t s) {
     // swizzled body needs 81: 5)
     const K small_kern = k_decode_fixed_skip<false, false, true>;
     if (a.check_mode > 1 || (a.check_mode && !a.err)) return hipErrorInvalidValue;
-    if (a.skip_packed && (a.check_mode || !a.sub_abs64)) return hipErrorInvalidValue;
+    if (a.skip_packed && (a.check_mode || (!a.sub_abs64 && !(a.mark32 && a.task_seg && a.seg_bits))))
+        return hipErrorInvalidValue;
     K kern = small ? small_kern
                    : (a.skip_packed ? skip_table[slow][pad] : table[a.check_mode][slow][pad]);
     // persistent grid = resident workgroups (registers and LDS both limit)

@@ -650,7 +650,9 @@ __global__ __launch_bounds__(kThreads) void k_mark_lds(IndexlessArgs a, const ui
 // the off[] round trip are not run.
 __global__ __launch_bounds__(kThreads) void k_mark_lite(IndexlessArgs a, const uint64_t* __restrict__ off,
                                                         const unsigned long long* __restrict__ woff,
-                                                        uint64_t* __restrict__ sub_abs, uint64_t sub_cap) {
+                                                        uint64_t* __restrict__ sub_abs, uint64_t sub_cap,
+                                                        uint32_t* __restrict__ mark32,
+                                                        uint32_t* __restrict__ task_seg) {
     const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
     uint64_t j0, cnt;
     if (woff) {
@@ -693,18 +695,25 @@ __global__ __launch_bounds__(kThreads) void k_mark_lite(IndexlessArgs a, const u
             pos = rel ? s_spec + rel : s_true;
             skip = rel ? u - idx : t;
         }
-        sub_abs[m / kIdx] = pos | (static_cast<uint64_t>(skip) << 48);
+        if (mark32) {  // the compact form: offset from the segment's nominal start (< 2048), skip < 1024
+            mark32[m / kIdx] = skip | (static_cast<uint32_t>(pos - s_spec) << 10) |
+                               (static_cast<uint32_t>(i & 0x7FFu) << 21);
+            if ((m % kTaskSym) == 0) task_seg[m / kTaskSym] = static_cast<uint32_t>(i);
+        } else {
+            sub_abs[m / kIdx] = pos | (static_cast<uint64_t>(skip) << 48);
+        }
     }
 }
 
 }  // namespace
 
 hipError_t launch_indexless_mark_lite(const IndexlessArgs& a, const uint64_t* off, const unsigned long long* woff,
-                                      uint64_t* sub_abs, uint64_t sub_cap, hipStream_t st) {
+                                      uint64_t* sub_abs, uint64_t sub_cap, hipStream_t st, uint32_t* mark32,
+                                      uint32_t* task_seg) {
     if (a.nseg == 0) return hipSuccess;
-    if (!a.samp || (!off && !woff)) return hipErrorInvalidValue;
+    if (!a.samp || (!off && !woff) || (!mark32 != !task_seg)) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_mark_lite, dim3((a.nseg + kThreads - 1) / kThreads), dim3(kThreads), 0, st, a, off, woff,
-                       sub_abs, sub_cap < (~0ull / kIdx) ? sub_cap : (~0ull / kIdx));
+                       sub_abs, sub_cap < (~0ull / kIdx) ? sub_cap : (~0ull / kIdx), mark32, task_seg);
     return hipGetLastError();
 }
 

@@ -98,6 +98,12 @@ struct DecodeArgs {
     // sub_abs64 entries as k_mark_lite writes them: a boundary at or before
     // the symbol in bits [0, 48) and the codes to skip from it in [48, 64)
     uint32_t skip_packed;
+    // (skip_packed) k_mark_lite's compact marks instead of sub_abs64: a u32
+    // per kIdx-th symbol (mark32_* below) and the segment index of every
+    // task's first mark; seg_bits = the segments' S
+    const uint32_t* mark32;
+    const uint32_t* task_seg;
+    uint32_t seg_bits;
     // k_decode_fixed: swizzle the input stage (16-B pieces XOR-permuted per
     // 128-B block, decode_wave.hip PaddedLdsWords): for mean code lengths
     // where the lanes' streams start ~32 m / k dwords apart every refill
@@ -424,9 +430,19 @@ hipError_t launch_indexless_emit(const IndexlessArgs& a, const uint64_t* off, ui
 // off: per-segment offsets, or null and woff: per-workgroup offsets (the
 // scan of IndexlessArgs::wtot; k_mark_lite scans inside each workgroup)
 // sub_cap: entries of sub_abs that may be written (the marks past it are not;
-// the caller sized sub_abs before the symbol count was known)
+// the caller sized sub_abs before the symbol count was known).
+// mark32 / task_seg non-null: the compact form instead of sub_abs (4 B per
+// mark + 4 B per task of kTaskSym symbols, half the u64 marks' traffic):
+// mark = skip | offset from its segment's nominal start << 10 | the
+// segment's index mod 2048 << 21; task_seg[t] = the segment index of task t's
+// first mark, from which a decoder recovers the others (a task spans far
+// fewer than 2048 segments).
+constexpr uint32_t mark32_skip(uint32_t m) { return m & 0x3FFu; }
+constexpr uint32_t mark32_rel(uint32_t m) { return (m >> 10) & 0x7FFu; }
+constexpr uint32_t mark32_seg(uint32_t m, uint32_t base_seg) { return base_seg + (((m >> 21) - base_seg) & 0x7FFu); }
 hipError_t launch_indexless_mark_lite(const IndexlessArgs& a, const uint64_t* off, const unsigned long long* woff,
-                                      uint64_t* sub_abs, uint64_t sub_cap, hipStream_t st);
+                                      uint64_t* sub_abs, uint64_t sub_cap, hipStream_t st,
+                                      uint32_t* mark32 = nullptr, uint32_t* task_seg = nullptr);
 constexpr uint64_t kSkipPosMask = (1ull << 48) - 1;
 hipError_t launch_indexless_mark(const IndexlessArgs& a, const uint64_t* off, uint64_t* sub_abs, uint32_t shift,
                                  hipStream_t s);

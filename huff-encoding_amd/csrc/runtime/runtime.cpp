@@ -1291,16 +1291,21 @@ Status decode_indexless_dev(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_
     // hold (shortest code), k_mark_lite bounded to it (22 us of idle stream
     // between the scan and k_mark_lite otherwise)
     bool marked = false;
+    // the compact marks (u32 per 64 symbols + u32 per task: dev::mark32_*)
+    // unless a consumer wants absolute u64 marks (the window end of the file
+    // path, the check build)
+    const bool compact = !check && !d_end;
     auto mark_early = [&]() -> Status {
         if (!d_user || check || d_end || !st.block_off || !dev::indexless_staged(st.a)) return Status::ok();
         uint32_t min_len = 64;
         for (const LeafCode& lc : t->t.leaves()) min_len = std::min<uint32_t>(min_len, std::max<uint32_t>(lc.len, 1));
         const uint64_t most = std::min<uint64_t>(user_cap, valid_bits / min_len);
         const uint64_t runs = (most + 63) >> 6;
-        DevBuf& sub_abs = ctx->idx_sub_abs;
-        HUFF_TRY(sub_abs.ensure(runs * 8 + 8));
+        HUFF_TRY(ctx->idx_mark32.ensure(runs * 4 + 8));
+        HUFF_TRY(ctx->idx_task_seg.ensure(((most + dev::kTaskSym - 1) / dev::kTaskSym) * 4 + 8));
         HIP_TRY(dev::launch_indexless_mark_lite(st.a, nullptr, static_cast<const unsigned long long*>(st.woff.p),
-                                                static_cast<uint64_t*>(sub_abs.p), runs, ctx->stream));
+                                                nullptr, runs, ctx->stream, static_cast<uint32_t*>(ctx->idx_mark32.p),
+                                                static_cast<uint32_t*>(ctx->idx_task_seg.p)));
         marked = true;
         return Status::ok();
     };
@@ -1322,6 +1327,13 @@ Status decode_indexless_dev(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_
         DevBuf& sub_abs = ctx->idx_sub_abs;
         if (check) {
             HUFF_TRY(indexless_mark(ctx, st, sub_abs, 6));
+        } else if (!marked && compact) {
+            HUFF_TRY(ctx->idx_mark32.ensure(((total + 63) >> 6) * 4 + 8));
+            HUFF_TRY(ctx->idx_task_seg.ensure(((total + dev::kTaskSym - 1) / dev::kTaskSym) * 4 + 8));
+            HIP_TRY(dev::launch_indexless_mark_lite(
+                st.a, st.block_off ? nullptr : static_cast<const uint64_t*>(st.off.p),
+                st.block_off ? static_cast<const unsigned long long*>(st.woff.p) : nullptr, nullptr, ~0ull, strm,
+                static_cast<uint32_t*>(ctx->idx_mark32.p), static_cast<uint32_t*>(ctx->idx_task_seg.p)));
         } else if (!marked) {
             HUFF_TRY(sub_abs.ensure(((total + 63) >> 6) * 8 + 8));
             HIP_TRY(dev::launch_indexless_mark_lite(
@@ -1330,14 +1342,18 @@ Status decode_indexless_dev(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_
                 static_cast<uint64_t*>(sub_abs.p), ~0ull, strm));
         }
         const uint64_t m = ((total - 1) >> 6) << 6;  // the last mark: symbol m
-        HUFF_TRY(walk_end(static_cast<const uint64_t*>(sub_abs.p) + (m >> 6), 0, nullptr, total - m, !check));
+        if (!compact)  // (d_end never goes with the compact marks)
+            HUFF_TRY(walk_end(static_cast<const uint64_t*>(sub_abs.p) + (m >> 6), 0, nullptr, total - m, !check));
         dev::DecodeArgs d{};
         d.comp = d_comp;
         d.comp_bytes = comp_bytes;
         d.lut = static_cast<const uint32_t*>(ctx->d_lut.p);
         d.lut_bits = dt->bits;
         d.lut_words = static_cast<uint32_t>(dt->lut.size());
-        d.sub_abs64 = static_cast<const uint64_t*>(sub_abs.p);
+        d.sub_abs64 = compact ? nullptr : static_cast<const uint64_t*>(sub_abs.p);
+        d.mark32 = compact ? static_cast<const uint32_t*>(ctx->idx_mark32.p) : nullptr;
+        d.task_seg = compact ? static_cast<const uint32_t*>(ctx->idx_task_seg.p) : nullptr;
+        d.seg_bits = static_cast<uint32_t>(st.a.seg_bits);
         d.skip_packed = check ? 0u : 1u;
         d.end_bit = valid_bits;
         d.nchunks = static_cast<uint32_t>((total + dev::kChunk - 1) / dev::kChunk);

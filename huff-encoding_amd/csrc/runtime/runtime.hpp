@@ -150,6 +150,7 @@ struct huff_ctx {
     // of its ~100 MB per GiB of stream cost more than the kernels)
     std::shared_ptr<huff::IndexlessSync> idx_ws;
     DevBuf idx_sub_abs;
+    DevBuf idx_mark32, idx_task_seg;  // the index-free decode's compact marks (k_mark_lite)
     huff::IndexlessSync& indexless_ws();
     // the .hff file path's pinned pieces and device buffers (filepath.cpp),
     // kept across calls: pinning ~0.5 GB per call costs more than the copies
