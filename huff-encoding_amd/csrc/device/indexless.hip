@@ -10,7 +10,9 @@
 //           walks a lead-in of up to kLeadBits before its segment and starts
 //           at the first boundary at or past i*S (nearly always the true
 //           one), keeps a sample slot every kSampBits bits, fixes its
-//           workgroup's segments in place and writes per-workgroup counts.
+//           workgroup's segments in place and writes per-workgroup counts;
+//           its segment records (start, count, merge point) are packed in one
+//           u64 each (SegRec / rec_pack below).
 //  fix-up : a segment whose start differs from its predecessor's exit is
 //           walked again from that exit with a second cursor on its old path;
 //           the cursor that is behind advances; when both sit on the same
@@ -95,16 +97,58 @@ __global__ __launch_bounds__(kThreads) void k_spec(Seg g, uint64_t* __restrict__
     c[i] = cnt;
 }
 
+// a segment's settled record: start, code count, and how its path relates to
+// the speculative one (IndexlessArgs::tm/dl). The unstaged path keeps it in
+// four arrays; the staged path packs it in one u64 (IndexlessArgs::rec): 8
+// bytes written by k_spec_lds and read by k_mark_lite per segment, not 24.
+struct SegRec {
+    uint64_t s, c;
+    uint32_t tm;
+    int32_t dl;
+};
+struct ArrayRecs {
+    uint64_t* s;
+    uint64_t* c;
+    uint32_t* tm;
+    int32_t* dl;
+    __device__ SegRec load(uint64_t i) const { return SegRec{s[i], c[i], tm[i], dl[i]}; }
+    __device__ void store(uint64_t i, const SegRec& v) const {
+        s[i] = v.s;
+        c[i] = v.c;
+        tm[i] = v.tm;
+        dl[i] = v.dl;
+    }
+};
+// bits [0, 16) count, [16, 32) tm (0xFFFF: kNoMerge), [32, 48) dl (int16),
+// [48, 64) start - i*S (staged segments < 1024 bits, codes <= 32 bits: every
+// field fits)
+__device__ __forceinline__ SegRec rec_unpack(uint64_t r, uint64_t i, uint64_t S) {
+    const uint32_t tm = static_cast<uint32_t>(r >> 16) & 0xFFFFu;
+    return SegRec{i * S + (r >> 48), r & 0xFFFFu, tm == 0xFFFFu ? kNoMerge : tm,
+                  static_cast<int32_t>(static_cast<int16_t>(static_cast<uint16_t>(r >> 32)))};
+}
+__device__ __forceinline__ uint64_t rec_pack(const SegRec& v, uint64_t i, uint64_t S) {
+    return (v.c & 0xFFFFu) | (static_cast<uint64_t>(v.tm == kNoMerge ? 0xFFFFu : v.tm & 0xFFFFu) << 16) |
+           (static_cast<uint64_t>(static_cast<uint16_t>(v.dl)) << 32) | ((v.s - i * S) << 48);
+}
+struct PackedRecs {
+    uint64_t* rec;
+    uint64_t S;
+    __device__ SegRec load(uint64_t i) const { return rec_unpack(rec[i], i, S); }
+    __device__ void store(uint64_t i, const SegRec& v) const { rec[i] = rec_pack(v, i, S); }
+};
+
 // round r of the fix-up, in place on x (a lane may read its predecessor's exit
 // from this round or the last: either is a boundary of a valid path, and a
 // changed exit sets flags[r], so the next round looks again)
 // nl / ncnt: a list the successor of a changed exit is appended to (the chain)
-__device__ __forceinline__ void fix_one(const Seg& g, uint64_t* __restrict__ s, uint64_t* __restrict__ x,
-                                        uint64_t* __restrict__ c, uint32_t* __restrict__ tm, int32_t* __restrict__ dl,
+template <class Recs>
+__device__ __forceinline__ void fix_one(const Seg& g, const Recs& R, uint64_t* __restrict__ x,
                                         unsigned int* __restrict__ flags, int r, uint64_t i, const uint32_t* plut,
                                         uint32_t* nl = nullptr, unsigned int* ncnt = nullptr) {
     const uint64_t ns = x[i - 1];
-    const uint64_t old_s = s[i];
+    SegRec v = R.load(i);
+    const uint64_t old_s = v.s;
     if (ns == old_s) return;
     const BitSrc src{reinterpret_cast<const uint32_t*>(g.comp), g.comp, g.comp_bytes};
     const Lut lut{plut, g.lut, g.K};
@@ -116,25 +160,26 @@ __device__ __forceinline__ void fix_one(const Seg& g, uint64_t* __restrict__ s, 
     bool a_alive = true, b_alive = true;
     for (;;) {
         if (a.pos == b.pos) {  // merged: same exit, count corrected
-            s[i] = ns;
-            c[i] = c[i] - cb + ca;
+            v.s = ns;
+            v.c = v.c - cb + ca;
             if (g.wtot && ca != cb) atomicAdd(g.wtot + i / kThreads, static_cast<unsigned long long>(ca - cb));
             // the old path met the speculative one at old-local tm1 with shift
             // dl1; the new path meets the old one at (ca, cb)
-            const uint32_t tm1 = tm[i];
-            if (tm1 != kNoMerge) {
+            if (v.tm != kNoMerge) {
                 const int64_t sh = static_cast<int64_t>(ca) - static_cast<int64_t>(cb);
-                const int64_t t2 = static_cast<int64_t>(tm1) + sh;
-                tm[i] = static_cast<uint32_t>(t2 > static_cast<int64_t>(ca) ? t2 : static_cast<int64_t>(ca));
-                dl[i] = dl[i] + static_cast<int32_t>(sh);
+                const int64_t t2 = static_cast<int64_t>(v.tm) + sh;
+                v.tm = static_cast<uint32_t>(t2 > static_cast<int64_t>(ca) ? t2 : static_cast<int64_t>(ca));
+                v.dl += static_cast<int32_t>(sh);
             }
+            R.store(i, v);
             return;
         }
         if (a.pos >= end || !a_alive) {  // new exit
-            s[i] = ns;
-            if (g.wtot && ca != c[i]) atomicAdd(g.wtot + i / kThreads, static_cast<unsigned long long>(ca - c[i]));
-            c[i] = ca;
-            tm[i] = kNoMerge;
+            v.s = ns;
+            if (g.wtot && ca != v.c) atomicAdd(g.wtot + i / kThreads, static_cast<unsigned long long>(ca - v.c));
+            v.c = ca;
+            v.tm = kNoMerge;
+            R.store(i, v);
             x[i] = a.pos;
             // the successor looks again: a new exit is rare, and comparing
             // with the old one is not possible (the staged pass writes x only
@@ -165,16 +210,15 @@ __global__ __launch_bounds__(kThreads) void k_fix(Seg g, uint64_t* __restrict__ 
     load_prim(plut, g);
     for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < g.nseg;
          i += static_cast<uint64_t>(gridDim.x) * blockDim.x)
-        if (i) fix_one(g, s, x, c, tm, dl, flags, r, i, plut);
+        if (i) fix_one(g, ArrayRecs{s, c, tm, dl}, x, flags, r, i, plut);
 }
 
 // round 0 after the staged speculative pass: only the segments that can
 // differ from their predecessor's exit — every workgroup's first segment and
 // the listed successors of in-workgroup new exits (each index once, so no two
 // lanes update one segment's merge record)
-__global__ __launch_bounds__(kThreads) void k_fix_list(Seg g, uint64_t* __restrict__ s, uint64_t* __restrict__ x,
-                                                       uint64_t* __restrict__ c, uint32_t* __restrict__ tm,
-                                                       int32_t* __restrict__ dl, unsigned int* __restrict__ flags,
+__global__ __launch_bounds__(kThreads) void k_fix_list(Seg g, PackedRecs R, uint64_t* __restrict__ x,
+                                                       unsigned int* __restrict__ flags,
                                                        const uint32_t* __restrict__ list, uint32_t* __restrict__ chain) {
     extern __shared__ uint32_t plut[];
     load_prim(plut, g);
@@ -183,7 +227,7 @@ __global__ __launch_bounds__(kThreads) void k_fix_list(Seg g, uint64_t* __restri
     for (uint64_t j = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; j < n;
          j += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
         const uint64_t i = j < firsts ? (j + 1) * kThreads : list[j - firsts];
-        fix_one(g, s, x, c, tm, dl, flags, 0, i, plut, chain, flags + kFixRounds + 1);
+        fix_one(g, R, x, flags, 0, i, plut, chain, flags + kFixRounds + 1);
     }
 }
 
@@ -196,9 +240,7 @@ __global__ __launch_bounds__(kThreads) void k_fix_list(Seg g, uint64_t* __restri
 // appends it); a lane reading an exit its predecessor changes in the same
 // round gets the successor listed again for the next round.
 constexpr int kChainThreads = 1024;
-__global__ __launch_bounds__(kChainThreads) void k_fix_chain(Seg g, uint64_t* __restrict__ s,
-                                                             uint64_t* __restrict__ x, uint64_t* __restrict__ c,
-                                                             uint32_t* __restrict__ tm, int32_t* __restrict__ dl,
+__global__ __launch_bounds__(kChainThreads) void k_fix_chain(Seg g, PackedRecs R, uint64_t* __restrict__ x,
                                                              unsigned int* __restrict__ flags,
                                                              uint32_t* __restrict__ chain) {
     if (__builtin_nontemporal_load(flags + kFixRounds + 1) == 0) return;  // round 0 changed no exit
@@ -215,7 +257,7 @@ __global__ __launch_bounds__(kChainThreads) void k_fix_chain(Seg g, uint64_t* __
         if (n == 0) break;
         const uint32_t* list = chain + static_cast<uint64_t>(cur) * g.nseg;
         uint32_t* nl = chain + static_cast<uint64_t>(cur ^ 1u) * g.nseg;
-        for (uint32_t j = threadIdx.x; j < n; j += blockDim.x) fix_one(g, s, x, c, tm, dl, flags, 0, list[j], plut, nl, ncnt);
+        for (uint32_t j = threadIdx.x; j < n; j += blockDim.x) fix_one(g, R, x, flags, 0, list[j], plut, nl, ncnt);
         __syncthreads();  // every fix of the round done (and n_sh read by every lane)
         if (threadIdx.x == 0) {
             atomicExch(cnt, 0u);
@@ -567,13 +609,10 @@ __global__ __launch_bounds__(kThreads) void k_spec_lds(IndexlessArgs a) {
         }
     }
     if (!live) return;
-    a.s[i] = s_out;
+    a.rec[i] = rec_pack(SegRec{s_out, cnt, tm_out, dl_out}, i, a.seg_bits);
     // the exit only where a fix-up reads it (fix_one reads its predecessor's):
     // the workgroup's last segment, and a new exit whose successor was listed
     if (threadIdx.x == kThreads - 1 || i + 1 == a.nseg || (tm_out == kNoMerge && cur != cur0)) a.x[i] = cur;
-    a.c[i] = cnt;
-    a.tm[i] = tm_out;
-    a.dl[i] = dl_out;
 }
 
 // the position `n` codes past the boundary `pos` of the staged range
@@ -610,14 +649,15 @@ __global__ __launch_bounds__(kThreads) void k_mark_lds(IndexlessArgs a, const ui
     if (i >= a.nseg) return;
     const uint32_t K = a.stab_bits, Kg = a.lut_bits;
     const uint64_t j0 = off[i];
-    const uint64_t cnt = a.c[i];
+    const SegRec v = rec_unpack(a.rec[i], i, a.seg_bits);
+    const uint64_t cnt = v.c;
     const uint64_t step = 1ull << shift;
     uint64_t m = (j0 + step - 1) & ~(step - 1);
     if (m >= j0 + cnt) return;
-    const uint64_t s_true = a.s[i];
+    const uint64_t s_true = v.s;
     const uint64_t s_spec = i * a.seg_bits;
-    const uint32_t tm = a.tm[i];
-    const int64_t dl = a.dl[i];
+    const uint32_t tm = v.tm;
+    const int64_t dl = v.dl;
     // the lane's samples, loaded at once (a dependent load per sample tried
     // cost a memory latency each)
     const SampWords sw = samp_load(a.samp, i);
@@ -654,10 +694,10 @@ __global__ __launch_bounds__(kThreads) void k_mark_lite(IndexlessArgs a, const u
                                                         uint32_t* __restrict__ mark32,
                                                         uint32_t* __restrict__ task_seg) {
     const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-    uint64_t j0, cnt;
+    const SegRec v = rec_unpack(i < a.nseg ? a.rec[i] : 0, i, a.seg_bits);
+    uint64_t j0, cnt = i < a.nseg ? v.c : 0;
     if (woff) {
         __shared__ uint32_t wsum[kThreads / 64];
-        cnt = i < a.nseg ? a.c[i] : 0;
         const uint32_t incl = wave_scan_incl(static_cast<uint32_t>(cnt));  // a workgroup's counts sum < 2^32
         if ((threadIdx.x & 63) == 63) wsum[threadIdx.x >> 6] = incl;
         __syncthreads();
@@ -669,15 +709,14 @@ __global__ __launch_bounds__(kThreads) void k_mark_lite(IndexlessArgs a, const u
     } else {
         if (i >= a.nseg) return;
         j0 = off[i];
-        cnt = a.c[i];
     }
     uint64_t m = (j0 + kIdx - 1) & ~static_cast<uint64_t>(kIdx - 1);
     const uint64_t m_end = j0 + cnt < sub_cap * kIdx ? j0 + cnt : sub_cap * kIdx;
     if (m >= m_end) return;
-    const uint64_t s_true = a.s[i];
+    const uint64_t s_true = v.s;
     const uint64_t s_spec = i * a.seg_bits;
-    const uint32_t tm = a.tm[i];
-    const int64_t dl = a.dl[i];
+    const uint32_t tm = v.tm;
+    const int64_t dl = v.dl;
     const SampWords sw = samp_load(a.samp, i);
     for (; m < m_end; m += kIdx) {
         const uint32_t t = static_cast<uint32_t>(m - j0);
@@ -705,13 +744,20 @@ __global__ __launch_bounds__(kThreads) void k_mark_lite(IndexlessArgs a, const u
     }
 }
 
+// c[i] from the packed records, for a scan over every segment (need_off)
+__global__ __launch_bounds__(kThreads) void k_rec_counts(const uint64_t* __restrict__ rec, uint64_t* __restrict__ c,
+                                                         uint64_t n) {
+    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i < n) c[i] = rec[i] & 0xFFFFu;
+}
+
 }  // namespace
 
 hipError_t launch_indexless_mark_lite(const IndexlessArgs& a, const uint64_t* off, const unsigned long long* woff,
                                       uint64_t* sub_abs, uint64_t sub_cap, hipStream_t st, uint32_t* mark32,
                                       uint32_t* task_seg) {
     if (a.nseg == 0) return hipSuccess;
-    if (!a.samp || (!off && !woff) || (!mark32 != !task_seg)) return hipErrorInvalidValue;
+    if (!a.samp || !a.rec || (!off && !woff) || (!mark32 != !task_seg)) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_mark_lite, dim3((a.nseg + kThreads - 1) / kThreads), dim3(kThreads), 0, st, a, off, woff,
                        sub_abs, sub_cap < (~0ull / kIdx) ? sub_cap : (~0ull / kIdx), mark32, task_seg);
     return hipGetLastError();
@@ -731,7 +777,7 @@ static bool use_staged(const IndexlessArgs& a) {
 hipError_t launch_indexless_mark(const IndexlessArgs& a, const uint64_t* off, uint64_t* sub_abs, uint32_t shift,
                                  hipStream_t st) {
     if (a.nseg == 0) return hipSuccess;
-    if (!use_staged(a) || !a.samp) return hipErrorInvalidValue;
+    if (!use_staged(a) || !a.samp || !a.rec) return hipErrorInvalidValue;
     const bool slow = a.max_len > a.stab_bits;
     IndexlessArgs m = a;
     m.wtab = nullptr;  // single steps: the walks stop at exact counts
@@ -745,7 +791,7 @@ bool indexless_staged(const IndexlessArgs& a) { return use_staged(a); }
 hipError_t launch_indexless_spec(const IndexlessArgs& a, hipStream_t st) {
     if (a.nseg == 0) return hipSuccess;
     if (use_staged(a)) {
-        if (!a.samp) return hipErrorInvalidValue;
+        if (!a.samp || !a.rec) return hipErrorInvalidValue;
         const bool slow = a.max_len > a.stab_bits;
         hipLaunchKernelGGL(slow ? k_spec_lds<true> : k_spec_lds<false>, dim3((a.nseg + kThreads - 1) / kThreads),
                            dim3(kThreads), lds_staged_bytes(a, kThreads), st, a);
@@ -766,15 +812,23 @@ hipError_t launch_indexless_settle_all(const IndexlessArgs& a, hipStream_t st) {
     const uint32_t grid = static_cast<uint32_t>(std::min<uint64_t>((a.nseg + kThreads - 1) / kThreads, 2048));
     if (a.fixlist && a.chain && use_staged(a)) {  // the staged pass listed what round 0 must look at
         const uint32_t lgrid = static_cast<uint32_t>(std::min<uint64_t>(((a.nseg / kThreads) + kThreads) / kThreads, 256));
-        hipLaunchKernelGGL(k_fix_list, dim3(std::max<uint32_t>(lgrid, 1)), dim3(kThreads), lds, st, g, a.s, a.x, a.c,
-                           a.tm, a.dl, a.flags, a.fixlist, a.chain);
-        hipLaunchKernelGGL(k_fix_chain, dim3(1), dim3(kChainThreads), lds, st, g, a.s, a.x, a.c, a.tm, a.dl, a.flags,
-                           a.chain);
+        const PackedRecs R{a.rec, a.seg_bits};
+        hipLaunchKernelGGL(k_fix_list, dim3(std::max<uint32_t>(lgrid, 1)), dim3(kThreads), lds, st, g, R, a.x,
+                           a.flags, a.fixlist, a.chain);
+        hipLaunchKernelGGL(k_fix_chain, dim3(1), dim3(kChainThreads), lds, st, g, R, a.x, a.flags, a.chain);
         return hipGetLastError();
     }
     for (int r = 0; r < kFixRounds; ++r)
         hipLaunchKernelGGL(k_fix, dim3(grid), dim3(kThreads), lds, st, g, a.s, a.x, a.c, a.tm, a.dl, a.flags, r);
     hipLaunchKernelGGL(k_settle, dim3(1), dim3(64), lds, st, g, a.s, a.x, a.c, a.tm, a.flags);
+    return hipGetLastError();
+}
+
+hipError_t launch_indexless_counts(const IndexlessArgs& a, hipStream_t st) {
+    if (a.nseg == 0) return hipSuccess;
+    if (!a.rec || !a.c) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_rec_counts, dim3((a.nseg + kThreads - 1) / kThreads), dim3(kThreads), 0, st, a.rec, a.c,
+                       a.nseg);
     return hipGetLastError();
 }
 

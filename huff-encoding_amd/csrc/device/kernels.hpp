@@ -165,6 +165,10 @@ struct IndexlessArgs {
     // (tm = kNoMerge: never within the segment)
     uint32_t* tm;
     int32_t* dl;
+    // (LDS-staged path) s, c, tm and dl of segment i packed in rec[i]
+    // (indexless.hip rec_pack: count, tm, dl, start - i*S; 16 bits each); the
+    // arrays above are then unused, but c for launch_indexless_counts
+    uint64_t* rec;
     // [0, kFixRounds): round r found a changed exit; [kFixRounds]: fixlist
     // count; [kFixRounds + 1, +2]: the counts of the chain's two lists;
     // [kFixRounds + 3]: the chain's fixes in all
@@ -422,6 +426,8 @@ hipError_t launch_indexless_spec(const IndexlessArgs& a, hipStream_t s);
 // round still changed an exit. No host round trip either way.
 hipError_t launch_indexless_settle_all(const IndexlessArgs& a, hipStream_t s);
 hipError_t launch_indexless_emit(const IndexlessArgs& a, const uint64_t* off, uint8_t* out, hipStream_t s);
+// (LDS-staged path) c[i] = the packed records' counts, for a scan over every segment
+hipError_t launch_indexless_counts(const IndexlessArgs& a, hipStream_t s);
 // restart index for the ring decoder: sub_abs[g] = start bit of symbol 256 g
 // sub_abs[g] = start bit of symbol g << shift (shift 8: the ring/wide
 // decoders' 256-symbol runs; 6: k_decode_fixed's kIdx = 64)

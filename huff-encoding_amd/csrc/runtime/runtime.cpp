@@ -1133,6 +1133,8 @@ Status indexless_sync(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_bytes,
         a.fixlist = static_cast<uint32_t*>(st.fixlist.p);
         HUFF_TRY(st.chain.ensure(nseg * 8 + 8));
         a.chain = static_cast<uint32_t*>(st.chain.p);
+        HUFF_TRY(st.rec.ensure(nseg * 8));
+        a.rec = static_cast<uint64_t*>(st.rec.p);
         a.wtot = static_cast<unsigned long long*>(st.wtot.p);
     } else {  // k_spec leaves the merge record to the fix-up rounds
         HIP_TRY(hipMemsetAsync(st.tm.p, 0, nseg * 4, strm));
@@ -1166,6 +1168,7 @@ Status indexless_sync(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_bytes,
         HIP_TRY(dev::launch_scan(static_cast<const uint64_t*>(st.wtot.p), static_cast<uint32_t>(nwg), 0,
                                  static_cast<uint64_t*>(st.woff.p), static_cast<uint64_t*>(st.tsum.p), strm, done));
     } else {
+        if (a.rec) HIP_TRY(dev::launch_indexless_counts(a, strm));  // the staged pass packs its counts
         HIP_TRY(dev::launch_scan(static_cast<const uint64_t*>(st.c.p), static_cast<uint32_t>(nseg), 0,
                                  static_cast<uint64_t*>(st.off.p), static_cast<uint64_t*>(st.tsum.p), strm, done));
     }

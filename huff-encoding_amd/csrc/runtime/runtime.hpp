@@ -252,7 +252,7 @@ Status decode_indexless_dev(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_
 // symbol offsets per segment in `off`, the symbol count in `total`
 struct IndexlessSync {
     const DecTables* dt = nullptr;  // tables of the tree, uploaded to ctx->d_lut
-    DevBuf s, x0, c, off, flag, tsum, samp, tm, dl, fixlist, chain;
+    DevBuf s, x0, c, off, flag, tsum, samp, tm, dl, fixlist, chain, rec;
     DevBuf wtot, woff;  // per-workgroup code counts of the staged pass and their exclusive scan
     dev::IndexlessArgs a{};
     uint64_t total = 0;
