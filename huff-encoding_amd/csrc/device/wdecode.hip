@@ -7,7 +7,7 @@
 // task's compressed bits are one contiguous range: the wave stages it in LDS
 // with coalesced 16-B loads (a range longer than the stage decodes from
 // global memory instead), then every lane makes exactly 64 lookups in a
-// two-level table (LDS when it fits): level 1 by the first K1 <= 10 bits,
+// two-level table (LDS when it fits): level 1 by the first K1 <= 11 bits,
 // level 2 by exactly the bits the deepest code below needs (host/wtree.cpp
 // build_wide_stab), two reads per letter for every lane, no divergence. An
 // entry carries the code length and the letter itself for letters of <= 4
