@@ -192,6 +192,9 @@ struct IndexlessArgs {
     // the global multi-level table `lut`
     const uint32_t* l2;
     uint32_t l2_words;
+    // > 0: l2 is the uniform form, 2^l2_e u8 lengths per slow window, no
+    // descriptors (DecTables::l2E)
+    uint32_t l2_e;
     // (LDS-staged path) the code count of each workgroup's 256 segments,
     // written by the speculative pass and kept by the fix-up kernels (atomic
     // deltas): the scan runs over workgroups, k_mark_lite scans inside one

@@ -22,6 +22,8 @@ struct Staged {
     const uint32_t* w;
     uint64_t base;       // bit position of w[0]'s most significant bit
     const uint32_t* l2;  // the level-2 length table in LDS (null: the global multi-level table)
+    uint32_t l2e = 0;    // > 0: its uniform form (IndexlessArgs::l2_e), else descriptors
+    bool nofill = false; // every code <= 16 bits: a slow step needs no refill of its own
 };
 
 // The block's range from its 16-B granule, 8 loads of 16 B per lane in
@@ -85,9 +87,13 @@ struct Cursor {
     const uint32_t* l2;
     uint64_t buf;
     uint32_t X, rp, nextw;
+    uint32_t l2e;
+    bool nofill;
     __device__ __forceinline__ void init(const Staged& st, uint64_t p) {
         w = st.w;
         l2 = st.l2;
+        l2e = st.l2e;
+        nofill = st.nofill;
         const uint64_t rel = p - st.base;
         rp = static_cast<uint32_t>(rel >> 5);
         const uint32_t sh = static_cast<uint32_t>(rel & 31);
@@ -103,12 +109,24 @@ struct Cursor {
         nextw = __builtin_bswap32(w[rp]);
     }
     // the length of the next code, consumed; codes longer than the table's
-    // index (kSsSlow) through the level-2 length table in LDS (descriptor
+    // index (kSsSlow) through the level-2 length table in LDS (the window's
     // index in the entry's bits [0, 7) and [8, 16)), else the global
-    // multi-level table
+    // multi-level table. Uniform form (l2e > 0): the window's 2^l2e lengths
+    // at l2e * index, one read; with every code <= 16 bits the chunk's refill
+    // every two codes covers it (>= 32 valid bits then), so no refills here.
     template <bool SLOW>
     __device__ __forceinline__ uint32_t step(const uint16_t* stab, uint32_t K, const uint32_t* glut, uint32_t Kg) {
         uint32_t e = stab[static_cast<uint32_t>(buf >> 32) >> (32 - K)];
+        if (SLOW && (e & kSsSlow) && l2 && l2e) {
+            if (!nofill) refill();  // >= 32 valid bits: the whole code (<= 32 bits)
+            const uint32_t s = (e & 0x7Fu) | ((e >> 8) << 7);
+            const uint32_t j = (static_cast<uint32_t>(buf >> 32) << K) >> (32 - l2e);
+            const uint32_t l1 = reinterpret_cast<const uint8_t*>(l2)[(s << l2e) + j];
+            buf <<= l1;
+            X -= l1;
+            if (!nofill) refill();
+            return l1;
+        }
         if (SLOW && (e & kSsSlow) && l2) {
             refill();  // >= 32 valid bits: the whole code (<= 32 bits)
             const uint32_t d = l2[(e & 0x7Fu) | ((e >> 8) << 7)];
@@ -255,6 +273,8 @@ __device__ __forceinline__ const uint16_t* load_stab(const A& a, uint32_t* lds) 
 template <class A>
 __device__ __forceinline__ Staged with_l2(Staged st, const A& a, const uint32_t* lds) {
     st.l2 = a.l2_words ? lds + stab_words(a) : nullptr;
+    st.l2e = a.l2_words ? a.l2_e : 0u;
+    st.nofill = st.l2e && a.max_len <= 16;
     return st;
 }
 

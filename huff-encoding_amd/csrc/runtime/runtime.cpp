@@ -202,15 +202,24 @@ static void build_walk_table(const HuffTree& t, uint32_t sbits, DecTables& out) 
 // that once took two dependent global reads (the 8-bit secondary tables) takes
 // two LDS reads. Skipped past kL2MaxBytes (the LDS beside the stage) or for
 // codes > 32 bits.
+// Uniform form (DecTables::l2E) when it fits: every slow window gets 2^Emax
+// lengths (Emax = the deepest leaf below any of them), so a slow step reads
+// one length at index << Emax | next bits instead of a descriptor and then a
+// length (two dependent LDS reads).
 static void build_len_l2(const HuffTree& t, DecTables& out) {
     constexpr size_t kL2MaxBytes = 24 * 1024;
     constexpr uint32_t kMaxDesc = 1u << 15;
     const uint32_t K = out.sbits;
     if (t.root_is_leaf() || out.maxdepth <= K || out.maxdepth > 32) return;
     const auto& nodes = t.nodes();
-    std::vector<uint32_t> desc;
-    std::vector<uint8_t> lens;
-    std::vector<std::pair<uint32_t, uint32_t>> slow;  // (window, descriptor)
+    struct Slow {
+        uint32_t window;
+        int32_t node;
+        uint32_t E;  // the deepest leaf below node, relative to it
+    };
+    std::vector<Slow> slow;
+    uint32_t Emax = 0;
+    size_t desc_bytes = 0;
     for (uint32_t i = 0; i < (1u << K); ++i) {
         int32_t x = t.root();
         bool leaf = false;
@@ -219,7 +228,7 @@ static void build_len_l2(const HuffTree& t, DecTables& out) {
             leaf = nodes[x].is_leaf;
         }
         if (leaf) continue;
-        uint32_t E = 0;  // the deepest leaf below x, relative to x
+        uint32_t E = 0;
         std::vector<std::pair<int32_t, uint32_t>> st{{x, 0}};
         while (!st.empty()) {
             auto [y, d] = st.back();
@@ -231,35 +240,47 @@ static void build_len_l2(const HuffTree& t, DecTables& out) {
                 st.push_back({nodes[y].right, d + 1});
             }
         }
-        if (desc.size() >= kMaxDesc || K + E > 32) return;
-        desc.push_back(static_cast<uint32_t>((lens.size() << 5) | E));  // byte offset fixed below
-        slow.push_back({i, static_cast<uint32_t>(desc.size() - 1)});
-        for (uint32_t j = 0; j < (1u << E); ++j) {
-            int32_t y = x;
-            uint32_t r = E;
-            for (uint32_t p = 0; p < E; ++p) {
-                y = ((j >> (E - 1 - p)) & 1u) ? nodes[y].right : nodes[y].left;
-                if (nodes[y].is_leaf) {
-                    r = p + 1;
-                    break;
-                }
-            }
-            lens.push_back(static_cast<uint8_t>(K + r));
-        }
-        if (desc.size() * 4 + lens.size() > kL2MaxBytes) return;
+        if (slow.size() >= kMaxDesc || K + E > 32) return;
+        slow.push_back({i, x, E});
+        Emax = std::max(Emax, E);
+        desc_bytes += 4 + (size_t(1) << E);
     }
-    if (desc.empty()) return;
-    const uint32_t base = static_cast<uint32_t>(desc.size() * 4);
-    for (uint32_t& d : desc) d = (((d >> 5) + base) << 5) | (d & 31u);
+    if (slow.empty()) return;
+    const bool uniform = (slow.size() << Emax) <= kL2MaxBytes;
+    if (!uniform && desc_bytes > kL2MaxBytes) return;
+    // the length of the code below `x` whose next E bits are j
+    auto len_below = [&](int32_t x, uint32_t E, uint32_t j) {
+        int32_t y = x;
+        for (uint32_t p = 0; p < E; ++p) {
+            y = ((j >> (E - 1 - p)) & 1u) ? nodes[y].right : nodes[y].left;
+            if (nodes[y].is_leaf) return static_cast<uint8_t>(K + p + 1);
+        }
+        return static_cast<uint8_t>(K + E);
+    };
+    std::vector<uint8_t> b;
+    if (uniform) {
+        out.l2E = Emax;
+        b.resize(slow.size() << Emax);
+        for (size_t s = 0; s < slow.size(); ++s)
+            for (uint32_t j = 0; j < (1u << Emax); ++j) b[(s << Emax) + j] = len_below(slow[s].node, Emax, j);
+    } else {  // descriptors (byte offset << 5 | E), then each window's 2^E lengths
+        out.l2E = 0;
+        b.resize(slow.size() * 4);
+        for (size_t s = 0; s < slow.size(); ++s) {
+            const uint32_t d = static_cast<uint32_t>((b.size() << 5) | slow[s].E);
+            std::memcpy(&b[s * 4], &d, 4);
+            for (uint32_t j = 0; j < (1u << slow[s].E); ++j) b.push_back(len_below(slow[s].node, slow[s].E, j));
+        }
+    }
     out.l2off = static_cast<uint32_t>(out.lut.size());
-    out.l2words = static_cast<uint32_t>((desc.size() * 4 + lens.size() + 15) / 16 * 4);
+    out.l2words = static_cast<uint32_t>((b.size() + 15) / 16 * 4);
     out.lut.resize(out.lut.size() + out.l2words, 0);
-    uint8_t* b = reinterpret_cast<uint8_t*>(out.lut.data() + out.l2off);
-    std::memcpy(b, desc.data(), desc.size() * 4);
-    std::memcpy(b + base, lens.data(), lens.size());
+    std::memcpy(out.lut.data() + out.l2off, b.data(), b.size());
+    std::vector<std::pair<uint32_t, uint32_t>> slow_ix;  // (window, index)
+    for (size_t s = 0; s < slow.size(); ++s) slow_ix.push_back({slow[s].window, static_cast<uint32_t>(s)});
     uint16_t* s = reinterpret_cast<uint16_t*>(out.lut.data() + out.soff);
     uint16_t* w = reinterpret_cast<uint16_t*>(out.lut.data() + out.woff);
-    for (auto [i, d] : slow) {
+    for (auto [i, d] : slow_ix) {
         const uint16_t e = static_cast<uint16_t>(dev::kSsSlow | (d & 0x7Fu) | ((d >> 7) << 8));
         s[i] = e;
         w[i] = e;
@@ -269,6 +290,7 @@ static void build_len_l2(const HuffTree& t, DecTables& out) {
 Status build_dec_tables(const HuffTree& t, DecTables& out) {
     const auto& nodes = t.nodes();
     out.lut.clear();
+    out.l2off = out.l2words = out.l2E = 0;
     if (t.root_is_leaf()) {  // every bit decodes the root letter (comp.rs:506-509)
         out.bits = 1;
         out.maxdepth = 1;
@@ -1117,6 +1139,7 @@ Status indexless_sync(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_bytes,
     if (dt->l2words && !std::getenv("HUFF_NO_L2")) {  // HUFF_NO_L2=1: the global secondary tables (A/B)
         a.l2 = static_cast<const uint32_t*>(ctx->d_lut.p) + dt->l2off;
         a.l2_words = dt->l2words;
+        a.l2_e = dt->l2E;
     }
     a.tm = static_cast<uint32_t*>(st.tm.p);
     a.dl = static_cast<int32_t*>(st.dl.p);

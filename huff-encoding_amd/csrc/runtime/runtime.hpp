@@ -59,7 +59,11 @@ struct DecTables {
     // (byte offset of the prefix's entries in this block << 5 | its index
     // bits E) then u8 code lengths; the slow entries of stab and the walk
     // table carry their descriptor index in bits [0, 7) and [8, 16). 0: none
-    uint32_t l2off = 0, l2words = 0;
+    // l2E > 0: the uniform form instead, no descriptors: every slow window s
+    // has 2^l2E lengths at byte s << l2E (l2E = the deepest leaf below any
+    // slow window), indexed by the l2E bits after the first sbits; the slow
+    // entries carry s the same way
+    uint32_t l2off = 0, l2words = 0, l2E = 0;
 };
 
 // append the multi-symbol table (decode.hip k_decode_ms) to out.lut
