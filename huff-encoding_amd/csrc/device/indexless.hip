@@ -372,7 +372,8 @@ __device__ __forceinline__ void samp_pick(const SampWords& w, uint32_t nsamp, ui
 // segment then find nothing to walk. Without it every lane walked from its
 // predecessor's exit to its first sample (>= 128 bits) and each wave waited
 // for its slowest lane.
-// The lead (IndexlessArgs::lead_bits) is kLeadBits rounded down to a multiple
+// The lead (IndexlessArgs::lead_bits; kLeadBitsLong when codes exceed the
+// walk table's index) is kLeadBits rounded down to a multiple
 // of the gcd of the code lengths, like the segment starts, so a lane never
 // starts out of phase: with all codes 6 bits long a 128-bit lead-in walked a
 // path that never met the true one and the fix-up chained through every
@@ -765,7 +766,7 @@ hipError_t launch_indexless_mark_lite(const IndexlessArgs& a, const uint64_t* of
 
 static size_t lds_staged_bytes(const IndexlessArgs& a, uint32_t segs) {
     return static_cast<size_t>((((((1u << a.stab_bits) + 1) / 2) + 3) & ~3u) + a.l2_words) * 4 +
-           ((segs * a.seg_bits + 7) / 8 + (kLeadBits + 7) / 8 + 128 + 15) / 16 * 16;
+           ((segs * a.seg_bits + 7) / 8 + (a.lead_bits + 7) / 8 + 128 + 15) / 16 * 16;
 }
 
 static bool use_staged(const IndexlessArgs& a) {

@@ -144,7 +144,7 @@ struct IndexlessArgs {
     uint64_t comp_bytes;
     uint64_t valid_bits;          // B
     uint64_t seg_bits;            // S (multiple of the gcd of code lengths)
-    uint32_t lead_bits;           // the staged pass's lead-in (<= kLeadBits, a multiple of the gcd; 0: none)
+    uint32_t lead_bits;           // the staged pass's lead-in (<= kLeadBitsLong, a multiple of the gcd; 0: none)
     uint64_t nseg;
     const uint32_t* lut;
     uint32_t lut_bits;
@@ -207,6 +207,11 @@ struct IndexlessArgs {
 #define HUFF_LEAD_BITS 128
 #endif
 constexpr uint32_t kLeadBits = HUFF_LEAD_BITS;
+// trees with codes longer than the walk table's index take longer to fall
+// onto the true path: twice the lead-in (wide letters, Zipf over 4,096:
+// W = 4 index-free 1.35 -> 1.27 ms, W = 2 2.01 -> 1.98; byte streams whose
+// codes all fit the table keep 128: 256 measured 1 % slower on text)
+constexpr uint32_t kLeadBitsLong = 2 * kLeadBits;
 // the speculative pass's sample spacing (indexless.hip); segments < 1024 bits
 #ifndef HUFF_SAMP_BITS
 #define HUFF_SAMP_BITS 96

@@ -116,7 +116,13 @@ struct Cursor {
     // every two codes covers it (>= 32 valid bits then), so no refills here.
     template <bool SLOW>
     __device__ __forceinline__ uint32_t step(const uint16_t* stab, uint32_t K, const uint32_t* glut, uint32_t Kg) {
-        uint32_t e = stab[static_cast<uint32_t>(buf >> 32) >> (32 - K)];
+        return step_entry<SLOW>(stab[static_cast<uint32_t>(buf >> 32) >> (32 - K)], K, glut, Kg);
+    }
+    // the same from the window's entry already read (a walk-table entry of a
+    // slow window is the single-symbol table's: the multi-code walk does not
+    // read it twice)
+    template <bool SLOW>
+    __device__ __forceinline__ uint32_t step_entry(uint32_t e, uint32_t K, const uint32_t* glut, uint32_t Kg) {
         if (SLOW && (e & kSsSlow) && l2 && l2e) {
             if (!nofill) refill();  // >= 32 valid bits: the whole code (<= 32 bits)
             const uint32_t s = (e & 0x7Fu) | ((e >> 8) << 7);
@@ -179,7 +185,7 @@ struct Cursor {
             if ((k & 1) == 0) refill();
             const uint32_t e = wtab[static_cast<uint32_t>(buf >> 32) >> (32 - K)];
             if (SLOW && (e & kSsSlow)) {
-                U += step<SLOW>(stab, K, glut, Kg);
+                U += step_entry<SLOW>(e, K, glut, Kg);
                 N += 1;
             } else {
                 const uint32_t u = (e >> 8) & 15u;
@@ -201,7 +207,7 @@ struct Cursor {
             if ((k & 1) == 0) refill();
             const uint32_t e = wtab[static_cast<uint32_t>(buf >> 32) >> (32 - K)];
             if (SLOW && (e & kSsSlow)) {
-                Q += step<SLOW>(stab, K, glut, Kg) + (1u << 16);
+                Q += step_entry<SLOW>(e, K, glut, Kg) + (1u << 16);
             } else {
                 const uint32_t u = (e >> 8) & 15u;
                 buf <<= u;

@@ -1123,7 +1123,8 @@ Status indexless_sync(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_bytes,
     a.comp_bytes = comp_bytes;
     a.valid_bits = valid_bits;
     a.seg_bits = S;
-    a.lead_bits = dev::kLeadBits / g * g;  // in phase with the segment starts
+    // in phase with the segment starts; longer for codes past the walk table
+    a.lead_bits = (dt->maxdepth > dt->sbits ? dev::kLeadBitsLong : dev::kLeadBits) / g * g;
     a.nseg = nseg;
     a.lut = static_cast<const uint32_t*>(ctx->d_lut.p);
     a.lut_bits = dt->bits;
