@@ -75,6 +75,48 @@ __device__ __forceinline__ bool step(BitReader& rd, const BitSrc& src, const Lut
     return true;
 }
 
+// how fix_one walks a code: the decoder's table (LDS primary, global
+// secondaries), or — on the staged path, whose fix-up needs only lengths —
+// the walk table and the level-2 length table, both in LDS (LenStep: a code
+// past the 12-bit walk table was two global reads, a window re-read and a
+// secondary table; wide Zipf over 4,096 letters has 16 % of them)
+struct LutStep {
+    Lut lut;
+    __device__ __forceinline__ bool operator()(BitReader& rd, const BitSrc& src, uint64_t B) const {
+        return step(rd, src, lut, B);
+    }
+};
+struct LenStep {
+    const uint16_t* wt;  // walk table: first code's length in bits [0, 6), kSsSlow
+    const uint8_t* l2;   // level-2 lengths (uniform: l2e > 0; else descriptors first)
+    uint32_t K, l2e;
+    __device__ __forceinline__ bool operator()(BitReader& rd, const BitSrc& src, uint64_t B) const {
+        if (rd.nb < 32) {  // >= 32 valid bits: any code (<= 32 bits)
+            rd.buf |= static_cast<uint64_t>(src.word(rd.wi)) << (32 - rd.nb);
+            ++rd.wi;
+            rd.nb += 32;
+        }
+        const uint32_t top = static_cast<uint32_t>(rd.buf >> 32);
+        const uint32_t e = wt[top >> (32 - K)];
+        uint32_t len = e & 63u;
+        if (e & kSsSlow) {
+            const uint32_t s = (e & 0x7Fu) | ((e >> 8) << 7);
+            if (l2e) {
+                len = l2[(s << l2e) + ((top << K) >> (32 - l2e))];
+            } else {
+                const uint32_t d = reinterpret_cast<const uint32_t*>(l2)[s];
+                len = l2[(d >> 5) + ((top << K) >> (32 - (d & 31u)))];
+            }
+        }
+        if (rd.pos + len > B) {
+            rd.pos = B;
+            return false;
+        }
+        rd.advance(src, len);
+        return true;
+    }
+};
+
 __global__ __launch_bounds__(kThreads) void k_spec(Seg g, uint64_t* __restrict__ s, uint64_t* __restrict__ x,
                                                    uint64_t* __restrict__ c) {
     extern __shared__ uint32_t plut[];
@@ -142,16 +184,15 @@ struct PackedRecs {
 // from this round or the last: either is a boundary of a valid path, and a
 // changed exit sets flags[r], so the next round looks again)
 // nl / ncnt: a list the successor of a changed exit is appended to (the chain)
-template <class Recs>
+template <class Recs, class Step>
 __device__ __forceinline__ void fix_one(const Seg& g, const Recs& R, uint64_t* __restrict__ x,
-                                        unsigned int* __restrict__ flags, int r, uint64_t i, const uint32_t* plut,
+                                        unsigned int* __restrict__ flags, int r, uint64_t i, const Step& step,
                                         uint32_t* nl = nullptr, unsigned int* ncnt = nullptr) {
     const uint64_t ns = x[i - 1];
     SegRec v = R.load(i);
     const uint64_t old_s = v.s;
     if (ns == old_s) return;
     const BitSrc src{reinterpret_cast<const uint32_t*>(g.comp), g.comp, g.comp_bytes};
-    const Lut lut{plut, g.lut, g.K};
     const uint64_t end = (i + 1 == g.nseg) ? g.B : ((i + 1) * g.S < g.B ? (i + 1) * g.S : g.B);
     BitReader a, b;
     a.seek(src, ns);
@@ -191,10 +232,10 @@ __device__ __forceinline__ void fix_one(const Seg& g, const Recs& R, uint64_t* _
             return;
         }
         if (a.pos < b.pos || !b_alive) {
-            a_alive = step(a, src, lut, g.B);
+            a_alive = step(a, src, g.B);
             ca += a_alive ? 1 : 0;
         } else {
-            b_alive = step(b, src, lut, g.B);
+            b_alive = step(b, src, g.B);
             cb += b_alive ? 1 : 0;
         }
     }
@@ -210,24 +251,52 @@ __global__ __launch_bounds__(kThreads) void k_fix(Seg g, uint64_t* __restrict__ 
     load_prim(plut, g);
     for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < g.nseg;
          i += static_cast<uint64_t>(gridDim.x) * blockDim.x)
-        if (i) fix_one(g, ArrayRecs{s, c, tm, dl}, x, flags, r, i, plut);
+        if (i) fix_one(g, ArrayRecs{s, c, tm, dl}, x, flags, r, i, LutStep{Lut{plut, g.lut, g.K}});
+}
+
+// the staged path's length tables for the fix-up (LenStep), copied to LDS;
+// wt null: the decoder's table (LutStep)
+struct FixTabs {
+    const uint16_t* wt;
+    const uint32_t* l2;
+    uint32_t K, l2_words, l2e;
+};
+// the stepper over the tables in LDS (`lds`: 2^K u16 then l2_words words)
+__device__ __forceinline__ LenStep load_len_step(const FixTabs& f, uint32_t* lds) {
+    const uint32_t tw = ((1u << f.K) + 1) / 2;
+    const uint32_t* w32 = reinterpret_cast<const uint32_t*>(f.wt);
+    for (uint32_t i = threadIdx.x; i < tw; i += blockDim.x) lds[i] = w32[i];
+    for (uint32_t i = threadIdx.x; i < f.l2_words; i += blockDim.x) lds[tw + i] = f.l2[i];
+    __syncthreads();
+    return LenStep{reinterpret_cast<const uint16_t*>(lds), reinterpret_cast<const uint8_t*>(lds + tw), f.K, f.l2e};
 }
 
 // round 0 after the staged speculative pass: only the segments that can
 // differ from their predecessor's exit — every workgroup's first segment and
 // the listed successors of in-workgroup new exits (each index once, so no two
 // lanes update one segment's merge record)
-__global__ __launch_bounds__(kThreads) void k_fix_list(Seg g, PackedRecs R, uint64_t* __restrict__ x,
-                                                       unsigned int* __restrict__ flags,
-                                                       const uint32_t* __restrict__ list, uint32_t* __restrict__ chain) {
-    extern __shared__ uint32_t plut[];
-    load_prim(plut, g);
+template <class Step>
+__device__ __forceinline__ void fix_list_body(const Seg& g, const PackedRecs& R, uint64_t* __restrict__ x,
+                                              unsigned int* __restrict__ flags, const uint32_t* __restrict__ list,
+                                              uint32_t* __restrict__ chain, const Step& step) {
     const uint64_t firsts = (g.nseg - 1) / kThreads;  // segments 256, 512, ...
     const uint64_t n = firsts + __builtin_nontemporal_load(flags + kFixRounds);
     for (uint64_t j = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; j < n;
          j += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
         const uint64_t i = j < firsts ? (j + 1) * kThreads : list[j - firsts];
-        fix_one(g, R, x, flags, 0, i, plut, chain, flags + kFixRounds + 1);
+        fix_one(g, R, x, flags, 0, i, step, chain, flags + kFixRounds + 1);
+    }
+}
+__global__ __launch_bounds__(kThreads) void k_fix_list(Seg g, PackedRecs R, uint64_t* __restrict__ x,
+                                                       unsigned int* __restrict__ flags,
+                                                       const uint32_t* __restrict__ list, uint32_t* __restrict__ chain,
+                                                       FixTabs f) {
+    extern __shared__ uint32_t plut[];
+    if (f.wt) {
+        fix_list_body(g, R, x, flags, list, chain, load_len_step(f, plut));
+    } else {
+        load_prim(plut, g);
+        fix_list_body(g, R, x, flags, list, chain, LutStep{Lut{plut, g.lut, g.K}});
     }
 }
 
@@ -240,12 +309,26 @@ __global__ __launch_bounds__(kThreads) void k_fix_list(Seg g, PackedRecs R, uint
 // appends it); a lane reading an exit its predecessor changes in the same
 // round gets the successor listed again for the next round.
 constexpr int kChainThreads = 1024;
+template <class Step>
+__device__ __forceinline__ void fix_chain_body(const Seg& g, const PackedRecs& R, uint64_t* __restrict__ x,
+                                               unsigned int* __restrict__ flags, uint32_t* __restrict__ chain,
+                                               const Step& step);
 __global__ __launch_bounds__(kChainThreads) void k_fix_chain(Seg g, PackedRecs R, uint64_t* __restrict__ x,
                                                              unsigned int* __restrict__ flags,
-                                                             uint32_t* __restrict__ chain) {
+                                                             uint32_t* __restrict__ chain, FixTabs f) {
     if (__builtin_nontemporal_load(flags + kFixRounds + 1) == 0) return;  // round 0 changed no exit
     extern __shared__ uint32_t plut[];
-    load_prim(plut, g);
+    if (f.wt) {
+        fix_chain_body(g, R, x, flags, chain, load_len_step(f, plut));
+    } else {
+        load_prim(plut, g);
+        fix_chain_body(g, R, x, flags, chain, LutStep{Lut{plut, g.lut, g.K}});
+    }
+}
+template <class Step>
+__device__ __forceinline__ void fix_chain_body(const Seg& g, const PackedRecs& R, uint64_t* __restrict__ x,
+                                               unsigned int* __restrict__ flags, uint32_t* __restrict__ chain,
+                                               const Step& step) {
     __shared__ uint32_t n_sh;
     uint32_t cur = 0;
     for (;;) {
@@ -257,7 +340,7 @@ __global__ __launch_bounds__(kChainThreads) void k_fix_chain(Seg g, PackedRecs R
         if (n == 0) break;
         const uint32_t* list = chain + static_cast<uint64_t>(cur) * g.nseg;
         uint32_t* nl = chain + static_cast<uint64_t>(cur ^ 1u) * g.nseg;
-        for (uint32_t j = threadIdx.x; j < n; j += blockDim.x) fix_one(g, R, x, flags, 0, list[j], plut, nl, ncnt);
+        for (uint32_t j = threadIdx.x; j < n; j += blockDim.x) fix_one(g, R, x, flags, 0, list[j], step, nl, ncnt);
         __syncthreads();  // every fix of the round done (and n_sh read by every lane)
         if (threadIdx.x == 0) {
             atomicExch(cnt, 0u);
@@ -814,9 +897,17 @@ hipError_t launch_indexless_settle_all(const IndexlessArgs& a, hipStream_t st) {
     if (a.fixlist && a.chain && use_staged(a)) {  // the staged pass listed what round 0 must look at
         const uint32_t lgrid = static_cast<uint32_t>(std::min<uint64_t>(((a.nseg / kThreads) + kThreads) / kThreads, 256));
         const PackedRecs R{a.rec, a.seg_bits};
-        hipLaunchKernelGGL(k_fix_list, dim3(std::max<uint32_t>(lgrid, 1)), dim3(kThreads), lds, st, g, R, a.x,
-                           a.flags, a.fixlist, a.chain);
-        hipLaunchKernelGGL(k_fix_chain, dim3(1), dim3(kChainThreads), lds, st, g, R, a.x, a.flags, a.chain);
+        // lengths only: the walk table and the level-2 lengths in LDS, when
+        // every code past the table has its level-2 entry
+        FixTabs f{};
+        size_t flds = lds;
+        if (a.stab && (a.max_len <= a.stab_bits || a.l2_words)) {
+            f = FixTabs{a.wtab ? a.wtab : a.stab, a.l2, a.stab_bits, a.l2_words, a.l2_e};
+            flds = std::max<size_t>(lds, (((1u << a.stab_bits) + 1) / 2 + a.l2_words) * 4);
+        }
+        hipLaunchKernelGGL(k_fix_list, dim3(std::max<uint32_t>(lgrid, 1)), dim3(kThreads), flds, st, g, R, a.x,
+                           a.flags, a.fixlist, a.chain, f);
+        hipLaunchKernelGGL(k_fix_chain, dim3(1), dim3(kChainThreads), flds, st, g, R, a.x, a.flags, a.chain, f);
         return hipGetLastError();
     }
     for (int r = 0; r < kFixRounds; ++r)

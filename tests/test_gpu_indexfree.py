@@ -227,3 +227,19 @@ def test_indexfree_lead_in_phase(H, O, ctx, monkeypatch, capfd):
         err = capfd.readouterr().err
         stats = re.findall(r"listed by the speculative pass (\d+), chain fixes (\d+)", err)
         assert stats and all(a == "0" and b == "0" for a, b in stats), err
+
+
+def test_indexfree_even_lengths_past_table(H, O, ctx):
+    """every code an even length, up to 14 bits (past the 12-bit walk table):
+    the long lead-in (kLeadBitsLong, kept a multiple of 2), the uniform
+    level-2 length table and the refill-free slow steps (codes <= 16 bits)
+    together; weights 4^k give a quaternary tree whatever the tie order"""
+    rng = np.random.default_rng(41)
+    letters = rng.permutation(256)[:22].astype(np.uint8)
+    counts = [4 ** (7 - i) for i in range(1, 7) for _ in range(3)] + [1] * 4
+    data = rng.permutation(np.repeat(letters, np.array(counts) * 300)).tobytes()
+    lens = O.Tree.from_weights(O.weights_from_bytes(data)).code_table()[1]
+    used = lens[letters]
+    assert (used % 2 == 0).all() and used.max() == 14, used
+    roundtrip(H, O, ctx, data)
+    roundtrip(H, O, ctx, data[: len(data) // 3 + 7])
