@@ -181,6 +181,81 @@ __global__ __launch_bounds__(T) void k_hist1(const uint8_t* __restrict__ base, u
     }
 }
 
+// Two chunks per 512-thread workgroup sharing ONE 32-copy LDS image: the
+// first chunk's threads add 1, the second's 1 << 16 (a copy counts at most
+// 8 threads x 256 bytes = 2,048 of a chunk, so neither half overflows), the
+// halves are split when the copies are summed. Twice the input in flight
+// per byte of LDS (the one-shot grid was LDS-bound at 5 workgroups per CU,
+// 320 KiB in flight against ~450 KiB for the calibration read): same-box
+// pass 1 uniform 0.215 -> 0.210 ms, Zipf 0.198 -> 0.193 (profiles/r05/hist_x2/).
+// The default; k_hist1 stays for HUFF_HIST_X2=0.
+template <int LOGC>
+__global__ __launch_bounds__(512) void k_hist1x2(const uint8_t* __restrict__ base, uint64_t lo, uint64_t hi,
+                                                 uint32_t nchunks, uint32_t* __restrict__ chunk_hist,
+                                                 unsigned long long* __restrict__ gw) {
+    constexpr uint32_t C = 1u << LOGC;
+    constexpr int T = 256;               // threads per chunk
+    constexpr int NL = kChunk / 16 / T;  // 16-B loads per lane
+    if (blockIdx.x == 0)
+        for (uint32_t i = threadIdx.x; i < kHistCopies * 256; i += 2 * T) gw[i] = 0;
+    __shared__ __attribute__((aligned(16))) uint32_t h[256 * C];
+    const uint32_t t = threadIdx.x, tl = t & (T - 1), half = t / T;
+    const uint32_t lane_c = t & (C - 1);
+    const uint32_t inc = half ? 0x10000u : 1u;
+    const uint32_t c = 2 * blockIdx.x + half;
+    const uint64_t cbeg = static_cast<uint64_t>(c) * kChunk;
+    const bool live = c < nchunks;
+    const bool full = live && cbeg >= lo && cbeg + kChunk <= hi;
+    uint4 v[NL];
+    if (full) {
+        const uint4* p = reinterpret_cast<const uint4*>(base + cbeg) + tl;
+#pragma unroll
+        for (int r = 0; r < NL; ++r) v[r] = ld_nt(p + r * T);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    uint4* h4 = reinterpret_cast<uint4*>(h);
+#pragma unroll
+    for (uint32_t i = 0; i < 256 * C / 4 / (2 * T); ++i) h4[t + i * 2 * T] = make_uint4(0, 0, 0, 0);
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_s_barrier();
+    auto add = [&](uint32_t w) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            __hip_atomic_fetch_add(&h[(((w >> (8 * k)) & 0xFFu) << LOGC) | lane_c], inc, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+    };
+    if (full) {
+#pragma unroll
+        for (int r = 0; r < NL; ++r) {
+            add(v[r].x);
+            add(v[r].y);
+            add(v[r].z);
+            add(v[r].w);
+        }
+    } else if (live) {
+        for (int r = 0; r < NL; ++r) {
+            const uint64_t off = cbeg + static_cast<uint64_t>(r) * (16 * T) + tl * 16;
+            if (off + 16 <= lo || off >= hi) continue;
+            for (int k = 0; k < 16; ++k)
+                if (off + k >= lo && off + k < hi)
+                    __hip_atomic_fetch_add(&h[(static_cast<uint32_t>(base[off + k]) << LOGC) | lane_c], inc,
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+    }
+    __syncthreads();
+    if (t < 256) {
+        uint32_t s0 = 0, s1 = 0;
+#pragma unroll 8
+        for (uint32_t j = 0; j < C; ++j) {
+            const uint32_t x = h[(t << LOGC) | ((j + t) & (C - 1))];
+            s0 += x & 0xFFFFu;
+            s1 += x >> 16;
+        }
+        chunk_hist[static_cast<uint64_t>(2 * blockIdx.x) * 256 + t] = s0;
+        if (2 * blockIdx.x + 1 < nchunks) chunk_hist[static_cast<uint64_t>(2 * blockIdx.x + 1) * 256 + t] = s1;
+    }
+}
+
 // gw[copy][b] += sum over a stripe of chunks of chunk_hist[c][b]
 __global__ __launch_bounds__(256) void k_rows_sum(const uint32_t* __restrict__ chunk_hist, uint32_t nchunks,
                                                   unsigned long long* __restrict__ gw) {
@@ -378,7 +453,16 @@ hipError_t launch_hist(const uint8_t* base, uint64_t lo, uint64_t hi, uint32_t n
     if (chunk_hist) {  // per-chunk rows wanted: one-shot grid, then the row sum
         // 32 copies: 16 measured equal on uniform bytes and 20 % slower on
         // Zipf (same-address conflicts between lanes l and l + 16)
-        hipLaunchKernelGGL(k_hist1<HUFF_HIST_LOGC>, dim3(nchunks), dim3(HUFF_HIST_THREADS), 0, s, base, lo, hi, chunk_hist, gw);
+// HUFF_HIST_X2=0: k_hist1, one chunk per workgroup (A/B builds)
+#ifndef HUFF_HIST_X2
+#define HUFF_HIST_X2 1
+#endif
+        if (HUFF_HIST_X2)
+            hipLaunchKernelGGL(k_hist1x2<HUFF_HIST_LOGC>, dim3((nchunks + 1) / 2), dim3(512), 0, s, base, lo, hi, nchunks,
+                               chunk_hist, gw);
+        else
+            hipLaunchKernelGGL(k_hist1<HUFF_HIST_LOGC>, dim3(nchunks), dim3(HUFF_HIST_THREADS), 0, s, base, lo, hi,
+                               chunk_hist, gw);
         const uint32_t g = nchunks < 512 ? nchunks : 512;
         hipLaunchKernelGGL(k_rows_sum, dim3(g), dim3(256), 0, s, chunk_hist, nchunks, gw);
         if (done.host) hipLaunchKernelGGL(k_hist_publish, dim3(1), dim3(256), 0, s, gw, done.host, done.tag);
