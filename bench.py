@@ -149,7 +149,7 @@ def cpu_baseline(workload: str, target_s: float):
 
 
 PHASE_KERNELS = {  # bench phase -> device kernels (names as in tools/summarize_prof.py)
-    "hist": ["k_hist1", "k_rows_sum"],
+    "hist": ["k_hist1x2", "k_rows_sum"],
     "chunk_bits": ["k_chunk_bits"],
     "scan": ["k_scan_tiles", "k_scan_fix"],
 }
