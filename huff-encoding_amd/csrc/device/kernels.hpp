@@ -195,6 +195,9 @@ struct IndexlessArgs {
     // > 0: l2 is the uniform form, 2^l2_e u8 lengths per slow window, no
     // descriptors (DecTables::l2E)
     uint32_t l2_e;
+    // uniform form with slow windows common (DecTables::l2dense): the walks
+    // read a length at every step instead of branching (segwalk.hpp)
+    uint32_t l2_dense;
     // (LDS-staged path) the code count of each workgroup's 256 segments,
     // written by the speculative pass and kept by the fix-up kernels (atomic
     // deltas): the scan runs over workgroups, k_mark_lite scans inside one

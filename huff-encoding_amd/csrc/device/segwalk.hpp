@@ -24,6 +24,7 @@ struct Staged {
     const uint32_t* l2;  // the level-2 length table in LDS (null: the global multi-level table)
     uint32_t l2e = 0;    // > 0: its uniform form (IndexlessArgs::l2_e), else descriptors
     bool nofill = false; // every code <= 16 bits: a slow step needs no refill of its own
+    bool dense = false;  // nofill, and slow windows common enough that every step reads a length
 };
 
 // The block's range from its 16-B granule, 8 loads of 16 B per lane in
@@ -88,12 +89,13 @@ struct Cursor {
     uint64_t buf;
     uint32_t X, rp, nextw;
     uint32_t l2e;
-    bool nofill;
+    bool nofill, dense;
     __device__ __forceinline__ void init(const Staged& st, uint64_t p) {
         w = st.w;
         l2 = st.l2;
         l2e = st.l2e;
         nofill = st.nofill;
+        dense = st.dense;
         const uint64_t rel = p - st.base;
         rp = static_cast<uint32_t>(rel >> 5);
         const uint32_t sh = static_cast<uint32_t>(rel & 31);
@@ -121,8 +123,24 @@ struct Cursor {
     // the same from the window's entry already read (a walk-table entry of a
     // slow window is the single-symbol table's: the multi-code walk does not
     // read it twice)
+    // dense: the length of a slow window's code read by every lane (a
+    // broadcast of byte 0 for the others), no divergent branch: when most
+    // steps of a wave have a slow lane anyway (wide Zipf over 4,096 letters:
+    // 16 % of the codes) the branch only added its exec-mask work
+    __device__ __forceinline__ uint32_t dense_len(uint32_t e, uint32_t K) const {
+        const uint32_t s = (e & 0x7Fu) | ((e >> 8) << 7);
+        const uint32_t j = (static_cast<uint32_t>(buf >> 32) << K) >> (32 - l2e);
+        return reinterpret_cast<const uint8_t*>(l2)[(e & kSsSlow) ? (s << l2e) + j : 0u];
+    }
     template <bool SLOW>
     __device__ __forceinline__ uint32_t step_entry(uint32_t e, uint32_t K, const uint32_t* glut, uint32_t Kg) {
+        if (SLOW && dense) {
+            const uint32_t l1 = dense_len(e, K);
+            const uint32_t len = (e & kSsSlow) ? l1 : (e & 63u);
+            buf <<= len;
+            X -= len;
+            return len;
+        }
         if (SLOW && (e & kSsSlow) && l2 && l2e) {
             if (!nofill) refill();  // >= 32 valid bits: the whole code (<= 32 bits)
             const uint32_t s = (e & 0x7Fu) | ((e >> 8) << 7);
@@ -184,7 +202,15 @@ struct Cursor {
         for (int k = 0; k < kChunkSteps; ++k) {
             if ((k & 1) == 0) refill();
             const uint32_t e = wtab[static_cast<uint32_t>(buf >> 32) >> (32 - K)];
-            if (SLOW && (e & kSsSlow)) {
+            if (SLOW && dense) {
+                const uint32_t l1 = dense_len(e, K);
+                const bool slow = (e & kSsSlow) != 0;
+                const uint32_t u = slow ? l1 : (e >> 8) & 15u;
+                buf <<= u;
+                X -= u;
+                U += u;
+                N += slow ? 1u : e >> 12;
+            } else if (SLOW && (e & kSsSlow)) {
                 U += step_entry<SLOW>(e, K, glut, Kg);
                 N += 1;
             } else {
@@ -281,6 +307,7 @@ __device__ __forceinline__ Staged with_l2(Staged st, const A& a, const uint32_t*
     st.l2 = a.l2_words ? lds + stab_words(a) : nullptr;
     st.l2e = a.l2_words ? a.l2_e : 0u;
     st.nofill = st.l2e && a.max_len <= 16;
+    st.dense = st.nofill && a.l2_dense;
     return st;
 }
 

@@ -260,6 +260,7 @@ static void build_len_l2(const HuffTree& t, DecTables& out) {
     std::vector<uint8_t> b;
     if (uniform) {
         out.l2E = Emax;
+        out.l2dense = slow.size() * 64 > (size_t(1) << K) && !std::getenv("HUFF_L2_SPARSE");  // (A/B: =1 branches)
         b.resize(slow.size() << Emax);
         for (size_t s = 0; s < slow.size(); ++s)
             for (uint32_t j = 0; j < (1u << Emax); ++j) b[(s << Emax) + j] = len_below(slow[s].node, Emax, j);
@@ -291,6 +292,7 @@ Status build_dec_tables(const HuffTree& t, DecTables& out) {
     const auto& nodes = t.nodes();
     out.lut.clear();
     out.l2off = out.l2words = out.l2E = 0;
+    out.l2dense = false;
     if (t.root_is_leaf()) {  // every bit decodes the root letter (comp.rs:506-509)
         out.bits = 1;
         out.maxdepth = 1;
@@ -1141,6 +1143,7 @@ Status indexless_sync(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_bytes,
         a.l2 = static_cast<const uint32_t*>(ctx->d_lut.p) + dt->l2off;
         a.l2_words = dt->l2words;
         a.l2_e = dt->l2E;
+        a.l2_dense = dt->l2dense ? 1u : 0u;
     }
     a.tm = static_cast<uint32_t*>(st.tm.p);
     a.dl = static_cast<int32_t*>(st.dl.p);

@@ -64,6 +64,9 @@ struct DecTables {
     // slow window), indexed by the l2E bits after the first sbits; the slow
     // entries carry s the same way
     uint32_t l2off = 0, l2words = 0, l2E = 0;
+    // the uniform form, and more than 1/64 of the windows slow (a 64-lane
+    // step then nearly always has a slow lane)
+    bool l2dense = false;
 };
 
 // append the multi-symbol table (decode.hip k_decode_ms) to out.lut
