@@ -7,7 +7,8 @@
 //  k_spec : lane i decodes speculatively from its segment to the first
 //           codeword boundary >= (i+1)*S: exit x[i] and symbol count c[i].
 //           The staged form (k_spec_lds, codes <= 32 bits, the default) first
-//           walks a lead-in of up to kLeadBits before its segment and starts
+//           walks a lead-in (kLeadBits; kLeadBitsLong for codes past the
+//           walk table) before its segment and starts
 //           at the first boundary at or past i*S (nearly always the true
 //           one), keeps a sample slot every kSampBits bits, fixes its
 //           workgroup's segments in place and writes per-workgroup counts;
@@ -19,7 +20,8 @@
 //           boundary the paths have merged (exit unchanged, count corrected,
 //           merge point and index shift against the speculative path
 //           recorded), otherwise the new exit is published and the successor
-//           looks again. Staged path: k_fix_list (every workgroup's first
+//           looks again (staged path: lengths from the walk and level-2
+//           tables in LDS). Staged path: k_fix_list (every workgroup's first
 //           segment and the segments the speculative pass listed) then
 //           k_fix_chain (one workgroup following the changed exits, a no-op
 //           when there are none). Otherwise kFixRounds k_fix launches (each a
