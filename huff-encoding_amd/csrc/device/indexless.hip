@@ -420,11 +420,24 @@ constexpr uint32_t kSampNone = 0xFFFFu;
 struct SampWords {
     uint32_t d[kSampStride / 2];
 };
+// 16-B loads at 4-B alignment (a segment's slots start at 20 i bytes): one
+// dwordx4 and one dword per lane instead of five dword loads
+typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 __device__ __forceinline__ SampWords samp_load(const uint16_t* samp, uint64_t i) {
     SampWords w;
     const uint32_t* p = reinterpret_cast<const uint32_t*>(samp + i * kSampStride);
+    constexpr uint32_t kD = kSampStride / 2;
+    uint32_t k = 0;
 #pragma unroll
-    for (uint32_t k = 0; k < kSampStride / 2; ++k) w.d[k] = p[k];
+    for (; k + 4 <= kD; k += 4) {
+        const u32x4_a4 v = *reinterpret_cast<const u32x4_a4*>(p + k);
+        w.d[k] = v.x;
+        w.d[k + 1] = v.y;
+        w.d[k + 2] = v.z;
+        w.d[k + 3] = v.w;
+    }
+#pragma unroll
+    for (; k < kD; ++k) w.d[k] = p[k];
     return w;
 }
 __device__ __forceinline__ uint32_t samp_slot(const SampWords& w, uint32_t k) {
