@@ -440,6 +440,23 @@ __device__ __forceinline__ SampWords samp_load(const uint16_t* samp, uint64_t i)
     for (; k < kD; ++k) w.d[k] = p[k];
     return w;
 }
+__device__ __forceinline__ void samp_store(uint16_t* samp, uint64_t i, const SampWords& w) {
+    uint32_t* p = reinterpret_cast<uint32_t*>(samp + i * kSampStride);
+    constexpr uint32_t kD = kSampStride / 2;
+    uint32_t k = 0;
+#pragma unroll
+    for (; k + 4 <= kD; k += 4)
+        *reinterpret_cast<u32x4_a4*>(p + k) = u32x4_a4{w.d[k], w.d[k + 1], w.d[k + 2], w.d[k + 3]};
+#pragma unroll
+    for (; k < kD; ++k) p[k] = w.d[k];
+}
+// slot k (a run-time index) by selects, so the words stay in registers
+__device__ __forceinline__ uint32_t samp_get(const SampWords& w, uint32_t k) {
+    uint32_t d = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < kSampStride / 2; ++j) d |= w.d[j] & (j == (k >> 1) ? ~0u : 0u);
+    return (d >> (16 * (k & 1))) & 0xFFFFu;
+}
 __device__ __forceinline__ uint32_t samp_slot(const SampWords& w, uint32_t k) {
     return (w.d[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
 }
@@ -546,7 +563,11 @@ __global__ __launch_bounds__(kThreads) void k_spec_lds(IndexlessArgs a) {
     c.init(st, cur);
     // samples: the first chunk end of this path at or after every kSampBits
     // bits past start (the slots above)
-    uint16_t* smp = a.samp + i * kSampStride;
+    // the slots in registers (all "none" until noted), stored at the end as
+    // whole dwords: ten scattered 2-B stores per lane were the alternative
+    SampWords sw;
+#pragma unroll
+    for (uint32_t j = 0; j < kSampStride / 2; ++j) sw.d[j] = 0xFFFFFFFFu;
     uint32_t next_k = 1;
     uint64_t next_bit = (a.nsamp && live) ? start + kSampBits : ~0ull;
     uint64_t last_idx = 0;  // the code index of the last recorded slot (the entry: 0)
@@ -555,7 +576,13 @@ __global__ __launch_bounds__(kThreads) void k_spec_lds(IndexlessArgs a) {
         if (cur >= next_bit) {
             const uint64_t off = cur - next_bit, didx = cnt - last_idx;
             const bool ok = off < 256 && didx < 255;
-            smp[next_k - 1] = static_cast<uint16_t>(ok ? off | (didx << 8) : kSampNone);
+            const uint32_t v16 = ok ? static_cast<uint32_t>(off | (didx << 8)) : kSampNone;
+            const uint32_t k = next_k - 1, sh = 16 * (k & 1);
+#pragma unroll
+            for (uint32_t j = 0; j < kSampStride / 2; ++j) {  // every word written: no indexed access
+                const uint32_t m = j == (k >> 1) ? 0xFFFFu << sh : 0u;
+                sw.d[j] = (sw.d[j] & ~m) | ((v16 << sh) & m);
+            }
             last_idx = ok ? cnt : last_idx;
             next_bit = ++next_k <= a.nsamp ? next_bit + kSampBits : ~0ull;
         }
@@ -605,7 +632,7 @@ __global__ __launch_bounds__(kThreads) void k_spec_lds(IndexlessArgs a) {
     }
     HUFF_STAMP(ws, 3);
     if (live)
-        for (; next_k <= a.nsamp; ++next_k) smp[next_k - 1] = static_cast<uint16_t>(kSampNone);
+        samp_store(a.samp, i, sw);
 
     // fix-up inside the workgroup, on the staged bits: lane i restarts from
     // lane i-1's exit (the first lane's predecessor is in another workgroup:
@@ -639,7 +666,7 @@ __global__ __launch_bounds__(kThreads) void k_spec_lds(IndexlessArgs a) {
         // passed the sample without landing on it: the next recorded one
         auto next_sample = [&]() {
             while (pa > pk) {
-                const uint32_t v = k < a.nsamp ? smp[k] : kSampNone;
+                const uint32_t v = k < a.nsamp ? samp_get(sw, k) : kSampNone;
                 ++k;
                 if (v != kSampNone) {
                     cum += v >> 8;
