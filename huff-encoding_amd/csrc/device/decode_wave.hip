@@ -548,6 +548,8 @@ template <bool SLOW, bool PAD>
 __global__ __launch_bounds__(kThreads) void k_decode_fixed_chk(DecodeArgs a) { decode_fixed_body<SLOW, PAD, true>(a); }
 // index-free streams with k_mark_lite's entries: each lane first decodes and
 // drops its skip codes
+// (forcing 7 or 8 waves per SIMD on the small-stage body spills 20 bytes
+// per lane: not built)
 template <bool SLOW, bool PAD, bool SMALL>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(PAD && !SLOW ? kPadWaves : 1, 8))) void k_decode_fixed_skip(DecodeArgs a) {
     decode_fixed_body<SLOW, PAD, false, true, SMALL>(a);
@@ -595,12 +597,7 @@ hipError_t launch_decode_fixed(const DecodeArgs& a, hipStream_t s) {
         return hipErrorInvalidValue;
     K kern = small ? small_kern
                    : (a.skip_packed ? skip_table[slow][pad] : table[a.check_mode][slow][pad]);
-    // persistent grid = resident workgroups (registers and LDS both limit)
-    int per_cu = 0;
-    hipError_t err = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kThreads, lds);
-    if (err != hipSuccess || per_cu < 1) per_cu = 1;
     const uint64_t want = (ntasks + kWaves - 1) / kWaves;
-    uint64_t cap = uint64_t(a.cu_count ? a.cu_count : 256) * per_cu;
     // production: one task per wave (a one-shot grid, as the byte map's): the
     // dispatcher refills the CUs as waves finish — same-box A/B against the
     // resident persistent grid Zipf 0.506 -> 0.501 ms, text 0.433 -> 0.423,
@@ -612,7 +609,13 @@ hipError_t launch_decode_fixed(const DecodeArgs& a, hipStream_t s) {
 #else
     constexpr bool oneshot = true;
 #endif
-    if (!a.check_mode && oneshot) cap = want;
+    uint64_t cap = want;
+    if (a.check_mode || !oneshot) {  // persistent grid = resident workgroups (registers and LDS both limit)
+        int per_cu = 0;
+        const hipError_t err = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kThreads, lds);
+        if (err != hipSuccess || per_cu < 1) per_cu = 1;
+        cap = uint64_t(a.cu_count ? a.cu_count : 256) * per_cu;
+    }
     const uint32_t grid = static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>(want, cap)));
     hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), lds, s, a);
     return hipGetLastError();
