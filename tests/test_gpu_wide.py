@@ -346,3 +346,27 @@ def test_device_job_large(W, ctx):
     cnt = W.decompress_dev(ctx, t, out.data_ptr(), nb, (8 - want_bits % 8) % 8, dec.data_ptr(), n)
     torch.cuda.synchronize()
     assert cnt == n and torch.equal(dec, x)
+
+
+def test_index_free_dense_slow_windows(W, O, ctx, monkeypatch):
+    """codes of 11-16 bits over 4,096 letters, with ~10 % of the 12-bit walk
+    table's windows slow: the sync kernels' branch-free dense steps (a
+    level-2 length read at every step, no refills), and with HUFF_L2_SPARSE=1
+    the branching steps; both decode the index-free container exactly"""
+    rng = np.random.default_rng(43)
+    k = 4096
+    w = np.where(np.arange(k) < 2048, 8.0, 1.0)
+    letters = rng.choice(k, 400_003, p=w / w.sum()).astype(np.int16)
+    u, c = np.unique(letters, return_counts=True)
+    codes = O.Tree.from_leaves([int(x) for x in u], [int(x) for x in c]).codes(k)
+    lens = [len(s) for s in codes.values()]
+    assert 12 < max(lens) <= 16
+    assert len({s[:12] for s in codes.values() if len(s) > 12}) * 64 > 1 << 12
+    cd = W.compress(letters, ctx)
+    raw = cd.to_bytes()
+    for sparse in (False, True):
+        if sparse:
+            monkeypatch.setenv("HUFF_L2_SPARSE", "1")
+        back_cd = W.WideCompressData.try_from_bytes(raw, np.int16)
+        assert not back_cd.has_index()
+        assert np.array_equal(W.decompress(back_cd, ctx), letters), sparse
