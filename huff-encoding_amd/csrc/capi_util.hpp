@@ -2,6 +2,7 @@
 // extern "C" files (capi.cpp, capi_wide.cpp). Nothing throws across the ABI.
 #pragma once
 
+#include <algorithm>
 #include <cstdint>
 #include <exception>
 #include <new>
@@ -31,37 +32,47 @@ int guarded(F&& f) {
 // HuffLeaf::code of a branch (leaf.rs:70-73): its path from the root, left
 // 0 / right 1 (tree_inner.rs:422-440); the root of a tree with children has
 // none (has_code false), a single-leaf root the code [0] (tree_inner.rs:
-// 310-315). Node needs is_leaf, left, right. false: the branch is not below
-// the root.
+// 310-315). Node needs is_leaf, left, right.
+//
+// parent_links: every node's link to its parent, (parent << 1) | side, -1 for
+// the root and any node not below it; built once per tree (the trees cache
+// it), so a code costs O(depth) instead of a depth-first search per call
+// (visiting every leaf of a large wide tree was O(nodes^2)).
 template <class Node>
-bool branch_path(const std::vector<Node>& nodes, int32_t root, int32_t branch, std::vector<uint8_t>& path,
-                 bool& has_code) {
+std::vector<int32_t> parent_links(const std::vector<Node>& nodes, int32_t root) {
+    std::vector<int32_t> up(nodes.size(), -1);
+    std::vector<int32_t> stack{root};
+    while (!stack.empty()) {
+        const int32_t v = stack.back();
+        stack.pop_back();
+        const Node& n = nodes[v];
+        if (n.is_leaf) continue;
+        up[n.left] = v << 1;
+        up[n.right] = (v << 1) | 1;
+        stack.push_back(n.left);
+        stack.push_back(n.right);
+    }
+    return up;
+}
+// false: the branch is not below the root
+template <class Node>
+bool branch_path(const std::vector<Node>& nodes, const std::vector<int32_t>& up, int32_t root, int32_t branch,
+                 std::vector<uint8_t>& path, bool& has_code) {
     path.clear();
     if (branch == root) {
         has_code = nodes[root].is_leaf;
         if (has_code) path.push_back(0);
         return true;
     }
-    // depth first from the root, left before right, keeping the path
-    std::vector<std::pair<int32_t, uint8_t>> stack{{root, 0}};  // (node, next side)
-    while (!stack.empty()) {
-        auto& top = stack.back();
-        const Node& n = nodes[top.first];
-        if (n.is_leaf || top.second > 1) {
-            stack.pop_back();
-            if (!path.empty()) path.pop_back();
-            continue;
-        }
-        const uint8_t side = top.second++;
-        const int32_t child = side ? n.right : n.left;
-        path.push_back(side);
-        if (child == branch) {
-            has_code = true;
-            return true;
-        }
-        stack.push_back({child, 0});
+    for (int32_t v = branch; v != root;) {
+        const int32_t l = up[v];
+        if (l < 0) return false;
+        path.push_back(static_cast<uint8_t>(l & 1));
+        v = l >> 1;
     }
-    return false;
+    std::reverse(path.begin(), path.end());
+    has_code = true;
+    return true;
 }
 
 }  // namespace huff::capi

@@ -129,7 +129,13 @@ int huff_wbranch_code(const huff_wtree* t, int32_t branch, uint8_t* bits, size_t
     if (!valid_wbranch(t, branch) || !nbits) return fail(HUFF_E_INVALID_ARG, "null argument or no such branch");
     std::vector<uint8_t> path;
     bool has = false;
-    if (!huff::capi::branch_path(t->t.nodes(), t->t.root(), branch, path, has))
+    bool below;
+    {
+        std::lock_guard<std::mutex> g(t->m);
+        if (t->up.empty()) t->up = huff::capi::parent_links(t->t.nodes(), t->t.root());
+        below = huff::capi::branch_path(t->t.nodes(), t->up, t->t.root(), branch, path, has);
+    }
+    if (!below)
         return fail(HUFF_E_INVALID_ARG, "the branch is not below the root");
     if (has_code) *has_code = has ? 1 : 0;
     *nbits = path.size();

@@ -195,6 +195,11 @@ __global__ __launch_bounds__(512) void k_hist1x2(const uint8_t* __restrict__ bas
                                                  unsigned long long* __restrict__ gw) {
     constexpr uint32_t C = 1u << LOGC;
     constexpr int T = 256;               // threads per chunk
+    // the zeroing loop below clears 256 C / 4 words in strides of 2 T, and a
+    // copy's 16-bit half counts up to kChunk / C bytes: both need C >= 8
+    // (HUFF_HIST_LOGC is a build knob; smaller values would miscount silently)
+    static_assert(LOGC >= 3 && LOGC <= 6, "k_hist1x2 needs 8..64 LDS copies (64 KiB of static LDS at most)");
+    static_assert(kChunk / C < 65536, "a copy's 16-bit half counter must not overflow");
     constexpr int NL = kChunk / 16 / T;  // 16-B loads per lane
     if (blockIdx.x == 0)
         for (uint32_t i = threadIdx.x; i < kHistCopies * 256; i += 2 * T) gw[i] = 0;

@@ -30,11 +30,6 @@ constexpr uint32_t kLutPtr = 0x80000000u;
 #define HUFF_PACK_WAVES 8
 #endif
 constexpr uint32_t kPackWaves = HUFF_PACK_WAVES;  // waves per pack workgroup (short codes; long codes: 4)
-// multi-symbol decode entry: up to 3 letters in bits [0, 24), bits used in
-// [24, 29), letter count in [29, 31); kMsSlow: the first code is longer than
-// the table's index bits (decode it with the single-symbol tables)
-constexpr uint32_t kMsMaxBits = 12;
-constexpr uint32_t kMsSlow = 0x80000000u;
 // single-symbol u16 decode entry (k_decode_fixed): code length in bits
 // [0, 6), letter in [8, 16); kSsSlow: the first code is longer than the
 // table's index bits (<= kSsMaxBits)
@@ -151,8 +146,6 @@ struct IndexlessArgs {
     uint64_t* s;                  // [nseg] settled segment starts
     uint64_t* x;                  // [nseg] exits
     uint64_t* c;                  // [nseg] symbol counts
-    const uint32_t* mlut;         // multi-symbol table (codes <= 32 bits: the LDS-staged kernels)
-    uint32_t mlut_bits;
     uint32_t max_len;
     // spec samples (LDS-staged path): segment i's slots at samp + stride i,
     // slot k the first chunk end of its speculative path at or after

@@ -1,5 +1,5 @@
 // segwalk.hpp — lane walks over a workgroup's staged bit range, shared by the
-// index-free decoders (indexless.hip, isplit.hip).
+// index-free decoders (indexless.hip; the round-4 isplit.hip is gone).
 //
 // A workgroup's 256 consecutive segments are one contiguous bit range: it is
 // staged in LDS once with coalesced 16-B loads (plus lookahead for the code

@@ -86,6 +86,8 @@ public:
 
     size_t num_leaves() const;
     uint32_t max_depth() const;
+    // over the leaves (a root leaf counts 1), and the gcd of their depths
+    void depth_range(uint32_t* min_depth, uint32_t* max_depth, uint32_t* gcd = nullptr) const;
     uint64_t root_weight() const { return nodes_[root_].weight; }
     bool root_is_leaf() const { return nodes_[root_].is_leaf; }
     const std::vector<HuffNode>& nodes() const { return nodes_; }

@@ -5,6 +5,7 @@
 // iteration order and the two minima are popped repeatedly
 // (tree_inner.rs:289-303).
 #include <algorithm>
+#include <numeric>
 #include <utility>
 
 #include "huff_coding.hpp"
@@ -151,10 +152,40 @@ size_t HuffTree::num_leaves() const {
     return c;
 }
 
+void HuffTree::depth_range(uint32_t* min_depth, uint32_t* max_depth, uint32_t* gcd) const {
+    // leaf depths without materialising the codes (leaves() allocates a path
+    // per leaf: ~20 us per call, on the host's path between the passes)
+    if (nodes_[root_].is_leaf) {  // tree_inner.rs:313-315: a root leaf's code is "0"
+        *min_depth = *max_depth = 1;
+        if (gcd) *gcd = 1;
+        return;
+    }
+    uint32_t lo = ~0u, hi = 0, g = 0;
+    std::vector<std::pair<int32_t, uint32_t>> st;
+    st.reserve(64);
+    st.push_back({root_, 0});
+    while (!st.empty()) {
+        const auto [n, d] = st.back();
+        st.pop_back();
+        const HuffNode& nd = nodes_[n];
+        if (nd.is_leaf) {
+            lo = std::min(lo, d);
+            hi = std::max(hi, d);
+            g = std::gcd(g, d);
+        } else {
+            st.push_back({nd.right, d + 1});
+            st.push_back({nd.left, d + 1});
+        }
+    }
+    *min_depth = lo;
+    *max_depth = hi;
+    if (gcd) *gcd = g;
+}
+
 uint32_t HuffTree::max_depth() const {
-    uint32_t m = 0;
-    for (const LeafCode& lc : leaves()) m = std::max(m, lc.len);
-    return m;
+    uint32_t lo, hi;
+    depth_range(&lo, &hi);
+    return hi;
 }
 
 std::vector<uint8_t> HuffTree::as_bin() const {

@@ -9,6 +9,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 
 namespace {
 
@@ -111,87 +112,88 @@ Status run_checked_decode(huff_ctx* ctx, dev::DecodeArgs& a, const std::function
                        std::to_string(want));
 }
 
-// multi-symbol table index bits: 12 (16 KiB); 11 and 10 measured slower on
-// Zipf (its 12-bit codes fall to the single-symbol path) and no faster on text
-static uint32_t ms_bits() { return dev::kMsMaxBits; }
+// The decode tables are built once per tree, on the host, between pass 1 and
+// the decode. Each used to walk the tree bit by bit for every one of its 2^K
+// windows (~0.2 ms uniform, ~0.45 ms Zipf on this container's CPU), which at
+// 128 MiB per rank outlasted the pack it hides behind; they are now filled
+// from the tree's top K levels once (O(2^K + nodes)) and the walk table by a
+// recurrence over window prefixes.
 
-void build_multi_table(const HuffTree& t, uint32_t mbits, DecTables& out) {
-    // entry i: walk the tree from the root over the mbits bits of i (MSB
-    // first), restarting at the root after every leaf, up to 3 letters; the
-    // walk is the reference's decompress (comp.rs:487-519) applied to i
+// the top K levels of the tree (K = sbits): entry i of `single` is the first
+// code of the K-bit window i (MSB first) as decompress walks it
+// (comp.rs:487-519): len | letter << 8, or kSsSlow when the window ends on an
+// internal node (listed in `slow` with that node, ascending window order)
+static void top_levels(const HuffTree& t, uint32_t K, uint16_t* single,
+                       std::vector<std::pair<uint32_t, int32_t>>* slow) {
     const auto& nodes = t.nodes();
-    out.mbits = mbits;
-    out.moff = static_cast<uint32_t>(out.lut.size());
-    out.lut.resize(out.lut.size() + (1u << mbits), 0);
-    uint32_t* m = out.lut.data() + out.moff;
-    const bool root_leaf = t.root_is_leaf();
-    for (uint32_t i = 0; i < (1u << mbits); ++i) {
-        uint32_t syms = 0, count = 0, used = 0;
-        int32_t x = t.root();
-        for (uint32_t p = 0; p < mbits && count < 3; ++p) {
-            const uint32_t bit = (i >> (mbits - 1 - p)) & 1u;
-            if (!root_leaf) x = bit ? nodes[x].right : nodes[x].left;
-            if (nodes[x].is_leaf) {  // root-leaf tree: every bit is one letter
-                syms |= static_cast<uint32_t>(nodes[x].letter) << (8 * count);
-                ++count;
-                used = p + 1;
-                x = t.root();
-            }
+    const uint32_t n = 1u << K;
+    if (t.root_is_leaf()) {  // every bit decodes the root letter (comp.rs:506-509)
+        const uint16_t e = static_cast<uint16_t>(1u | (static_cast<uint32_t>(nodes[t.root()].letter) << 8));
+        for (uint32_t i = 0; i < n; ++i) single[i] = e;
+        return;
+    }
+    struct F {
+        int32_t node;
+        uint32_t depth, path;
+    };
+    std::vector<F> st{{t.root(), 0, 0}};
+    while (!st.empty()) {
+        const F f = st.back();
+        st.pop_back();
+        const HuffNode& nd = nodes[f.node];
+        if (f.depth && nd.is_leaf) {
+            const uint16_t e = static_cast<uint16_t>(f.depth | (static_cast<uint32_t>(nd.letter) << 8));
+            const uint32_t lo = f.path << (K - f.depth), hi = (f.path + 1) << (K - f.depth);
+            for (uint32_t i = lo; i < hi; ++i) single[i] = e;
+        } else if (f.depth == K) {
+            single[f.path] = static_cast<uint16_t>(dev::kSsSlow);
+            if (slow) slow->push_back({f.path, f.node});
+        } else {  // right first on the stack: windows come out in ascending order
+            st.push_back({nd.right, f.depth + 1, (f.path << 1) | 1});
+            st.push_back({nd.left, f.depth + 1, f.path << 1});
         }
-        m[i] = count ? (syms | (used << 24) | (count << 29)) : dev::kMsSlow;
     }
 }
 
-// entry i of the single-symbol table: the first code of the sbits-bit window
-// i (MSB first), walked from the root as decompress does (comp.rs:487-519)
-static void build_single_table(const HuffTree& t, uint32_t sbits, DecTables& out) {
-    const auto& nodes = t.nodes();
+// entry i of the single-symbol table: the first code of the sbits-bit window i
+static void build_single_table(const HuffTree& t, uint32_t sbits, DecTables& out,
+                               std::vector<std::pair<uint32_t, int32_t>>* slow = nullptr) {
     const uint32_t n = 1u << sbits;
     out.sbits = sbits;
     out.soff = static_cast<uint32_t>(out.lut.size());
     out.lut.resize(out.lut.size() + (n + 1) / 2, 0);
-    uint16_t* s = reinterpret_cast<uint16_t*>(out.lut.data() + out.soff);
-    for (uint32_t i = 0; i < n; ++i) {
-        uint16_t e = static_cast<uint16_t>(dev::kSsSlow);
-        if (t.root_is_leaf()) {  // every bit decodes the root letter (comp.rs:506-509)
-            e = static_cast<uint16_t>(1u | (static_cast<uint32_t>(nodes[t.root()].letter) << 8));
-        } else {
-            int32_t x = t.root();
-            for (uint32_t p = 0; p < sbits; ++p) {
-                x = ((i >> (sbits - 1 - p)) & 1u) ? nodes[x].right : nodes[x].left;
-                if (nodes[x].is_leaf) {
-                    e = static_cast<uint16_t>((p + 1) | (static_cast<uint32_t>(nodes[x].letter) << 8));
-                    break;
-                }
-            }
-        }
-        s[i] = e;
-    }
+    top_levels(t, sbits, reinterpret_cast<uint16_t*>(out.lut.data() + out.soff), slow);
 }
 
 // entry i of the walk table: every complete code of the sbits-bit window i
-// (bits used, count), for walking a stream without its letters
+// (bits used, count, the first code's length), for walking a stream without
+// its letters. Over the windows' suffixes: the m-bit string v holds its
+// first code (length l <= m, from the single table at v << (K - m)) and then
+// the complete codes of its last m - l bits, so (count, used) of every
+// m-bit string follow from those of shorter ones, m = 1 .. K.
 static void build_walk_table(const HuffTree& t, uint32_t sbits, DecTables& out) {
-    const auto& nodes = t.nodes();
-    const uint32_t n = 1u << sbits;
+    (void)t;
+    const uint32_t K = sbits, n = 1u << K;
     out.woff = static_cast<uint32_t>(out.lut.size());
     out.lut.resize(out.lut.size() + (n + 1) / 2, 0);
+    const uint16_t* single = reinterpret_cast<const uint16_t*>(out.lut.data() + out.soff);
     uint16_t* w = reinterpret_cast<uint16_t*>(out.lut.data() + out.woff);
-    const bool root_leaf = t.root_is_leaf();
-    for (uint32_t i = 0; i < n; ++i) {
-        uint32_t used = 0, count = 0, first = 0;
-        int32_t x = t.root();
-        for (uint32_t p = 0; p < sbits; ++p) {
-            if (!root_leaf) x = ((i >> (sbits - 1 - p)) & 1u) ? nodes[x].right : nodes[x].left;
-            if (nodes[x].is_leaf) {
-                if (!count) first = p + 1;
-                ++count;
-                used = p + 1;
-                x = t.root();
-            }
+    // cu[(1 << m) + v] = count | used << 8 of the m-bit string v
+    std::vector<uint16_t> cu(size_t(2) << K, 0);
+    for (uint32_t m = 1; m <= K; ++m) {
+        uint16_t* row = cu.data() + (size_t(1) << m);
+        for (uint32_t v = 0; v < (1u << m); ++v) {
+            const uint32_t e = single[v << (K - m)];
+            const uint32_t l = e & 63u;
+            if ((e & dev::kSsSlow) || l > m) continue;  // no complete code
+            const uint32_t r = cu[(size_t(1) << (m - l)) + (v & ((1u << (m - l)) - 1))];
+            row[v] = static_cast<uint16_t>(((r & 0xFFu) + 1) | (((r >> 8) + l) << 8));
+            if (m == K)
+                w[v] = static_cast<uint16_t>(l | (((r >> 8) + l) << 8) | (((r & 0xFFu) + 1) << 12));
         }
-        w[i] = count ? static_cast<uint16_t>(first | (used << 8) | (count << 12)) : static_cast<uint16_t>(dev::kSsSlow);
     }
+    for (uint32_t v = 0; v < n; ++v)
+        if ((cu[n + v] & 0xFFu) == 0) w[v] = static_cast<uint16_t>(dev::kSsSlow);
 }
 
 // The sync kernels' level-2 length table (DecTables::l2off): for every
@@ -206,7 +208,8 @@ static void build_walk_table(const HuffTree& t, uint32_t sbits, DecTables& out) 
 // lengths (Emax = the deepest leaf below any of them), so a slow step reads
 // one length at index << Emax | next bits instead of a descriptor and then a
 // length (two dependent LDS reads).
-static void build_len_l2(const HuffTree& t, DecTables& out) {
+static void build_len_l2(const HuffTree& t, const std::vector<std::pair<uint32_t, int32_t>>& slow_nodes,
+                         DecTables& out) {
     constexpr size_t kL2MaxBytes = 24 * 1024;
     constexpr uint32_t kMaxDesc = 1u << 15;
     const uint32_t K = out.sbits;
@@ -220,14 +223,7 @@ static void build_len_l2(const HuffTree& t, DecTables& out) {
     std::vector<Slow> slow;
     uint32_t Emax = 0;
     size_t desc_bytes = 0;
-    for (uint32_t i = 0; i < (1u << K); ++i) {
-        int32_t x = t.root();
-        bool leaf = false;
-        for (uint32_t p = 0; p < K && !leaf; ++p) {
-            x = ((i >> (K - 1 - p)) & 1u) ? nodes[x].right : nodes[x].left;
-            leaf = nodes[x].is_leaf;
-        }
-        if (leaf) continue;
+    for (const auto& [i, x] : slow_nodes) {
         uint32_t E = 0;
         std::vector<std::pair<int32_t, uint32_t>> st{{x, 0}};
         while (!st.empty()) {
@@ -298,18 +294,14 @@ Status build_dec_tables(const HuffTree& t, DecTables& out) {
         out.maxdepth = 1;
         const uint32_t e = (1u << 8) | nodes[t.root()].letter;
         out.lut = {e, e};
-        build_multi_table(t, ms_bits(), out);
         build_single_table(t, 1, out);
         build_walk_table(t, 1, out);
         return Status::ok();
     }
-    const uint32_t maxd = t.max_depth();  // > dev::kLongMaxLen: the deep kernels (deep.hip)
+    uint32_t mind = 0, maxd = 0;  // maxd > dev::kLongMaxLen: the deep kernels (deep.hip)
+    t.depth_range(&mind, &maxd);
     out.maxdepth = maxd;
-    {
-        uint32_t mind = 255;
-        for (const LeafCode& lc : t.leaves()) mind = std::min(mind, lc.len);
-        out.all8 = (mind == 8 && maxd == 8);
-    }
+    out.all8 = (mind == 8 && maxd == 8);
     out.bits = std::min<uint32_t>(maxd, dev::kLutMaxBits - 1);  // 11 bits: 8 KiB of LDS
     if (out.bits < 1) out.bits = 1;
     out.lut.assign(1u << out.bits, 0);
@@ -348,10 +340,10 @@ Status build_dec_tables(const HuffTree& t, DecTables& out) {
             }
         }
     }
-    build_multi_table(t, ms_bits(), out);
-    build_single_table(t, std::min<uint32_t>(maxd, dev::kSsMaxBits), out);
+    std::vector<std::pair<uint32_t, int32_t>> slow;  // the single table's slow windows and their nodes
+    build_single_table(t, std::min<uint32_t>(maxd, dev::kSsMaxBits), out, &slow);
     build_walk_table(t, out.sbits, out);
-    build_len_l2(t, out);
+    build_len_l2(t, slow, out);
     return Status::ok();
 }
 
@@ -539,6 +531,7 @@ huff::Status huff_enc::hist() {
             if (q == hipSuccess && (__atomic_load_n(&hw[b], __ATOMIC_ACQUIRE) >> 48) != done.tag)
                 return huff::Status::err(HUFF_E_HIP, "pass 1 finished without publishing its weights");
             if (q != hipSuccess && q != hipErrorNotReady) HIP_TRY(q);
+            if (spin >= 4095) std::this_thread::yield();  // a long wait: give the core back (as indexless_sync)
         }
     }
     have_hist = true;
@@ -1086,8 +1079,8 @@ Status indexless_sync(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_bytes,
                       const std::function<Status()>& before_wait) {
     const DecTables* dt = st.dt;
     // segment length: a multiple of the gcd of all code lengths
-    uint32_t g = 0;
-    for (const LeafCode& lc : t->t.leaves()) g = std::gcd(g, lc.len);
+    uint32_t g = 0, lo_, hi_;
+    t->t.depth_range(&lo_, &hi_, &g);
     if (g == 0) g = 1;
     // codes <= 32 bits take the LDS-staged kernels, longer codes 2048-bit segments
     // (~992 bits: with the one 8 KiB walk table a workgroup's LDS stays under
@@ -1133,8 +1126,6 @@ Status indexless_sync(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_bytes,
     a.s = static_cast<uint64_t*>(st.s.p);
     a.x = static_cast<uint64_t*>(st.x0.p);
     a.c = static_cast<uint64_t*>(st.c.p);
-    a.mlut = static_cast<const uint32_t*>(ctx->d_lut.p) + dt->moff;
-    a.mlut_bits = dt->mbits;
     a.max_len = dt->maxdepth;
     a.stab = reinterpret_cast<const uint16_t*>(static_cast<const uint32_t*>(ctx->d_lut.p) + dt->soff);
     a.stab_bits = dt->sbits;
@@ -1205,6 +1196,10 @@ Status indexless_sync(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_bytes,
         const uint64_t v = __atomic_load_n(hw, __ATOMIC_ACQUIRE);
         if ((v >> 48) == done.tag) {
             st.total = v & ((1ull << 48) - 1);
+            // a fault in the speculative or fix-up kernels (launched before
+            // the scan) surfaces here, not only at the caller's next sync
+            const hipError_t q = hipStreamQuery(strm);
+            if (q != hipSuccess && q != hipErrorNotReady) HIP_TRY(q);
             if (std::getenv("HUFF_FIX_STATS")) {  // diagnostics: how much the fix-up did (a synchronising copy)
                 unsigned int f[8];
                 HIP_TRY(hipMemcpyAsync(f, st.flag.p, sizeof f, hipMemcpyDeviceToHost, strm));
@@ -1219,6 +1214,10 @@ Status indexless_sync(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_bytes,
             if (q == hipSuccess && (__atomic_load_n(hw, __ATOMIC_ACQUIRE) >> 48) != done.tag)
                 return Status::err(HUFF_E_HIP, "the index-free scan finished without publishing its total");
             if (q != hipSuccess && q != hipErrorNotReady) HIP_TRY(q);
+            // a long wait (a huge stream, or a stream queued behind other
+            // work): stop burning the core; the first ~4 K spins stay hot
+            // (the total normally lands within tens of microseconds)
+            if (spin >= 4095) std::this_thread::yield();
         }
     }
 }
@@ -1327,8 +1326,8 @@ Status decode_indexless_dev(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_
     const bool compact = !check && !d_end;
     auto mark_early = [&]() -> Status {
         if (!d_user || check || d_end || !st.block_off || !dev::indexless_staged(st.a)) return Status::ok();
-        uint32_t min_len = 64;
-        for (const LeafCode& lc : t->t.leaves()) min_len = std::min<uint32_t>(min_len, std::max<uint32_t>(lc.len, 1));
+        uint32_t min_len = 64, max_len_;
+        t->t.depth_range(&min_len, &max_len_);
         const uint64_t most = std::min<uint64_t>(user_cap, valid_bits / min_len);
         const uint64_t runs = (most + 63) >> 6;
         HUFF_TRY(ctx->idx_mark32.ensure(runs * 4 + 8));

@@ -44,9 +44,6 @@ struct DecTables {
     uint32_t bits = 0;
     uint32_t maxdepth = 0;
     bool all8 = false;          // every leaf at depth 8: decode is a byte map
-    // multi-symbol table, appended to `lut` at word `moff`: [1 << mbits]
-    // entries for the top mbits bits of the window (dev::kMs* layout)
-    uint32_t mbits = 0, moff = 0;
     // single-symbol u16 table (decode_wave.hip k_decode_fixed), packed two
     // entries per word at word `soff`: [1 << sbits] entries, used | letter << 8,
     // kSsSlow for windows whose first code is longer than sbits
@@ -69,8 +66,6 @@ struct DecTables {
     bool l2dense = false;
 };
 
-// append the multi-symbol table (decode.hip k_decode_ms) to out.lut
-void build_multi_table(const HuffTree& t, uint32_t mbits, DecTables& out);
 
 // HUFF_DISABLE_FIXED8=1 forces the general kernels even for all-8-bit codes
 bool fixed8_disabled();
@@ -89,6 +84,7 @@ struct huff_tree {
     mutable std::mutex m;
     mutable std::unique_ptr<huff::EncTables> enc;
     mutable std::unique_ptr<huff::DecTables> dec;
+    mutable std::vector<int32_t> up;  // parent links for branch codes (capi_util.hpp parent_links), built once
 
     huff_tree();
     const huff::EncTables& enc_tables() const;

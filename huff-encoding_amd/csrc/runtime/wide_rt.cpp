@@ -396,8 +396,8 @@ Status wdecode_indexless_dev(huff_ctx* ctx, const huff_wtree* t, const uint8_t* 
     bool marked = false;
     auto mark_early = [&]() -> Status {
         if (!skip || !d_out || !st.block_off || !dev::indexless_staged(st.a)) return Status::ok();
-        uint32_t min_len = 64;
-        for (const LeafCode& lc : shape->t.leaves()) min_len = std::min<uint32_t>(min_len, std::max<uint32_t>(lc.len, 1));
+        uint32_t min_len = 64, max_len_;
+        shape->t.depth_range(&min_len, &max_len_);
         const uint64_t runs = (std::min<uint64_t>(cap_letters, valid_bits / min_len) + 63) >> 6;
         HUFF_TRY(sub_abs.ensure(runs * 8 + 8));
         HIP_TRY(dev::launch_indexless_mark_lite(st.a, nullptr, static_cast<const unsigned long long*>(st.woff.p),

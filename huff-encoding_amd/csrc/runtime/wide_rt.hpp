@@ -20,6 +20,7 @@ struct huff_wtree {
     mutable std::unique_ptr<huff::WideEncTables> enc;
     mutable std::unique_ptr<huff::WideDecTables> dec;
     mutable std::unique_ptr<huff_tree> shape;
+    mutable std::vector<int32_t> up;  // parent links for branch codes (capi_util.hpp parent_links), built once
 
     huff_wtree();
     huff::Status enc_tables(const huff::WideEncTables** out) const;

@@ -75,6 +75,22 @@ _PANICS = {_lib.E_EMPTY_WEIGHTS, _lib.E_EMPTY_COMP, _lib.E_PADDING, _lib.E_TREE_
 _CLI = {_lib.E_IO, _lib.E_MISSING_HEADER, _lib.E_INVALID_HEADER, _lib.E_UNRECOGNIZED}
 
 
+def branch_code(fn, h, node: int) -> Optional[str]:
+    """leaf.rs:70-73 through huff_branch_code / huff_wbranch_code: the code as
+    a '0'/'1' string, None for a root with children; a code longer than the
+    first buffer (a deep try_from_bin tree) is read again at its reported size"""
+    cap = 512
+    while True:
+        bits = (C.c_uint8 * cap)()
+        n, has_code = C.c_size_t(), C.c_int()
+        rc = fn(h, node, bits, cap, C.byref(n), C.byref(has_code))
+        if rc == _lib.E_BUFFER_TOO_SMALL and n.value > cap:
+            cap = n.value
+            continue
+        _check(rc)
+        return "".join(str(bits[k]) for k in range(n.value)) if has_code.value else None
+
+
 def _check(rc: int):
     if rc == _lib.HUFF_OK:
         return
@@ -350,10 +366,7 @@ class HuffBranch:
         L = load()
         has, letter, weight = C.c_int(), C.c_uint8(), C.c_uint64()
         _check(L.huff_branch_leaf(self._tree.h, self._node, C.byref(has), C.byref(letter), C.byref(weight)))
-        bits = (C.c_uint8 * 512)()
-        n, has_code = C.c_size_t(), C.c_int()
-        _check(L.huff_branch_code(self._tree.h, self._node, bits, 512, C.byref(n), C.byref(has_code)))
-        code = "".join(str(bits[k]) for k in range(n.value)) if has_code.value else None
+        code = branch_code(L.huff_branch_code, self._tree.h, self._node)
         return HuffLeaf(int(letter.value) if has.value else None, int(weight.value), code)
 
     def left_child(self) -> Optional["HuffBranch"]:

@@ -189,10 +189,9 @@ class WideBranch:
         has, weight = C.c_int(), C.c_uint64()
         raw = (C.c_uint8 * lt.width)()
         _check(L.huff_wbranch_leaf(self._tree.h, self._node, C.byref(has), raw, C.byref(weight)))
-        bits = (C.c_uint8 * 4096)()
-        n, has_code = C.c_size_t(), C.c_int()
-        _check(L.huff_wbranch_code(self._tree.h, self._node, bits, 4096, C.byref(n), C.byref(has_code)))
-        code = "".join(str(bits[k]) for k in range(n.value)) if has_code.value else None
+        from . import branch_code
+
+        code = branch_code(L.huff_wbranch_code, self._tree.h, self._node)
         letter = lt.to_int(bytes(raw)) if has.value else None
         return HuffLeaf(letter, int(weight.value), code)
 

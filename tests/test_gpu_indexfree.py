@@ -243,3 +243,43 @@ def test_indexfree_even_lengths_past_table(H, O, ctx):
     assert (used % 2 == 0).all() and used.max() == 14, used
     roundtrip(H, O, ctx, data)
     roundtrip(H, O, ctx, data[: len(data) // 3 + 7])
+
+
+def test_capacity_below_count(H, O, ctx):
+    """the index-free path starts k_mark_lite before the count is
+    known and sizes the marks by the caller's capacity. A buffer shorter than
+    the decoded count must fail with HUFF_E_BUFFER_TOO_SMALL and the true
+    count, write nothing past its capacity, and leave the context able to
+    decode the same stream again with a large enough buffer."""
+    import ctypes as C
+
+    import torch
+    from huff_coding import _lib
+
+    data = O.gen_zipf(0x5EED0002, (1 << 20) + 4321).tobytes()
+    t = O.Tree.from_weights(O.weights_from_bytes(data))
+    code, ln = t.code_table()
+    host = np.frombuffer(data, np.uint8)
+    comp, bits = O.fast_encode(host, code, ln, threads=8)
+    pad = (8 - bits % 8) % 8
+    tree = H.HuffTree.try_from_bin(t.as_bin())
+    dc = torch.from_numpy(np.concatenate([comp, np.zeros(64, np.uint8)])).cuda()
+    n = len(data)
+    out = torch.full((n + 4096,), 0xAB, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    L = _lib.load()
+    for cap in (n - 1, n // 2, 4096 + 17, 1):
+        got = C.c_size_t()
+        rc = L.huff_dev_decompress(ctx.h, tree.h, C.c_void_p(dc.data_ptr()), comp.size, pad,
+                                   C.c_void_p(out.data_ptr()), cap, C.byref(got))
+        torch.cuda.synchronize()
+        assert rc == _lib.E_BUFFER_TOO_SMALL and got.value == n, (cap, rc, got.value)
+        res = out.cpu().numpy()
+        assert (res[cap:] == 0xAB).all(), f"capacity {cap}: wrote past the buffer"
+    from huff_coding import device as D
+
+    assert D.decompress_dev(ctx, tree, dc.data_ptr(), comp.size, pad, out.data_ptr(), n) == n
+    torch.cuda.synchronize()
+    res = out.cpu().numpy()
+    assert np.array_equal(res[:n], host)
+    assert (res[n:] == 0xAB).all()

@@ -370,3 +370,41 @@ def test_index_free_dense_slow_windows(W, O, ctx, monkeypatch):
         back_cd = W.WideCompressData.try_from_bytes(raw, np.int16)
         assert not back_cd.has_index()
         assert np.array_equal(W.decompress(back_cd, ctx), letters), sparse
+
+
+def test_index_free_capacity_below_count(W, O, ctx):
+    """ADVICE r5, the wide index-free path: a letter capacity below the
+    decoded count fails with HUFF_E_BUFFER_TOO_SMALL and the true count,
+    writes nothing past the capacity, and the same context then decodes the
+    stream with a large enough buffer"""
+    import ctypes as C
+
+    import torch
+    from huff_coding import _lib
+
+    rng = np.random.default_rng(97)
+    letters = zipf_letters(rng, 300_007, np.int16)
+    cd = W.compress(letters, ctx)
+    raw = cd.to_bytes()
+    back_cd = W.WideCompressData.try_from_bytes(raw, np.int16)
+    comp = np.frombuffer(back_cd.comp_bytes(), np.uint8)
+    pad = back_cd.padding_bits()
+    t = back_cd.huff_tree()
+    n = letters.size
+    dc = torch.from_numpy(np.concatenate([comp, np.zeros(64, np.uint8)])).cuda()
+    out = torch.full((n + 2048,), 0x5A5A, dtype=torch.int16, device="cuda")
+    torch.cuda.synchronize()
+    L = _lib.load()
+    for cap in (n - 1, n // 3, 65):
+        got = C.c_size_t()
+        rc = L.huff_dev_wdecompress(ctx.h, t.h, C.c_void_p(dc.data_ptr()), comp.size, pad,
+                                    C.c_void_p(out.data_ptr()), cap, C.byref(got))
+        torch.cuda.synchronize()
+        assert rc == _lib.E_BUFFER_TOO_SMALL and got.value == n, (cap, rc, got.value)
+        res = out.cpu().numpy()
+        assert (res[cap:] == 0x5A5A).all(), f"capacity {cap}: wrote past the buffer"
+    assert W.decompress_dev(ctx, t, dc.data_ptr(), comp.size, pad, out.data_ptr(), n) == n
+    torch.cuda.synchronize()
+    res = out.cpu().numpy()
+    assert np.array_equal(res[:n], letters)
+    assert (res[n:] == 0x5A5A).all()

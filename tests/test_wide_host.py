@@ -133,3 +133,23 @@ def test_container_roundtrip_and_errors(W):
         W.WideCompressData.new(b"", 0, t)
     with pytest.raises(H.HuffPanic):
         W.WideCompressData.new(b"\x00", 8, t)
+
+
+def test_deep_tree_leaf_codes(W):
+    """a try_from_bin tree deeper than the first code buffer (a
+    caterpillar of 5,000 u16 letters: depth 4,999) gives every leaf its full
+    code through HuffBranch::leaf (leaf.rs:70-73), as the reference does,
+    and walking every leaf stays linear (parent links, not a DFS per code)"""
+    import time
+
+    k = 5000
+    bits = "".join("10" + format(i, "016b") for i in range(k - 1)) + "0" + format(k - 1, "016b")
+    t = W.WideTree.try_from_bin(bits, np.uint16)
+    b = t.root()
+    t0 = time.perf_counter()
+    for depth in range(k - 1):
+        leaf = b.left_child().leaf()
+        assert leaf.letter() == depth and leaf.code() == "1" * depth + "0"
+        b = b.right_child()
+    assert b.leaf().letter() == k - 1 and b.leaf().code() == "1" * (k - 1)
+    assert time.perf_counter() - t0 < 30
