@@ -456,6 +456,8 @@ int huff_enc_pack_shards(huff_enc* e, const uint64_t* hists, uint32_t world, uin
         huff::Status st = e->pack(t.get(), base, prev + 8 - np, np, d_out, out_cap, &bits);
         if (bits_out) *bits_out = bits;
         HUFF_TRY(st);
+        const huff::DecTables* dt = nullptr;  // ready for the decode that follows (huff_enc_compress)
+        HUFF_TRY(e->ctx->upload_dec_tables(t.get(), &dt));
         *tree_out = t.release();
         return huff::Status::ok();
     });
@@ -477,6 +479,13 @@ int huff_enc_compress(huff_enc* e, uint8_t* d_out, size_t out_cap, huff_tree** t
         const auto t2 = std::chrono::steady_clock::now();
         uint64_t bits = 0;
         huff::Status st = e->pack(t.get(), 0, nullptr, 0, d_out, out_cap, &bits);
+        // the decode tables of the new tree, built and queued for upload
+        // while pass 2 runs: a decode that follows finds them ready (built
+        // there, they held its launch back ~20-35 us past the pack at 128 MiB)
+        if (st.code == HUFF_OK) {
+            const huff::DecTables* dt = nullptr;
+            HUFF_TRY(e->ctx->upload_dec_tables(t.get(), &dt));
+        }
         if (trace) {
             const auto t3 = std::chrono::steady_clock::now();
             auto us = [](auto a, auto b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
