@@ -391,6 +391,40 @@ constexpr uint32_t kDecodeFixedCheck = 11;
 // host[b] = (tag << 48) | total_b. host == nullptr: the totals stay in gw.
 // a result published straight to pinned host memory: (tag << 48) | value
 // in one 8-byte store (pass 1's weights, a scan's grand total)
+// Index-free decode in one pass (syncdec.hip): tiles of 256 segments, a lane
+// per segment decoding its letters into registers, an in-tile fix-up, a
+// decoupled look-back over the tiles for the output offsets, letters out
+// through LDS windows; k_sync_tail then decodes the letters the lanes could
+// not hold and publishes the count. Byte letters, max_len <= stab_bits <= 12.
+constexpr uint32_t kSyncCap = 128;         // letters per lane in registers
+constexpr uint32_t kSyncWin = 4096;        // output window per wave (bytes)
+constexpr uint32_t kSyncLook = 256;        // staged bytes past a tile's last segment end
+constexpr uint32_t kSyncTicket = 0, kSyncJobs = 1, kSyncErr = 2, kSyncMis = 3;  // ctrl words
+constexpr uint64_t kSyncBad = (1ull << 48) - 1;  // published instead of the count: take the pipeline
+struct SyncDecArgs {
+    const uint8_t* comp;
+    uint64_t comp_bytes;
+    uint64_t valid_bits;
+    uint64_t seg_bits;            // S: a multiple of the code lengths' gcd, lead_bits <= S
+    uint64_t nseg;
+    uint32_t lead_bits;           // a multiple of the gcd
+    uint32_t lead0_bits;          // a tile's first lane's (its entry is the tile's), >= lead_bits
+    const uint16_t* stab;         // single-symbol table (DecTables::soff), 2^stab_bits entries
+    uint32_t stab_bits;
+    uint8_t* out;                 // any alignment; nothing at or past out_cap is written
+    uint64_t out_cap;
+    unsigned long long* tile;     // [ceil(nseg / 256)] tile words, zeroed before the launch
+    unsigned int* ctrl;           // [4] ticket, job count, error, look-back waits; zeroed before the launch
+    unsigned long long* total;    // [1] the letter count (the last tile)
+    uint64_t* jobs;               // [3 * job_cap]: start bit, first letter, letters
+    uint64_t job_cap;
+    unsigned long long* host_total;  // pinned: (tag << 48) | count (kSyncBad: failed), by k_sync_tail
+    uint64_t tag;
+    uint64_t* stamps;             // timing builds (HUFF_STAMPS): 10 words per wave (bitreader.hpp WaveStamps)
+};
+size_t sync_decode_lds_bytes(const SyncDecArgs& a);
+hipError_t launch_sync_decode(const SyncDecArgs& a, hipStream_t s);
+
 struct HistDone {
     unsigned long long* host = nullptr;
     uint64_t tag = 0;  // 16 bits

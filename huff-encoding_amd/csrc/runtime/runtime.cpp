@@ -342,6 +342,12 @@ Status build_dec_tables(const HuffTree& t, DecTables& out) {
     }
     std::vector<std::pair<uint32_t, int32_t>> slow;  // the single table's slow windows and their nodes
     build_single_table(t, std::min<uint32_t>(maxd, dev::kSsMaxBits), out, &slow);
+    if (slow.empty()) {
+        const uint16_t* st = reinterpret_cast<const uint16_t*>(out.lut.data() + out.soff);
+        uint64_t sum = 0;
+        for (uint32_t i = 0; i < (1u << out.sbits); ++i) sum += st[i] & 63u;
+        out.kraft_bits = static_cast<double>(sum) / static_cast<double>(1u << out.sbits);
+    }
     build_walk_table(t, out.sbits, out);
     build_len_l2(t, slow, out);
     return Status::ok();
@@ -1229,6 +1235,113 @@ Status indexless_mark(huff_ctx* ctx, IndexlessSync& st, DevBuf& sub_abs, uint32_
     return Status::ok();
 }
 
+// HUFF_SYNC_DECODE=1: the one-pass index-free decoder (syncdec.hip) where it
+// applies. Opt-in: measured slower than the pipeline (1 GiB
+// Zipf 1.52-1.70 vs 1.04 ms; its look-back waits and variable-length output
+// cost more than the second walk they save); the tests run both.
+static bool sync_decode_enabled() {
+    const char* e = std::getenv("HUFF_SYNC_DECODE");
+    return e && *e == '1';
+}
+
+// The one-pass index-free decoder (syncdec.hip) into the caller's buffer.
+// *done false: it does not apply, or it reported that its tail job list
+// overflowed (pathologically skewed streams): the pipeline decodes instead.
+static Status decode_sync(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_bytes, uint64_t valid_bits,
+                          const huff_tree* t, const DecTables* dt, uint8_t* d_user, size_t user_cap, bool* done,
+                          uint64_t* nsym) {
+    *done = false;
+    if (!sync_decode_enabled() || dt->maxdepth > dt->sbits || dt->sbits < 1 || dt->sbits > 12) return Status::ok();
+    uint32_t g = 0, lo_, hi_;
+    t->t.depth_range(&lo_, &hi_, &g);
+    if (g == 0) g = 1;
+    // segments holding ~0.72 kSyncCap letters at the tree's Kraft mean, at an
+    // odd dword stride (S = 32 mod 64: lanes start on different LDS banks),
+    // a multiple of the gcd of the code lengths (every start in phase)
+    const double target = 0.72 * dev::kSyncCap * dt->kraft_bits;
+    uint64_t kmax = std::max<uint64_t>(1, static_cast<uint64_t>(target) / g);
+    uint64_t S = g * kmax;
+    for (uint64_t k = kmax; k >= 1 && k + 64 >= kmax; --k)
+        if ((g * k) % 64 == 32) {
+            S = g * k;
+            break;
+        }
+    // lead-ins (HUFF_SYNC_LEAD / _LEAD0 for A/B): every lane's, and the
+    // longer one of a tile's first lane
+    auto env_u = [](const char* k, uint32_t d) {
+        const char* e = std::getenv(k);
+        return e && *e ? static_cast<uint32_t>(std::strtoul(e, nullptr, 10)) : d;
+    };
+    const uint32_t lead = std::max<uint32_t>(g, env_u("HUFF_SYNC_LEAD", 96) / g * g);
+    const uint32_t lead0 = std::max<uint32_t>(lead, env_u("HUFF_SYNC_LEAD0", 256) / g * g);
+    S = std::min<uint64_t>(std::max<uint64_t>(S, lead0), 1024 / g * g);
+    const uint64_t nseg = (valid_bits + S - 1) / S;
+    const uint64_t ntiles = (nseg + 255) / 256;
+    if (ntiles > 0x7FFFFFFFull) return Status::ok();
+    HUFF_TRY(ctx->sd_ws.ensure(32 + ntiles * 8));
+    const uint64_t job_cap = nseg / 8 + 1024;
+    HUFF_TRY(ctx->sd_jobs.ensure(job_cap * 24));
+    HUFF_TRY(ctx->pin_total.ensure(8));
+    if (!ctx->pin_total_dev) {
+        std::memset(ctx->pin_total.p, 0, 8);
+        HIP_TRY(hipHostGetDevicePointer(&ctx->pin_total_dev, ctx->pin_total.p, 0));
+    }
+    ctx->total_seq = (ctx->total_seq % 0xFFFF) + 1;
+    uint8_t* ws = static_cast<uint8_t*>(ctx->sd_ws.p);
+    dev::SyncDecArgs a{};
+    a.comp = d_comp;
+    a.comp_bytes = comp_bytes;
+    a.valid_bits = valid_bits;
+    a.seg_bits = S;
+    a.nseg = nseg;
+    a.lead_bits = lead;
+    a.lead0_bits = lead0;
+    a.stab = reinterpret_cast<const uint16_t*>(static_cast<const uint32_t*>(ctx->d_lut.p) + dt->soff);
+    a.stab_bits = dt->sbits;
+    a.out = d_user;
+    a.out_cap = user_cap;
+    a.ctrl = reinterpret_cast<unsigned int*>(ws);
+    a.total = reinterpret_cast<unsigned long long*>(ws + 16);
+    a.tile = reinterpret_cast<unsigned long long*>(ws + 32);
+    a.jobs = static_cast<uint64_t*>(ctx->sd_jobs.p);
+    a.job_cap = job_cap;
+    a.host_total = static_cast<unsigned long long*>(ctx->pin_total_dev);
+    a.tag = ctx->total_seq;
+#ifdef HUFF_STAMPS
+    a.stamps = stamp_region(0);
+#endif
+    HIP_TRY(hipMemsetAsync(ws, 0, 32 + ntiles * 8, ctx->stream));
+    HIP_TRY(dev::launch_sync_decode(a, ctx->stream));
+    HIP_TRY(hipEventRecord(ctx->lut_free, ctx->stream));
+    const uint64_t* hw = static_cast<const uint64_t*>(ctx->pin_total.p);
+    for (uint64_t spin = 0;; ++spin) {
+        const uint64_t v = __atomic_load_n(hw, __ATOMIC_ACQUIRE);
+        if ((v >> 48) == a.tag) {
+            const uint64_t n = v & dev::kSyncBad;
+            if (std::getenv("HUFF_FIX_STATS")) {  // diagnostics: the tail's jobs (a synchronising copy)
+                unsigned int c[4];
+                HIP_TRY(hipMemcpyAsync(c, a.ctrl, sizeof c, hipMemcpyDeviceToHost, ctx->stream));
+                HIP_TRY(hipStreamSynchronize(ctx->stream));
+                std::fprintf(stderr, "huff sync decode: segments %llu of %llu bits, tail jobs %u, look-back waits %u, %s\n",
+                             static_cast<unsigned long long>(nseg), static_cast<unsigned long long>(S), c[dev::kSyncJobs],
+                             c[dev::kSyncMis],
+                             n == dev::kSyncBad ? "fell back to the pipeline" : "done");
+            }
+            if (n == dev::kSyncBad) return Status::ok();  // the pipeline instead
+            *nsym = n;
+            *done = true;
+            return Status::ok();
+        }
+        if ((spin & 1023) == 1023) {
+            const hipError_t q = hipStreamQuery(ctx->stream);
+            if (q == hipSuccess && (__atomic_load_n(hw, __ATOMIC_ACQUIRE) >> 48) != a.tag)
+                return Status::err(HUFF_E_HIP, "the one-pass index-free decode finished without publishing its count");
+            if (q != hipSuccess && q != hipErrorNotReady) HIP_TRY(q);
+            if (spin >= 4095) std::this_thread::yield();
+        }
+    }
+}
+
 Status decode_indexless_dev(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_bytes, uint64_t valid_bits,
                             const huff_tree* t, DevBuf& out, uint64_t* nsym, uint8_t* d_user, size_t user_cap,
                             unsigned long long* d_end) {
@@ -1312,9 +1425,14 @@ Status decode_indexless_dev(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_
         HIP_TRY(hipEventRecord(ctx->lut_free, ctx->stream));
         return Status::ok();
     }
+    const uint32_t check = decode_check_mode();
+    if (d_user && !d_end && !check) {  // one pass (syncdec.hip), when it applies
+        bool done = false;
+        HUFF_TRY(decode_sync(ctx, d_comp, comp_bytes, valid_bits, t, dt, d_user, user_cap, &done, nsym));
+        if (done) return out_ptr(*nsym);  // (a short buffer: nothing past it was written)
+    }
     IndexlessSync& st = ctx->indexless_ws();
     st.dt = dt;
-    const uint32_t check = decode_check_mode();
     // with a caller's buffer, the marks go out before the host waits for the
     // count: sub_abs sized for the most symbols the stream or the buffer can
     // hold (shortest code), k_mark_lite bounded to it (22 us of idle stream

@@ -61,6 +61,10 @@ struct DecTables {
     // slow window), indexed by the l2E bits after the first sbits; the slow
     // entries carry s the same way
     uint32_t l2off = 0, l2words = 0, l2E = 0;
+    // mean code length weighted 2^-len (the Kraft mean: the mean of the
+    // single-symbol table's lengths), the one-pass index-free decoder's guess
+    // of bits per letter when it sizes its segments (syncdec.hip)
+    double kraft_bits = 8.0;
     // the uniform form, and more than 1/64 of the windows slow (a 64-lane
     // step then nearly always has a slow lane)
     bool l2dense = false;
@@ -154,6 +158,7 @@ struct huff_ctx {
     std::shared_ptr<huff::IndexlessSync> idx_ws;
     DevBuf idx_sub_abs;
     DevBuf idx_mark32, idx_task_seg;  // the index-free decode's compact marks (k_mark_lite)
+    DevBuf sd_ws, sd_jobs;            // the one-pass index-free decoder's tile words / control, its tail jobs
     huff::IndexlessSync& indexless_ws();
     // the .hff file path's pinned pieces and device buffers (filepath.cpp),
     // kept across calls: pinning ~0.5 GB per call costs more than the copies

@@ -94,18 +94,26 @@ def index_free_cases(O, rng):
     yield "fibonacci-24", rng.permutation(letters).tobytes()
 
 
+@pytest.fixture(params=["sync", "pipeline"])
+def decoder(request, monkeypatch):
+    """the one-pass decoder (syncdec.hip, the default where it applies) and
+    the pipeline (indexless.hip: HUFF_SYNC_DECODE=0) on the same cases"""
+    monkeypatch.setenv("HUFF_SYNC_DECODE", "1" if request.param == "sync" else "0")
+    return request.param
+
+
 @pytest.fixture(scope="module")
 def cases(O):
     return list(index_free_cases(O, np.random.default_rng(2024)))
 
 
-def test_indexfree_matches_oracle(H, O, ctx, cases):
+def test_indexfree_matches_oracle(H, O, ctx, cases, decoder):
     for name, data in cases:
         roundtrip(H, O, ctx, data)
 
 
 @pytest.mark.parametrize("l2", [True, False], ids=["l2-lds", "l2-global"])
-def test_indexfree_codes_past_table(H, O, ctx, l2, monkeypatch):
+def test_indexfree_codes_past_table(H, O, ctx, l2, monkeypatch, decoder):
     """codes of 13-23 bits: the walks' level-2 length table in LDS, and
     with HUFF_NO_L2=1 the global multi-level table"""
     if not l2:
@@ -115,7 +123,7 @@ def test_indexfree_codes_past_table(H, O, ctx, l2, monkeypatch):
         roundtrip(H, O, ctx, np.minimum(rng.geometric(p, n), 255).astype(np.uint8).tobytes())
 
 
-def test_indexfree_misaligned_output(H, O, ctx, cases):
+def test_indexfree_misaligned_output(H, O, ctx, cases, decoder):
     for name, data in cases[:4]:
         roundtrip(H, O, ctx, data[:1_000_003], misalign=3)
 
@@ -139,7 +147,7 @@ def test_indexfree_equals_check_build(H, O, ctx, monkeypatch):
     assert torch.equal(outs[0], outs[1])
 
 
-def test_indexfree_garbage_payloads(H, O, ctx):
+def test_indexfree_garbage_payloads(H, O, ctx, decoder):
     """random payloads under fixed trees: whatever the bits, the letters and
     the dropped final code match the reference walk"""
     import torch
@@ -162,7 +170,7 @@ def test_indexfree_garbage_payloads(H, O, ctx):
 
 
 @pytest.mark.parametrize("kind", ["zipf", "text"])
-def test_indexfree_full_size_foreign_stream(H, O, ctx, kind, monkeypatch):
+def test_indexfree_full_size_foreign_stream(H, O, ctx, kind, monkeypatch, decoder):
     """BASELINE size: the 1 GiB Zipf (configs[2]) and text streams written on
     the CPU by the oracle's table-driven encoder (no restart index, as the
     reference writes every stream: comp.rs:128-184, 487-519), decoded through
@@ -201,6 +209,7 @@ def test_indexfree_fix_chain(H, O, ctx, monkeypatch, capfd):
     import re
 
     monkeypatch.setenv("HUFF_FIX_STATS", "1")
+    monkeypatch.setenv("HUFF_SYNC_DECODE", "0")  # the pipeline's fix-up kernels
     rng = np.random.default_rng(31)
     chain = 0
     for k, n in ((160, 4_000_001), (40, 3_000_001), (250, 4_000_003), (129, 3_000_017)):
@@ -223,13 +232,21 @@ def test_indexfree_lead_in_phase(H, O, ctx, monkeypatch, capfd):
     rng = np.random.default_rng(37)
     for k in (8, 64):
         data = rng.permutation(np.tile(np.arange(1, k + 1, dtype=np.uint8), 3_000_000 // k)).tobytes()
+        monkeypatch.setenv("HUFF_SYNC_DECODE", "0")
         roundtrip(H, O, ctx, data)
         err = capfd.readouterr().err
         stats = re.findall(r"listed by the speculative pass (\d+), chain fixes (\d+)", err)
         assert stats and all(a == "0" and b == "0" for a, b in stats), err
+        # the one-pass decoder: segments and lead-in in phase too, so no lane
+        # is re-counted (no tail jobs) and it does not fall back
+        monkeypatch.setenv("HUFF_SYNC_DECODE", "1")
+        roundtrip(H, O, ctx, data)
+        err = capfd.readouterr().err
+        stats = re.findall(r"huff sync decode: segments \d+ of \d+ bits, tail jobs (\d+), look-back waits \d+, (.*)", err)
+        assert stats and all(j == "0" and w == "done" for j, w in stats), err
 
 
-def test_indexfree_even_lengths_past_table(H, O, ctx):
+def test_indexfree_even_lengths_past_table(H, O, ctx, decoder):
     """every code an even length, up to 14 bits (past the 12-bit walk table):
     the long lead-in (kLeadBitsLong, kept a multiple of 2), the uniform
     level-2 length table and the refill-free slow steps (codes <= 16 bits)
@@ -245,7 +262,7 @@ def test_indexfree_even_lengths_past_table(H, O, ctx):
     roundtrip(H, O, ctx, data[: len(data) // 3 + 7])
 
 
-def test_capacity_below_count(H, O, ctx):
+def test_capacity_below_count(H, O, ctx, decoder):
     """the index-free path starts k_mark_lite before the count is
     known and sizes the marks by the caller's capacity. A buffer shorter than
     the decoded count must fail with HUFF_E_BUFFER_TOO_SMALL and the true
@@ -269,6 +286,8 @@ def test_capacity_below_count(H, O, ctx):
     torch.cuda.synchronize()
     L = _lib.load()
     for cap in (n - 1, n // 2, 4096 + 17, 1):
+        out.fill_(0xAB)  # (the one-pass decoder writes the letters that fit)
+        torch.cuda.synchronize()
         got = C.c_size_t()
         rc = L.huff_dev_decompress(ctx.h, tree.h, C.c_void_p(dc.data_ptr()), comp.size, pad,
                                    C.c_void_p(out.data_ptr()), cap, C.byref(got))

@@ -35,6 +35,7 @@ PHASES = {
     "k_spec_lds": ["stage", "multi_walk", "exit_walk", "samples+barrier", "fixup"],
     "k_decode_fixed_skip": ["table", "input_stage", "skip_codes", "letters", "transpose", "stores"],
     "k_decode_fixed": ["table", "input_stage", "(skip)", "letters", "transpose", "stores"],
+    "k_sync_decode": ["stage", "lead_in", "letters", "fixup", "look_back", "prefix", "out"],
 }
 
 
@@ -84,6 +85,9 @@ def main():
     ap.add_argument("--bytes", type=int, default=1 << 30)
     ap.add_argument("--seg", type=int, default=992, help="segment bits of the build (runtime.cpp HUFF_SEG_TARGET)")
     ap.add_argument("--walks", type=int, default=1, help="segments per thread of k_spec_lds")
+    ap.add_argument("--sync", type=int, default=0,
+                    help="segment bits of the one-pass decoder (syncdec.hip; HUFF_FIX_STATS prints them): "
+                         "its stamps (region 0) instead of the pipeline's")
     args = ap.parse_args()
     torch.cuda.set_device(0)
     L = C.CDLL(_lib.LIB_PATH)
@@ -116,8 +120,12 @@ def main():
     # segments of the speculative pass: runtime.cpp indexless_sync (args.seg bits for these trees)
     nseg = (bits + args.seg - 1) // args.seg
     per_wg = 256 * args.walks
-    for name, r, waves in (("k_spec_lds", 0, (nseg + per_wg - 1) // per_wg * 4), ("k_decode_fixed_skip", 1, ntasks),
-                           ("k_decode_fixed", 2, ntasks)):
+    kernels = (("k_spec_lds", 0, (nseg + per_wg - 1) // per_wg * 4), ("k_decode_fixed_skip", 1, ntasks),
+               ("k_decode_fixed", 2, ntasks))
+    if args.sync:
+        nseg = (bits + args.sync - 1) // args.sync
+        kernels = (("k_sync_decode", 0, (nseg + 255) // 256 * 4), ("k_decode_fixed", 2, ntasks))
+    for name, r, waves in kernels:
         buf = np.zeros((waves, 10), np.uint64)
         assert L.huff_diag_stamps(r, buf.ctypes.data, buf.size) == 0
         res[name] = summarize(name, buf)
