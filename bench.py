@@ -162,12 +162,19 @@ INDEXFREE_KERNELS = ["k_spec_lds", "k_fix_list", "k_fix_chain", "k_scan_tiles", 
                      "k_decode_fixed_skip"]
 
 
+def traffic_name(kind, fixed8):
+    """the PMC summary's workload name: the general kernels on all-8-bit
+    uniform bytes (the `general` record, HUFF_DISABLE_FIXED8=1) have their own
+    (profiles/traffic_uniform_general*.json, tools/gpu_r6_traffic.sh)"""
+    return f"{kind}_general" if kind == "uniform" and not fixed8 else kind
+
+
 def indexfree_traffic(kind, fixed8):
     """HBM bytes of one index-free decode of the 1 GiB job: the byte map's
     for all-8-bit codes, else the sum over the pipeline's kernels"""
     if fixed8:
         return dominant_traffic(kind, "decode", True, None)
-    path = os.path.join(ROOT, "profiles", f"traffic_{kind}_indexfree.json")
+    path = os.path.join(ROOT, "profiles", f"traffic_{traffic_name(kind, fixed8)}_indexfree.json")
     if not os.path.exists(path):
         return None, None
     t = json.load(open(path))
@@ -180,7 +187,7 @@ def dominant_traffic(kind, phase, fixed8, dec_kernel):
     """HBM bytes per launch of the dominant phase from the committed PMC
     summary of this workload (profiles/traffic_<kind>.json, written by
     tools/make_traffic.py from a rocprofv3 --pmc run of the same kernels)."""
-    path = os.path.join(ROOT, "profiles", f"traffic_{kind}.json")
+    path = os.path.join(ROOT, "profiles", f"traffic_{traffic_name(kind, fixed8)}.json")
     if not os.path.exists(path):
         return None, None
     t = json.load(open(path))
