@@ -14,10 +14,82 @@
 namespace huff {
 
 
+// The merges when no two items of the heap ever weigh the same: then every
+// pop has one possible result whatever the heap's layout, so the sorted
+// leaves and a FIFO of joints (produced in non-decreasing weight) give the
+// tree RustMaxHeap gives, node for node, without its ~500 data-dependent
+// sift loops (~8 of the host's ~10 us between pass 1 and pass 2). Any tie
+// (equal leaves, a joint equal to a leaf or to another joint, the duplicate
+// byte-0 leaf) returns false and the caller takes the heap.
+static bool merge_untied(const uint64_t* weights, size_t n, std::vector<HuffNode>& nodes, int32_t& root) {
+    if (n > 512) return false;
+    {  // equal leaves (common: 1 GiB of uniform bytes has ~4 equal pairs of
+       // counts): out before the sort, through a small open-addressing set
+        uint64_t set[1024];
+        bool used[1024] = {};
+        for (size_t i = 0; i < n; ++i) {
+            uint32_t h = static_cast<uint32_t>((weights[i] * 0x9E3779B97F4A7C15ull) >> 54);
+            while (used[h]) {
+                if (set[h] == weights[i]) return false;
+                h = (h + 1) & 1023u;
+            }
+            used[h] = true;
+            set[h] = weights[i];
+        }
+    }
+    int32_t order[512];
+    for (size_t i = 0; i < n; ++i) order[i] = static_cast<int32_t>(i);
+    std::sort(order, order + n, [&](int32_t a, int32_t b) { return weights[a] < weights[b]; });
+    struct J {
+        uint64_t w;
+        int32_t node;
+    };
+    J joints[512];
+    size_t li = 0, jh = 0, jt = 0;
+    // the lighter of the two queue fronts; false on a tie between them
+    auto take = [&](uint64_t& w, int32_t& node) {
+        const bool hl = li < n, hj = jh < jt;
+        if (hl && hj && weights[order[li]] == joints[jh].w) return false;
+        if (hl && (!hj || weights[order[li]] < joints[jh].w)) {
+            node = order[li];
+            w = weights[order[li++]];
+        } else {
+            node = joints[jh].node;
+            w = joints[jh++].w;
+        }
+        return true;
+    };
+    for (size_t left = n; left > 1; --left) {
+        uint64_t wa, wb;
+        int32_t a, b;
+        if (!take(wa, a) || !take(wb, b)) return false;  // min -> left, next_min -> right
+        const uint64_t jw = wa + wb;
+        if (jt > jh && joints[jt - 1].w == jw) return false;  // two equal joints
+        HuffNode joint;
+        joint.weight = jw;
+        joint.left = a;
+        joint.right = b;
+        nodes.push_back(joint);
+        joints[jt++] = J{jw, static_cast<int32_t>(nodes.size() - 1)};
+    }
+    uint64_t w;
+    if (!take(w, root)) return false;
+    return true;
+}
+
 Status HuffTree::from_leaves(const uint8_t* letters, const uint64_t* weights, size_t n, HuffTree& out) {
     if (n == 0) return Status::err(HUFF_E_EMPTY_WEIGHTS, "provided empty weights");
     out.nodes_.clear();
     out.nodes_.reserve(2 * n);
+    for (size_t i = 0; i < n; ++i) {
+        HuffNode leaf;
+        leaf.is_leaf = true;
+        leaf.letter = letters[i];
+        leaf.weight = weights[i];
+        out.nodes_.push_back(leaf);
+    }
+    if (merge_untied(weights, n, out.nodes_, out.root_)) return Status::ok();
+    out.nodes_.clear();
     RustMaxHeap heap(n + 1);
     for (size_t i = 0; i < n; ++i) {  // branch_heap.rs:52-58
         HuffNode leaf;

@@ -8,7 +8,11 @@
 #include <map>
 #include <string>
 
+#include <random>
+#include <vector>
+
 #include "host/huff_coding.hpp"
+#include "host/rust_heap.hpp"
 
 using namespace huff;
 
@@ -169,10 +173,57 @@ static void shard_plan_matches_single_stream() {
     }
 }
 
+// The untied two-queue fast path in HuffTree::from_leaves must build the very
+// tree the BinaryHeap loop builds (tree.rs:148-170): same node order, same
+// children, same root, on random weight sets with and without ties.
+static void tree_fast_path_matches_heap() {
+    std::mt19937_64 r(7);
+    int bad = 0;
+    for (int it = 0; it < 30000; ++it) {
+        size_t n = 1 + r() % 257;
+        uint8_t l[257];
+        uint64_t w[257];
+        uint64_t range = (it % 3 == 0) ? 20 : (it % 3 == 1) ? 100000 : (1ull << 40);
+        for (size_t i = 0; i < n; ++i) {
+            l[i] = (uint8_t)i;
+            w[i] = 1 + r() % range;
+        }
+        HuffTree a;
+        CHECK(HuffTree::from_leaves(l, w, n, a).code == HUFF_OK);
+        std::vector<HuffNode> nodes;
+        RustMaxHeap heap(n + 1);
+        for (size_t i = 0; i < n; ++i) {
+            HuffNode lf;
+            lf.is_leaf = true;
+            lf.letter = l[i];
+            lf.weight = w[i];
+            nodes.push_back(lf);
+            heap.push({w[i], (int32_t)i});
+        }
+        while (heap.size() > 1) {
+            auto x = heap.pop(), y = heap.pop();
+            HuffNode j;
+            j.weight = x.w + y.w;
+            j.left = x.node;
+            j.right = y.node;
+            nodes.push_back(j);
+            heap.push({j.weight, (int32_t)nodes.size() - 1});
+        }
+        int32_t root = heap.pop().node;
+        bool same = root == a.root() && nodes.size() == a.nodes().size();
+        for (size_t i = 0; same && i < nodes.size(); ++i)
+            same = nodes[i].left == a.nodes()[i].left && nodes[i].right == a.nodes()[i].right &&
+                   nodes[i].weight == a.nodes()[i].weight && nodes[i].is_leaf == a.nodes()[i].is_leaf;
+        if (!same) ++bad;
+    }
+    CHECK(bad == 0);
+}
+
 int main() {
     shard_plan_matches_single_stream();
     tree_normal_init();
     tree_single_branch();
+    tree_fast_path_matches_heap();
     tree_invalid_weights();
     tree_from_bin();
     tree_bits_known_answers();
