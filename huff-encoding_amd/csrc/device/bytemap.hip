@@ -125,14 +125,14 @@ hipError_t launch_index_expand(uint64_t n, const uint64_t* task_base, const uint
     const uint64_t nsub = (n + kIdx - 1) / kIdx;
     if (nsub == 0) return hipSuccess;
     const uint64_t want = (nsub + 255) / 256;
-    hipLaunchKernelGGL(k_index_expand, dim3(static_cast<uint32_t>(want < 4096 ? want : 4096)), dim3(256), 0, s, nsub,
+    launch_k(k_index_expand, dim3(static_cast<uint32_t>(want < 4096 ? want : 4096)), dim3(256), 0, s, nsub,
                        task_base, sub16, chunk_start, sub_bit);
     return hipGetLastError();
 }
 
 hipError_t launch_arith_index(uint64_t n, uint32_t nchunks, uint64_t base_bits, uint64_t* chunk_start,
                               uint32_t* sub_bit, hipStream_t s) {
-    hipLaunchKernelGGL(k_arith_index, dim3(1024), dim3(256), 0, s, n, nchunks, base_bits, chunk_start, sub_bit);
+    launch_k(k_arith_index, dim3(1024), dim3(256), 0, s, n, nchunks, base_bits, chunk_start, sub_bit);
     return hipGetLastError();
 }
 
@@ -142,7 +142,7 @@ hipError_t launch_bytemap(const BytemapArgs& a, hipStream_t s) {
     uint64_t blocks = (nvec + kThreads * kPieces - 1) / (kThreads * kPieces);
     if (blocks < 1) blocks = 1;
     if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_bytemap, dim3(static_cast<uint32_t>(blocks)), dim3(kThreads), 0, s, a);
+    launch_k(k_bytemap, dim3(static_cast<uint32_t>(blocks)), dim3(kThreads), 0, s, a);
     return hipGetLastError();
 }
 

@@ -96,14 +96,14 @@ uint32_t sum_blocks(uint64_t n) {
 
 hipError_t launch_task_sums(const uint8_t* x, uint64_t n, uint64_t* sums, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_task_sums, dim3(sum_blocks(n)), dim3(kThreads), 0, s, x, n, sums);
+    launch_k(k_task_sums, dim3(sum_blocks(n)), dim3(kThreads), 0, s, x, n, sums);
     return hipGetLastError();
 }
 
 hipError_t launch_task_sums_check(const uint8_t* x, uint64_t n, const uint64_t* sums, unsigned int* err,
                                   hipStream_t s) {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_task_sums_check, dim3(sum_blocks(n)), dim3(kThreads), 0, s, x, n, sums, err);
+    launch_k(k_task_sums_check, dim3(sum_blocks(n)), dim3(kThreads), 0, s, x, n, sums, err);
     return hipGetLastError();
 }
 

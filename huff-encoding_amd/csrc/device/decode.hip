@@ -196,7 +196,7 @@ size_t decode_lds_bytes(uint32_t lut_bits) {
 hipError_t launch_decode(const DecodeArgs& a, hipStream_t s) {
     if (a.nchunks == 0) return hipSuccess;
     if (a.max_len <= 32) return a.stab ? launch_decode_fixed(a, s) : hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_decode<true>, dim3(a.nchunks), dim3(kThreads), decode_lds_bytes(a.lut_bits), s, a);
+    launch_k(k_decode<true>, dim3(a.nchunks), dim3(kThreads), decode_lds_bytes(a.lut_bits), s, a);
     return hipGetLastError();
 }
 

@@ -617,7 +617,7 @@ hipError_t launch_decode_fixed(const DecodeArgs& a, hipStream_t s) {
         cap = uint64_t(a.cu_count ? a.cu_count : 256) * per_cu;
     }
     const uint32_t grid = static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>(want, cap)));
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreads), lds, s, a);
+    launch_k(kern, dim3(grid), dim3(kThreads), lds, s, a);
     return hipGetLastError();
 }
 

@@ -173,14 +173,14 @@ __global__ void k_shift_bits(const uint8_t* __restrict__ src, uint8_t* __restric
 }  // namespace
 
 hipError_t launch_walk_end(const WalkEndArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(k_walk_end, dim3(1), dim3(64), (1u << a.lut_bits) * 4, s, a);
+    launch_k(k_walk_end, dim3(1), dim3(64), (1u << a.lut_bits) * 4, s, a);
     return hipGetLastError();
 }
 
 hipError_t launch_shift_bits(const uint8_t* src, uint8_t* dst, uint64_t n, uint32_t r, hipStream_t s) {
     if (n == 0) return hipSuccess;
     const uint64_t want = (n + 255) / 256;
-    hipLaunchKernelGGL(k_shift_bits, dim3(static_cast<uint32_t>(want < 8192 ? want : 8192)), dim3(256), 0, s, src,
+    launch_k(k_shift_bits, dim3(static_cast<uint32_t>(want < 8192 ? want : 8192)), dim3(256), 0, s, src,
                        dst, n, r);
     return hipGetLastError();
 }
@@ -188,7 +188,7 @@ hipError_t launch_shift_bits(const uint8_t* src, uint8_t* dst, uint64_t n, uint3
 hipError_t launch_pack_deep(const DeepPackArgs& a, hipStream_t s) {
     if (a.nchunks == 0) return hipSuccess;
     const uint32_t grid = (a.nchunks + kDeepWaves - 1) / kDeepWaves;
-    hipLaunchKernelGGL(k_pack_deep, dim3(grid < 4096 ? grid : 4096), dim3(kDeepWaves * 64), 0, s, a);
+    launch_k(k_pack_deep, dim3(grid < 4096 ? grid : 4096), dim3(kDeepWaves * 64), 0, s, a);
     return hipGetLastError();
 }
 
@@ -196,13 +196,13 @@ hipError_t launch_decode_deep(const DecodeArgs& a, hipStream_t s) {
     if (a.n == 0) return hipSuccess;
     const uint64_t groups = (a.n + kIdx - 1) / kIdx;
     const uint64_t want = (groups + 255) / 256;
-    hipLaunchKernelGGL(k_decode_deep, dim3(static_cast<uint32_t>(want < 4096 ? want : 4096)), dim3(256),
+    launch_k(k_decode_deep, dim3(static_cast<uint32_t>(want < 4096 ? want : 4096)), dim3(256),
                        (1u << a.lut_bits) * 4, s, a);
     return hipGetLastError();
 }
 
 hipError_t launch_decode_deep_serial(const DeepSerialArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(k_decode_deep_serial, dim3(1), dim3(64), (1u << a.lut_bits) * 4, s, a);
+    launch_k(k_decode_deep_serial, dim3(1), dim3(64), (1u << a.lut_bits) * 4, s, a);
     return hipGetLastError();
 }
 

@@ -463,46 +463,46 @@ hipError_t launch_hist(const uint8_t* base, uint64_t lo, uint64_t hi, uint32_t n
 #define HUFF_HIST_X2 1
 #endif
         if (HUFF_HIST_X2)
-            hipLaunchKernelGGL(k_hist1x2<HUFF_HIST_LOGC>, dim3((nchunks + 1) / 2), dim3(512), 0, s, base, lo, hi, nchunks,
+            launch_k(k_hist1x2<HUFF_HIST_LOGC>, dim3((nchunks + 1) / 2), dim3(512), 0, s, base, lo, hi, nchunks,
                                chunk_hist, gw);
         else
-            hipLaunchKernelGGL(k_hist1<HUFF_HIST_LOGC>, dim3(nchunks), dim3(HUFF_HIST_THREADS), 0, s, base, lo, hi,
+            launch_k(k_hist1<HUFF_HIST_LOGC>, dim3(nchunks), dim3(HUFF_HIST_THREADS), 0, s, base, lo, hi,
                                chunk_hist, gw);
         const uint32_t g = nchunks < 512 ? nchunks : 512;
-        hipLaunchKernelGGL(k_rows_sum, dim3(g), dim3(256), 0, s, chunk_hist, nchunks, gw);
-        if (done.host) hipLaunchKernelGGL(k_hist_publish, dim3(1), dim3(256), 0, s, gw, done.host, done.tag);
+        launch_k(k_rows_sum, dim3(g), dim3(256), 0, s, chunk_hist, nchunks, gw);
+        if (done.host) launch_k(k_hist_publish, dim3(1), dim3(256), 0, s, gw, done.host, done.tag);
         return hipGetLastError();
     }
     uint32_t grid = nchunks < 1024 ? nchunks : 1024;
     const hipError_t e = hipMemsetAsync(gw, 0, kHistCopies * 256 * 8, s);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_hist, dim3(grid), dim3(kThreads), 0, s, base, lo, hi, nchunks, chunk_hist, gw);
+    launch_k(k_hist, dim3(grid), dim3(kThreads), 0, s, base, lo, hi, nchunks, chunk_hist, gw);
     return hipGetLastError();
 }
 
 hipError_t launch_hist_row(const unsigned long long* gw, const uint8_t* in, uint64_t n, long long* row,
                            hipStream_t s) {
-    hipLaunchKernelGGL(k_hist_row, dim3(1), dim3(256), 0, s, gw, in, n, row);
+    launch_k(k_hist_row, dim3(1), dim3(256), 0, s, gw, in, n, row);
     return hipGetLastError();
 }
 
 hipError_t launch_chunk_bits(const uint32_t* chunk_hist, uint32_t nchunks, const CodeLens& len, uint64_t* bits,
                              hipStream_t s) {
     if (nchunks == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_chunk_bits, dim3((nchunks + 3) / 4), dim3(256), 0, s, chunk_hist, nchunks, len, bits);
+    launch_k(k_chunk_bits, dim3((nchunks + 3) / 4), dim3(256), 0, s, chunk_hist, nchunks, len, bits);
     return hipGetLastError();
 }
 
 hipError_t launch_scan(const uint64_t* bits, uint32_t nchunks, uint64_t base, uint64_t* start, uint64_t* tsum,
                        hipStream_t s, HistDone done) {
     const uint32_t tiles = nchunks ? (nchunks + 1023) / 1024 : 1;
-    hipLaunchKernelGGL(k_scan_tiles, dim3(tiles), dim3(1024), 0, s, bits, nchunks, start, tsum);
+    launch_k(k_scan_tiles, dim3(tiles), dim3(1024), 0, s, bits, nchunks, start, tsum);
     if (tiles <= 64) {
-        hipLaunchKernelGGL(k_scan_fix_small, dim3(tiles), dim3(1024), 0, s, nchunks, base, tsum, start, done.host,
+        launch_k(k_scan_fix_small, dim3(tiles), dim3(1024), 0, s, nchunks, base, tsum, start, done.host,
                            done.tag);
     } else {
-        hipLaunchKernelGGL(k_scan_tsum, dim3(1), dim3(1024), 0, s, tiles, tsum);
-        hipLaunchKernelGGL(k_scan_fix, dim3(tiles), dim3(1024), 0, s, nchunks, base, tsum, start, done.host,
+        launch_k(k_scan_tsum, dim3(1), dim3(1024), 0, s, tiles, tsum);
+        launch_k(k_scan_fix, dim3(tiles), dim3(1024), 0, s, nchunks, base, tsum, start, done.host,
                            done.tag);
     }
     return hipGetLastError();
@@ -513,7 +513,7 @@ hipError_t launch_find_first(const uint8_t* in, uint64_t n, const uint8_t* missi
     if (n == 0) return hipSuccess;
     uint64_t blocks = (n + 255) / 256;
     uint32_t grid = blocks < 4096 ? static_cast<uint32_t>(blocks) : 4096;
-    hipLaunchKernelGGL(k_find_first, dim3(grid), dim3(256), 0, s, in, n, missing_mask, pos);
+    launch_k(k_find_first, dim3(grid), dim3(256), 0, s, in, n, missing_mask, pos);
     return hipGetLastError();
 }
 

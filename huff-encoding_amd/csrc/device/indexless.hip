@@ -884,7 +884,7 @@ hipError_t launch_indexless_mark_lite(const IndexlessArgs& a, const uint64_t* of
                                       uint32_t* task_seg) {
     if (a.nseg == 0) return hipSuccess;
     if (!a.samp || !a.rec || (!off && !woff) || (!mark32 != !task_seg)) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_mark_lite, dim3((a.nseg + kThreads - 1) / kThreads), dim3(kThreads), 0, st, a, off, woff,
+    launch_k(k_mark_lite, dim3((a.nseg + kThreads - 1) / kThreads), dim3(kThreads), 0, st, a, off, woff,
                        sub_abs, sub_cap < (~0ull / kIdx) ? sub_cap : (~0ull / kIdx), mark32, task_seg);
     return hipGetLastError();
 }
@@ -907,7 +907,7 @@ hipError_t launch_indexless_mark(const IndexlessArgs& a, const uint64_t* off, ui
     const bool slow = a.max_len > a.stab_bits;
     IndexlessArgs m = a;
     m.wtab = nullptr;  // single steps: the walks stop at exact counts
-    hipLaunchKernelGGL(slow ? k_mark_lds<true> : k_mark_lds<false>, dim3((m.nseg + kThreads - 1) / kThreads),
+    launch_k(slow ? k_mark_lds<true> : k_mark_lds<false>, dim3((m.nseg + kThreads - 1) / kThreads),
                        dim3(kThreads), lds_staged_bytes(m, kThreads), st, m, off, sub_abs, shift);
     return hipGetLastError();
 }
@@ -919,13 +919,13 @@ hipError_t launch_indexless_spec(const IndexlessArgs& a, hipStream_t st) {
     if (use_staged(a)) {
         if (!a.samp || !a.rec) return hipErrorInvalidValue;
         const bool slow = a.max_len > a.stab_bits;
-        hipLaunchKernelGGL(slow ? k_spec_lds<true> : k_spec_lds<false>, dim3((a.nseg + kThreads - 1) / kThreads),
+        launch_k(slow ? k_spec_lds<true> : k_spec_lds<false>, dim3((a.nseg + kThreads - 1) / kThreads),
                            dim3(kThreads), lds_staged_bytes(a, kThreads), st, a);
         return hipGetLastError();
     }
     const Seg g = make_seg(a);
     const size_t lds = (1u << a.lut_bits) * 4;
-    hipLaunchKernelGGL(k_spec, dim3((a.nseg + kThreads - 1) / kThreads), dim3(kThreads), lds, st, g, a.s, a.x,
+    launch_k(k_spec, dim3((a.nseg + kThreads - 1) / kThreads), dim3(kThreads), lds, st, g, a.s, a.x,
                        a.c);
     return hipGetLastError();
 }
@@ -947,21 +947,21 @@ hipError_t launch_indexless_settle_all(const IndexlessArgs& a, hipStream_t st) {
             f = FixTabs{a.wtab ? a.wtab : a.stab, a.l2, a.stab_bits, a.l2_words, a.l2_e};
             flds = std::max<size_t>(lds, (((1u << a.stab_bits) + 1) / 2 + a.l2_words) * 4);
         }
-        hipLaunchKernelGGL(k_fix_list, dim3(std::max<uint32_t>(lgrid, 1)), dim3(kThreads), flds, st, g, R, a.x,
+        launch_k(k_fix_list, dim3(std::max<uint32_t>(lgrid, 1)), dim3(kThreads), flds, st, g, R, a.x,
                            a.flags, a.fixlist, a.chain, f);
-        hipLaunchKernelGGL(k_fix_chain, dim3(1), dim3(kChainThreads), flds, st, g, R, a.x, a.flags, a.chain, f);
+        launch_k(k_fix_chain, dim3(1), dim3(kChainThreads), flds, st, g, R, a.x, a.flags, a.chain, f);
         return hipGetLastError();
     }
     for (int r = 0; r < kFixRounds; ++r)
-        hipLaunchKernelGGL(k_fix, dim3(grid), dim3(kThreads), lds, st, g, a.s, a.x, a.c, a.tm, a.dl, a.flags, r);
-    hipLaunchKernelGGL(k_settle, dim3(1), dim3(64), lds, st, g, a.s, a.x, a.c, a.tm, a.flags);
+        launch_k(k_fix, dim3(grid), dim3(kThreads), lds, st, g, a.s, a.x, a.c, a.tm, a.dl, a.flags, r);
+    launch_k(k_settle, dim3(1), dim3(64), lds, st, g, a.s, a.x, a.c, a.tm, a.flags);
     return hipGetLastError();
 }
 
 hipError_t launch_indexless_counts(const IndexlessArgs& a, hipStream_t st) {
     if (a.nseg == 0) return hipSuccess;
     if (!a.rec || !a.c) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_rec_counts, dim3((a.nseg + kThreads - 1) / kThreads), dim3(kThreads), 0, st, a.rec, a.c,
+    launch_k(k_rec_counts, dim3((a.nseg + kThreads - 1) / kThreads), dim3(kThreads), 0, st, a.rec, a.c,
                        a.nseg);
     return hipGetLastError();
 }
@@ -970,7 +970,7 @@ hipError_t launch_indexless_emit(const IndexlessArgs& a, const uint64_t* off, ui
     if (a.nseg == 0) return hipSuccess;
     const Seg g = make_seg(a);
     const size_t lds = (1u << a.lut_bits) * 4;
-    hipLaunchKernelGGL(k_emit, dim3((a.nseg + kThreads - 1) / kThreads), dim3(kThreads), lds, st, g, a.s, a.c, off,
+    launch_k(k_emit, dim3((a.nseg + kThreads - 1) / kThreads), dim3(kThreads), lds, st, g, a.s, a.c, off,
                        out);
     return hipGetLastError();
 }

@@ -12,10 +12,36 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+#ifdef __HIPCC__
+#include <hip/hip_ext.h>
+#endif
 
 #include <cstdint>
 
 namespace huff::dev {
+
+// Kernel timing without marker packets. huff_ctx::timed() parks its event
+// pair here; every launch inside the timed region carries the events on its
+// own dispatch packet (hipExtLaunchKernelGGL) instead of two hipEventRecord
+// markers around it: the first launch takes the start event, each launch
+// re-records the stop event, so the pair spans the region's kernels. Outside
+// a timed region launch_k is a plain launch.
+struct LaunchEvents {
+    hipEvent_t start = nullptr, stop = nullptr;
+};
+LaunchEvents& launch_events();  // this thread's pair (runtime.cpp)
+#ifdef __HIPCC__
+template <typename F, typename... Args>
+inline void launch_k(F kernel, dim3 grid, dim3 block, uint32_t lds, hipStream_t s, Args... args) {
+    LaunchEvents& e = launch_events();
+    if (e.stop) {
+        hipExtLaunchKernelGGL(kernel, grid, block, lds, s, e.start, e.stop, 0, args...);
+        e.start = nullptr;
+    } else {
+        hipLaunchKernelGGL(kernel, grid, block, lds, s, args...);
+    }
+}
+#endif
 
 constexpr uint32_t kChunk = 65536;      // input bytes (= symbols) per chunk / workgroup
 constexpr uint32_t kRound = 4096;       // bytes per workgroup round (256 lanes x 16 B)

@@ -267,13 +267,13 @@ hipError_t launch_pack(bool long_codes, const PackArgs& a, hipStream_t s) {
     if (a.nchunks == 0) return hipSuccess;
     const size_t lds = pack_lds_bytes(long_codes, a.max_len, a.stage_words);
     if (long_codes) {
-        hipLaunchKernelGGL(k_pack<true>, dim3(a.grid), dim3(pack_waves<true>() * 64), lds, s, a);
+        launch_k(k_pack<true>, dim3(a.grid), dim3(pack_waves<true>() * 64), lds, s, a);
     } else if (a.max_len <= 8) {  // 4 codes per OR pair
-        hipLaunchKernelGGL((k_pack<false, 4>), dim3(a.grid), dim3(pack_waves<false>() * 64), lds, s, a);
+        launch_k((k_pack<false, 4>), dim3(a.grid), dim3(pack_waves<false>() * 64), lds, s, a);
     } else if (a.max_len <= 16) {
-        hipLaunchKernelGGL((k_pack<false, 2>), dim3(a.grid), dim3(pack_waves<false>() * 64), lds, s, a);
+        launch_k((k_pack<false, 2>), dim3(a.grid), dim3(pack_waves<false>() * 64), lds, s, a);
     } else {
-        hipLaunchKernelGGL((k_pack<false, 1>), dim3(a.grid), dim3(pack_waves<false>() * 64), lds, s, a);
+        launch_k((k_pack<false, 1>), dim3(a.grid), dim3(pack_waves<false>() * 64), lds, s, a);
     }
     return hipGetLastError();
 }

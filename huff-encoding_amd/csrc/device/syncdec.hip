@@ -632,8 +632,8 @@ hipError_t launch_sync_decode(const SyncDecArgs& a, hipStream_t s) {
         !a.ctrl || !a.tile || !a.total)
         return hipErrorInvalidValue;
     const uint64_t ntiles = (a.nseg + kThreads - 1) / kThreads;
-    hipLaunchKernelGGL(k_sync_decode, dim3(static_cast<uint32_t>(ntiles)), dim3(kThreads), sync_decode_lds_bytes(a), s, a);
-    hipLaunchKernelGGL(k_sync_tail, dim3(64), dim3(256), 0, s, a);
+    launch_k(k_sync_decode, dim3(static_cast<uint32_t>(ntiles)), dim3(kThreads), sync_decode_lds_bytes(a), s, a);
+    launch_k(k_sync_tail, dim3(64), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 

@@ -99,9 +99,9 @@ hipError_t launch_generate(int kind, uint64_t seed, uint64_t offset, const uint6
                            hipStream_t s) {
     if (n == 0) return hipSuccess;
     const uint32_t grid = 4096;
-    if (kind == 0) hipLaunchKernelGGL(k_gen_uniform, dim3(grid), dim3(256), 0, s, seed, offset, out, n);
-    else if (kind == 1) hipLaunchKernelGGL(k_gen_zipf, dim3(grid), dim3(256), 0, s, seed, offset, cdf, out, n);
-    else if (kind == 2) hipLaunchKernelGGL(k_gen_text, dim3(grid), dim3(256), 0, s, seed, offset, out, n);
+    if (kind == 0) launch_k(k_gen_uniform, dim3(grid), dim3(256), 0, s, seed, offset, out, n);
+    else if (kind == 1) launch_k(k_gen_zipf, dim3(grid), dim3(256), 0, s, seed, offset, cdf, out, n);
+    else if (kind == 2) launch_k(k_gen_text, dim3(grid), dim3(256), 0, s, seed, offset, out, n);
     else return hipErrorInvalidValue;
     return hipGetLastError();
 }
@@ -191,10 +191,10 @@ hipError_t launch_calib(int mode, const uint8_t* src, uint8_t* dst, uint64_t n, 
     auto* q = reinterpret_cast<calib_u32x4*>(dst);
     const uint32_t g4 = static_cast<uint32_t>(std::max<uint64_t>(1, nvec / 1024));
     switch (mode) {
-        case 0: hipLaunchKernelGGL(k_calib_read, dim3(g4), dim3(256), 0, s, p, nvec, sink); break;
-        case 1: hipLaunchKernelGGL(k_calib_read_blk, dim3((nvec + 4095) / 4096), dim3(256), 0, s, p, nvec, sink); break;
-        case 2: hipLaunchKernelGGL(k_calib_copy, dim3(g4), dim3(256), 0, s, p, q, nvec); break;
-        default: hipLaunchKernelGGL(k_calib_copy_blk, dim3((nvec + 1023) / 1024), dim3(256), 0, s, p, q, nvec); break;
+        case 0: launch_k(k_calib_read, dim3(g4), dim3(256), 0, s, p, nvec, sink); break;
+        case 1: launch_k(k_calib_read_blk, dim3((nvec + 4095) / 4096), dim3(256), 0, s, p, nvec, sink); break;
+        case 2: launch_k(k_calib_copy, dim3(g4), dim3(256), 0, s, p, q, nvec); break;
+        default: launch_k(k_calib_copy_blk, dim3((nvec + 1023) / 1024), dim3(256), 0, s, p, q, nvec); break;
     }
     return hipGetLastError();
 }

@@ -263,13 +263,13 @@ __global__ __launch_bounds__(kTreeLanes) void k_tree_batch(TreeBatchArgs a) {
 hipError_t launch_hist_batch(const uint8_t* in, const uint64_t* off, uint32_t nstreams, uint64_t* hist,
                              hipStream_t s) {
     if (nstreams == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_hist_batch, dim3(nstreams), dim3(256), 0, s, in, off, hist);
+    launch_k(k_hist_batch, dim3(nstreams), dim3(256), 0, s, in, off, hist);
     return hipGetLastError();
 }
 
 hipError_t launch_tree_batch(const TreeBatchArgs& a, hipStream_t s) {
     if (a.nstreams == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_tree_batch, dim3((a.nstreams + kTreeLanes - 1) / kTreeLanes), dim3(kTreeLanes), 0, s, a);
+    launch_k(k_tree_batch, dim3((a.nstreams + kTreeLanes - 1) / kTreeLanes), dim3(kTreeLanes), 0, s, a);
     return hipGetLastError();
 }
 

@@ -406,7 +406,7 @@ hipError_t launch_as(const WideDecArgs& a, size_t shared, uint32_t waves, hipStr
     const uint64_t want = (ntasks + waves - 1) / waves;
     const uint64_t cap = uint64_t(a.cu_count ? a.cu_count : 256) * per_cu;
     const uint32_t grid = static_cast<uint32_t>(want < cap ? want : cap);
-    hipLaunchKernelGGL(k, dim3(grid), dim3(waves * 64), lds, s, a);
+    launch_k(k, dim3(grid), dim3(waves * 64), lds, s, a);
     return hipGetLastError();
 }
 

@@ -682,7 +682,7 @@ hipError_t bits_go(const WideArgs& a, hipStream_t s) {
     const size_t lds = wide_lds_bytes(a, false, LDS);
     static const hipError_t attr = allow_lds(k_wbits<W, V, LDS>, 128 * 1024);
     if (attr != hipSuccess) return attr;
-    hipLaunchKernelGGL((k_wbits<W, V, LDS>), dim3(enc_grid(a, lds)), dim3(kEncWaves * 64), lds, s, a);
+    launch_k((k_wbits<W, V, LDS>), dim3(enc_grid(a, lds)), dim3(kEncWaves * 64), lds, s, a);
     return hipGetLastError();
 }
 
@@ -691,7 +691,7 @@ hipError_t pack_go(const WideArgs& a, hipStream_t s) {
     const size_t lds = wide_lds_bytes(a, true, LDS);
     static const hipError_t attr = allow_lds(k_wpack<W, V, LDS, G>, 128 * 1024);
     if (attr != hipSuccess) return attr;
-    hipLaunchKernelGGL((k_wpack<W, V, LDS, G>), dim3(enc_grid(a, lds)), dim3(kEncWaves * 64), lds, s, a);
+    launch_k((k_wpack<W, V, LDS, G>), dim3(enc_grid(a, lds)), dim3(kEncWaves * 64), lds, s, a);
     return hipGetLastError();
 }
 
@@ -732,10 +732,10 @@ void decode_as(const WideDecArgs& a, hipStream_t s) {
     const size_t prim = (size_t(1) << a.lut_bits) * 4;
     const size_t lw = (static_cast<size_t>(a.nleaves) * sizeof(T) + 15) / 16 * 16;
     if (lw <= kLetterLdsMax)
-        hipLaunchKernelGGL((k_wdecode<T, true>), dim3(grid_for(dec_groups_host(a), a.cu_count, prim + lw)), dim3(kThreads),
+        launch_k((k_wdecode<T, true>), dim3(grid_for(dec_groups_host(a), a.cu_count, prim + lw)), dim3(kThreads),
                            prim + lw, s, a);
     else
-        hipLaunchKernelGGL((k_wdecode<T, false>), dim3(grid_for(dec_groups_host(a), a.cu_count, prim)), dim3(kThreads), prim,
+        launch_k((k_wdecode<T, false>), dim3(grid_for(dec_groups_host(a), a.cu_count, prim)), dim3(kThreads), prim,
                            s, a);
 }
 

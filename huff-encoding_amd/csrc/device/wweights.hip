@@ -246,27 +246,27 @@ hipError_t wcount_launch(const WCountArgs& a, hipStream_t st) {
                      a.unbounded ? a.slots : a.slots / 4 * 3};
     switch (a.width) {
         case 1:
-            hipLaunchKernelGGL(k_wcount_direct<1>, dim3(static_cast<uint32_t>((a.n + kDirectPerBlock - 1) / kDirectPerBlock)),
+            launch_k(k_wcount_direct<1>, dim3(static_cast<uint32_t>((a.n + kDirectPerBlock - 1) / kDirectPerBlock)),
                                dim3(kT), 256 * 4, st, a.in, a.n, a.counts);
             break;
         case 2: {
             static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(k_wcount_direct<2>),
                                                                hipFuncAttributeMaxDynamicSharedMemorySize, 32768 * 4);
             if (attr != hipSuccess) return attr;
-            hipLaunchKernelGGL(k_wcount_direct<2>, dim3(static_cast<uint32_t>((a.n + kDirectPerBlock - 1) / kDirectPerBlock)),
+            launch_k(k_wcount_direct<2>, dim3(static_cast<uint32_t>((a.n + kDirectPerBlock - 1) / kDirectPerBlock)),
                                dim3(kT), 32768 * 4, st, a.in, a.n, a.counts);
             break;
         }
         case 4:
-            hipLaunchKernelGGL(k_wcount_hash<4>, dim3(grid_for(a.n, 64, 4096)), dim3(kT), 0, st, a.in, a.n, a.keys_lo,
+            launch_k(k_wcount_hash<4>, dim3(grid_for(a.n, 64, 4096)), dim3(kT), 0, st, a.in, a.n, a.keys_lo,
                                a.counts, tab, a.sent);
             break;
         case 8:
-            hipLaunchKernelGGL(k_wcount_hash<8>, dim3(grid_for(a.n, 64, 4096)), dim3(kT), 0, st, a.in, a.n, a.keys_lo,
+            launch_k(k_wcount_hash<8>, dim3(grid_for(a.n, 64, 4096)), dim3(kT), 0, st, a.in, a.n, a.keys_lo,
                                a.counts, tab, a.sent);
             break;
         case 16:
-            hipLaunchKernelGGL(k_wcount_hash16, dim3(grid_for(a.n, 16, 8192)), dim3(kT), 0, st, a.in, a.n, a.keys_lo,
+            launch_k(k_wcount_hash16, dim3(grid_for(a.n, 16, 8192)), dim3(kT), 0, st, a.in, a.n, a.keys_lo,
                                a.keys_hi, a.state, a.counts, tab);
             break;
         default:
@@ -277,7 +277,7 @@ hipError_t wcount_launch(const WCountArgs& a, hipStream_t st) {
 
 hipError_t wextract_launch(const WCountArgs& a, hipStream_t st) {
     if (a.n == 0 || a.width <= 2) return hipSuccess;
-    hipLaunchKernelGGL(k_wextract, dim3(grid_for(a.slots, 16, 8192)), dim3(kT), 0, st, a.keys_lo,
+    launch_k(k_wextract, dim3(grid_for(a.slots, 16, 8192)), dim3(kT), 0, st, a.keys_lo,
                        a.width == 16 ? a.keys_hi : nullptr, a.counts, a.slots, a.out_lo, a.out_hi, a.out_c, a.nout, a.out_cap);
     return hipGetLastError();
 }

@@ -415,6 +415,11 @@ huff::Status huff_ctx::activate() const {
     return huff::Status::ok();
 }
 
+huff::dev::LaunchEvents& huff::dev::launch_events() {
+    static thread_local LaunchEvents e;
+    return e;
+}
+
 huff::Status huff_ctx::timed(const char* name, const std::function<hipError_t()>& launch) {
     if (!timing) {
         HIP_TRY(launch());
@@ -426,12 +431,33 @@ huff::Status huff_ctx::timed(const char* name, const std::function<hipError_t()>
             e = free_events.back();
             free_events.pop_back();
         } else {
-            HIP_TRY(hipEventCreate(&e));
+            // HUFF_TIME_FENCE=none|device: events without the system-scope
+            // fence on completion (A/B: step time within noise of the
+            // default, profiles/r06/timing)
+            static const unsigned flags = [] {
+                const char* f = std::getenv("HUFF_TIME_FENCE");
+                if (f && !std::strcmp(f, "none")) return unsigned(hipEventDisableSystemFence);
+                if (f && !std::strcmp(f, "device")) return unsigned(hipEventReleaseToDevice);
+                return 0u;
+            }();
+            HIP_TRY(hipEventCreateWithFlags(&e, flags));
         }
     }
-    HIP_TRY(hipEventRecord(ev[0], stream));
-    HIP_TRY(launch());
-    HIP_TRY(hipEventRecord(ev[1], stream));
+    // the region's launches carry the pair themselves (kernels.hpp launch_k);
+    // a region that launched nothing gets two markers, as does HUFF_TIME_MARKERS=1
+    static const bool markers = [] {
+        const char* m = std::getenv("HUFF_TIME_MARKERS");
+        return m && *m == '1';
+    }();
+    auto& le = huff::dev::launch_events();
+    if (markers) HIP_TRY(hipEventRecord(ev[0], stream));
+    else le = {ev[0], ev[1]};
+    const hipError_t err = launch();
+    const bool none = le.start != nullptr;
+    le = {};
+    HIP_TRY(err);
+    if (none && !markers) HIP_TRY(hipEventRecord(ev[0], stream));
+    if (none || markers) HIP_TRY(hipEventRecord(ev[1], stream));
     pending.push_back({name, ev[0], ev[1]});
     return huff::Status::ok();
 }
