@@ -340,28 +340,40 @@ def run_workload(s: Setup, kind: str, n: int, with_cpu: bool, strong: bool = Fal
             state["out"] = torch.empty(state["cap"], dtype=torch.uint8, device="cuda")
             return encode()
 
-    def step():
+    # N=1 weak steps are software-pipelined: the next step's pass 1 is queued
+    # between this step's pack and its decode (huff_enc_hist_launch), so the
+    # host tree build overlaps the decode instead of idling the GPU (~27 us a
+    # step, profiles/r06/pipeline). Every step still runs pass 1, tree, pass 2
+    # and decode over the whole batch.
+    pipe = world == 1 and flush is None and not args.no_pipeline
+
+    def step(more=False):
         tree, bits = encode_grow()
+        if pipe and more:
+            job.hist_launch()
         job.decode(tree, state["out"].data_ptr(), dec.data_ptr())
         return bits, tree
 
-    for _ in range(args.warmup):
-        step()
+    for i in range(args.warmup):
+        step(i + 1 < args.warmup)
     torch.cuda.synchronize()
     if not args.no_verify:
         assert torch.equal(dec[:n], x[:n]), "decode(encode(x)) != x"
 
     # timed region: K steps (weak: back to back; strong: each step alone,
-    # after a 512 MiB rewrite that evicts the Infinity Cache)
-    ctx.set_timing(True)
+    # after a 512 MiB rewrite that evicts the Infinity Cache). The library's
+    # HIP-event kernel timing runs on every --time-every'th step of it (each
+    # event-carrying dispatch leaves ~5 us of idle behind it: profiles/r06/timing)
+    every = max(1, args.time_every)
     ctx.reset_timing()
     bits, tree = 0, None
     if flush is None:
         s.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for _ in range(args.steps):
-            bits, tree = step()
+        for i in range(args.steps):
+            ctx.set_timing(i % every == 0)
+            bits, tree = step(i + 1 < args.steps)
         torch.cuda.synchronize()
         s.barrier()
         elapsed = time.perf_counter() - t0
@@ -372,6 +384,7 @@ def run_workload(s: Setup, kind: str, n: int, with_cpu: bool, strong: bool = Fal
             s.barrier()
             torch.cuda.synchronize()
             t0 = time.perf_counter()
+            ctx.set_timing(i % every == 0)
             bits, tree = step()
             torch.cuda.synchronize()
             s.barrier()
@@ -480,6 +493,8 @@ def run_workload(s: Setup, kind: str, n: int, with_cpu: bool, strong: bool = Fal
                                            "how": "huff_dev_calibrate: 16-B nontemporal stream, best of 5"},
                      "frac_of_copy_ceiling": round(ach / copy_ceil, 4)},
         "kernels": kernels,
+        "kernel_timing_every": every,  # kernels[*].launches: the sampled steps
+        "pipelined": pipe,
         "e2e": {"encode_GBps": round(world * n / (t_enc / args.steps) / 1e9, 1),
                 "decode_GBps": round(world * n / (t_dec / args.steps) / 1e9, 1),
                 "encode_ms": round(t_enc * 1e3 / args.steps, 4), "decode_ms": round(t_dec * 1e3 / args.steps, 4),
@@ -621,6 +636,10 @@ def main():
                     help="N=1: time the .hff file path on a 1 GiB file of this workload")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="N=1: run each step's pass 1 after the previous decode (no overlap of the tree build)")
+    ap.add_argument("--time-every", type=int, default=4,
+                    help="kernel durations (HIP events) sampled on every Nth timed step")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: rehearse the N>1 path with several ranks on one GPU")
     args = ap.parse_args()

@@ -401,7 +401,10 @@ int huff_enc_create(huff_ctx* ctx, const uint8_t* d_in, size_t n, huff_enc** out
 
 void huff_enc_free(huff_enc* e) {
     if (!e) return;
-    if (e->ctx) hipSetDevice(e->ctx->device);
+    if (e->ctx) {
+        hipSetDevice(e->ctx->device);
+        if (e->ctx->hist_pending == e) e->ctx->hist_pending = nullptr;
+    }
     delete e;
 }
 
@@ -412,6 +415,11 @@ int huff_enc_hist(huff_enc* e, uint64_t weights[256]) {
         if (weights) std::memcpy(weights, e->w, sizeof(e->w));
         return huff::Status::ok();
     });
+}
+
+int huff_enc_hist_launch(huff_enc* e) {
+    if (!e) return fail(HUFF_E_INVALID_ARG, "null argument");
+    return guarded([&] { return e->hist_launch(); });
 }
 
 int huff_enc_hist_row(huff_enc* e, int64_t* d_row) {
@@ -457,7 +465,7 @@ int huff_enc_pack_shards(huff_enc* e, const uint64_t* hists, uint32_t world, uin
         if (bits_out) *bits_out = bits;
         HUFF_TRY(st);
         const huff::DecTables* dt = nullptr;  // ready for the decode that follows (huff_enc_compress)
-        HUFF_TRY(e->ctx->upload_dec_tables(t.get(), &dt));
+        HUFF_TRY(e->ctx->upload_dec_tables(t.get(), &dt, true));
         *tree_out = t.release();
         return huff::Status::ok();
     });
@@ -479,18 +487,23 @@ int huff_enc_compress(huff_enc* e, uint8_t* d_out, size_t out_cap, huff_tree** t
         const auto t2 = std::chrono::steady_clock::now();
         uint64_t bits = 0;
         huff::Status st = e->pack(t.get(), 0, nullptr, 0, d_out, out_cap, &bits);
+        const auto tl = std::chrono::steady_clock::now();  // pass 2 launched
         // the decode tables of the new tree, built and queued for upload
         // while pass 2 runs: a decode that follows finds them ready (built
         // there, they held its launch back ~20-35 us past the pack at 128 MiB)
         if (st.code == HUFF_OK) {
             const huff::DecTables* dt = nullptr;
-            HUFF_TRY(e->ctx->upload_dec_tables(t.get(), &dt));
+            HUFF_TRY(e->ctx->upload_dec_tables(t.get(), &dt, true));
         }
         if (trace) {
             const auto t3 = std::chrono::steady_clock::now();
             auto us = [](auto a, auto b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
-            std::fprintf(stderr, "huff_enc_compress host us: hist %.1f tree %.1f pack %.1f\n", us(t0, t1), us(t1, t2),
-                         us(t2, t3));
+            auto ns = [](auto a) {
+                return static_cast<long long>(
+                    std::chrono::duration_cast<std::chrono::nanoseconds>(a.time_since_epoch()).count());
+            };
+            std::fprintf(stderr, "huff_enc_compress host us: hist %.1f tree %.1f pack %.1f at %lld %lld %lld %lld %lld\n",
+                         us(t0, t1), us(t1, t2), us(t2, t3), ns(t0), ns(t1), ns(t2), ns(tl), ns(t3));
         }
         if (bits_out) *bits_out = bits;
         HUFF_TRY(st);

@@ -128,8 +128,8 @@ __global__ __launch_bounds__(T) void k_hist1(const uint8_t* __restrict__ base, u
                                              unsigned long long* __restrict__ gw) {
     constexpr uint32_t C = 1u << LOGC;  // LDS copies of the histogram
     constexpr int NL = kChunk / 16 / T;  // 16-B loads per lane
-    if (blockIdx.x == 0)  // k_rows_sum (next on the stream) accumulates into gw
-        for (uint32_t i = threadIdx.x; i < kHistCopies * 256; i += T) gw[i] = 0;
+    if (blockIdx.x == 0)  // k_rows_sum / k_rows_publish (next on the stream) accumulate into gw
+        for (uint32_t i = threadIdx.x; i < kHistCopies * 256 + 1; i += T) gw[i] = 0;
     __shared__ __attribute__((aligned(16))) uint32_t h[256 * C];
     const uint32_t t = threadIdx.x;
     const uint32_t lane_c = t & (C - 1);
@@ -201,8 +201,8 @@ __global__ __launch_bounds__(512) void k_hist1x2(const uint8_t* __restrict__ bas
     static_assert(LOGC >= 3 && LOGC <= 6, "k_hist1x2 needs 8..64 LDS copies (64 KiB of static LDS at most)");
     static_assert(kChunk / C < 65536, "a copy's 16-bit half counter must not overflow");
     constexpr int NL = kChunk / 16 / T;  // 16-B loads per lane
-    if (blockIdx.x == 0)
-        for (uint32_t i = threadIdx.x; i < kHistCopies * 256; i += 2 * T) gw[i] = 0;
+    if (blockIdx.x == 0)  // the weights and k_rows_publish's ticket (gw[kHistCopies * 256])
+        for (uint32_t i = threadIdx.x; i < kHistCopies * 256 + 1; i += 2 * T) gw[i] = 0;
     __shared__ __attribute__((aligned(16))) uint32_t h[256 * C];
     const uint32_t t = threadIdx.x, tl = t & (T - 1), half = t / T;
     const uint32_t lane_c = t & (C - 1);
@@ -277,6 +277,79 @@ __global__ __launch_bounds__(256) void k_rows_sum(const uint32_t* __restrict__ c
     for (; c < nchunks; c += g) s0 += chunk_hist[static_cast<uint64_t>(c) * 256 + t];
     const uint64_t s = s0 + s1 + s2 + s3;
     if (s) atomicAdd(&gw[(blockIdx.x % kHistCopies) * 256 + t], static_cast<unsigned long long>(s));
+}
+
+// k_rows_sum and k_hist_publish in one launch (pass 1 with a host reader):
+// 16 waves per workgroup, a wave per chunk row at a time (16 B per lane,
+// bins 4l..4l+3) with four rows in flight, the waves summed in LDS and added
+// into gw's XCD copy, then the last workgroup to take a ticket
+// (gw[kHistCopies * 256], zeroed by pass 1's first workgroup) publishes the
+// totals as k_hist_publish does. Few workgroups (<= 128): each pays one
+// agent-scope release (an L2 write-back) before its ticket, and a 1,024-group
+// version spent 26 us there (profiles/r06/pipeline).
+#ifndef HUFF_ROWS_PUBLISH
+#define HUFF_ROWS_PUBLISH 1
+#endif
+#ifndef HUFF_RP_GROUPS
+#define HUFF_RP_GROUPS 128
+#endif
+constexpr uint32_t kRpWaves = 16;
+__global__ __launch_bounds__(kRpWaves * 64) void k_rows_publish(const uint32_t* __restrict__ chunk_hist,
+                                                                uint32_t nchunks, unsigned long long* gw,
+                                                                unsigned long long* host, uint64_t tag) {
+    __shared__ uint64_t part[kRpWaves][256];
+    __shared__ uint32_t last;
+    const uint32_t t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const uint32_t stride = gridDim.x * kRpWaves;
+    const uint4* rows = reinterpret_cast<const uint4*>(chunk_hist) + lane;  // 64 uint4 per row
+    uint64_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+    uint32_t c = blockIdx.x * kRpWaves + wave;
+    for (; c + 3 * stride < nchunks; c += 4 * stride) {
+        uint4 v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = rows[static_cast<uint64_t>(c + k * stride) * 64];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            a0 += v[k].x;
+            a1 += v[k].y;
+            a2 += v[k].z;
+            a3 += v[k].w;
+        }
+    }
+    for (; c < nchunks; c += stride) {
+        const uint4 v = rows[static_cast<uint64_t>(c) * 64];
+        a0 += v.x;
+        a1 += v.y;
+        a2 += v.z;
+        a3 += v.w;
+    }
+    part[wave][4 * lane] = a0;
+    part[wave][4 * lane + 1] = a1;
+    part[wave][4 * lane + 2] = a2;
+    part[wave][4 * lane + 3] = a3;
+    __syncthreads();
+    if (t < 256) {
+        uint64_t s = 0;
+#pragma unroll
+        for (uint32_t w = 0; w < kRpWaves; ++w) s += part[w][t];
+        if (s)
+            __hip_atomic_fetch_add(&gw[(blockIdx.x % kHistCopies) * 256 + t], static_cast<unsigned long long>(s),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();  // every add of this workgroup issued before its ticket
+    if (t == 0) {
+        const unsigned long long k = __hip_atomic_fetch_add(&gw[kHistCopies * 256], 1ull, __ATOMIC_ACQ_REL,
+                                                            __HIP_MEMORY_SCOPE_AGENT);
+        last = k == gridDim.x - 1u;
+    }
+    __syncthreads();
+    if (!last || t >= 256) return;
+    __atomic_thread_fence(__ATOMIC_ACQUIRE);
+    uint64_t tot = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kHistCopies; ++k)
+        tot += __hip_atomic_load(&gw[k * 256 + t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&host[t], (tag << 48) | tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // Pass 1's result straight to pinned host memory: word b = total of bin b
@@ -468,6 +541,14 @@ hipError_t launch_hist(const uint8_t* base, uint64_t lo, uint64_t hi, uint32_t n
         else
             launch_k(k_hist1<HUFF_HIST_LOGC>, dim3(nchunks), dim3(HUFF_HIST_THREADS), 0, s, base, lo, hi,
                                chunk_hist, gw);
+        if (done.host && HUFF_ROWS_PUBLISH) {
+            // >= 4 rows per wave where the job has them, 128 workgroups at most
+            const uint32_t want = (nchunks + 4 * kRpWaves - 1) / (4 * kRpWaves);
+            const uint32_t g = want < HUFF_RP_GROUPS ? want : HUFF_RP_GROUPS;
+            launch_k(k_rows_publish, dim3(g), dim3(kRpWaves * 64), 0, s, chunk_hist, nchunks, gw, done.host,
+                     done.tag);
+            return hipGetLastError();
+        }
         const uint32_t g = nchunks < 512 ? nchunks : 512;
         launch_k(k_rows_sum, dim3(g), dim3(256), 0, s, chunk_hist, nchunks, gw);
         if (done.host) launch_k(k_hist_publish, dim3(1), dim3(256), 0, s, gw, done.host, done.tag);

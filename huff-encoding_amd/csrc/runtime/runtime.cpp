@@ -4,6 +4,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cctype>
+#include <chrono>
 #include <numeric>
 #include <cstdio>
 #include <cstdlib>
@@ -483,9 +484,12 @@ huff::Status huff_ctx::sync() {
     return huff::Status::ok();
 }
 
-huff::Status huff_ctx::upload_dec_tables(const huff_tree* t, const huff::DecTables** dt) {
+huff::Status huff_ctx::upload_dec_tables(const huff_tree* t, const huff::DecTables** dt, bool for_decode) {
     HUFF_TRY(t->dec_tables(dt));
     if (lut_tree_id == t->id) return huff::Status::ok();
+    // no copy and no cross-stream wait in front of a byte-map decode (~5 us
+    // of idle before it on the headline step)
+    if (for_decode && (*dt)->all8 && !huff::fixed8_disabled()) return huff::Status::ok();
     const size_t bytes = (*dt)->lut.size() * 4;
     HUFF_TRY(pin_lut.ensure(bytes));  // waits until the previous upload has left it
     std::memcpy(pin_lut.p, (*dt)->lut.data(), bytes);
@@ -516,7 +520,7 @@ huff::Status huff_enc::init(huff_ctx* c, const uint8_t* d, uint64_t nbytes) {
     have_hist = packed = sums_valid = false;
     const size_t nc = std::max<uint32_t>(nchunks, 1);
     HUFF_TRY(chunk_hist.ensure(nc * 256 * 4));
-    HUFF_TRY(gw.ensure(huff::dev::kHistCopies * 256 * 8));
+    HUFF_TRY(gw.ensure(huff::dev::kHistCopies * 256 * 8 + 8));  // + k_rows_publish's ticket
 
     HUFF_TRY(chunk_bits.ensure(nc * 8));
     HUFF_TRY(chunk_start.ensure((nc + 1) * 8));
@@ -527,15 +531,30 @@ huff::Status huff_enc::init(huff_ctx* c, const uint8_t* d, uint64_t nbytes) {
     return huff::Status::ok();
 }
 
-huff::Status huff_enc::hist() {
-    HUFF_TRY(ctx->activate());
-    hipStream_t s = ctx->stream;
-    if (nchunks == 0) {
-        for (int b = 0; b < 256; ++b) w[b] = 0;
-        have_hist = true;
-        packed = false;
-        return huff::Status::ok();
+// Host waits on a tagged pinned word (pass 1's weights, the index-free
+// totals). hipStreamQuery on a stream whose work is still running queues a
+// marker behind that work, which left ~6 us of idle in front of the next
+// kernel (profiles/r06/pipeline). The liveness check (did the stream end
+// without publishing? did a kernel fault?) therefore runs only once a wait
+// has outlasted 2 ms, then once a millisecond, yielding the core between.
+class SpinWait {
+public:
+    bool check_due() {
+        if ((++spin_ & 255) != 0) return false;
+        const auto now = std::chrono::steady_clock::now();
+        if (now - t0_ < std::chrono::milliseconds(2)) return false;
+        std::this_thread::yield();
+        if (now - last_ < std::chrono::milliseconds(1)) return false;
+        last_ = now;
+        return true;
     }
+
+private:
+    std::chrono::steady_clock::time_point t0_ = std::chrono::steady_clock::now(), last_{};
+    uint64_t spin_ = 0;
+};
+
+huff::Status huff_enc::launch_publish(uint64_t* tag) {
     HUFF_TRY(ctx->pin_w.ensure(256 * 8));
     if (!ctx->pin_w_dev) {
         std::memset(ctx->pin_w.p, 0, 256 * 8);
@@ -545,27 +564,72 @@ huff::Status huff_enc::hist() {
     done.host = static_cast<unsigned long long*>(ctx->pin_w_dev);
     ctx->hist_seq = (ctx->hist_seq % 0xFFFF) + 1;  // 1..65535: never the zeroed buffer's tag
     done.tag = ctx->hist_seq;
-    const uint64_t* hw = static_cast<const uint64_t*>(ctx->pin_w.p);
     HUFF_TRY(ctx->timed("hist", [&] {
         return huff::dev::launch_hist(d_in, 0, n, nchunks, static_cast<uint32_t*>(chunk_hist.p),
-                                      static_cast<unsigned long long*>(gw.p), s, done);
+                                      static_cast<unsigned long long*>(gw.p), ctx->stream, done);
     }));
+    *tag = done.tag;
+    return huff::Status::ok();
+}
+
+huff::Status huff_enc::wait_weights(uint64_t tag) {
     // every word carries the launch's tag once written (k_hist_publish)
+    const uint64_t* hw = static_cast<const uint64_t*>(ctx->pin_w.p);
+    hipStream_t s = ctx->stream;
     int b = 0;
-    for (uint64_t spin = 0; b < 256; ++spin) {
+    SpinWait sw;
+    while (b < 256) {
         const uint64_t v = __atomic_load_n(&hw[b], __ATOMIC_ACQUIRE);
-        if ((v >> 48) == done.tag) {
+        if ((v >> 48) == tag) {
             w[b++] = v & ((1ull << 48) - 1);
             continue;
         }
-        if ((spin & 1023) == 1023) {
+        if (sw.check_due()) {
             const hipError_t q = hipStreamQuery(s);
-            if (q == hipSuccess && (__atomic_load_n(&hw[b], __ATOMIC_ACQUIRE) >> 48) != done.tag)
+            if (q == hipSuccess && (__atomic_load_n(&hw[b], __ATOMIC_ACQUIRE) >> 48) != tag)
                 return huff::Status::err(HUFF_E_HIP, "pass 1 finished without publishing its weights");
             if (q != hipSuccess && q != hipErrorNotReady) HIP_TRY(q);
-            if (spin >= 4095) std::this_thread::yield();  // a long wait: give the core back (as indexless_sync)
         }
     }
+    return huff::Status::ok();
+}
+
+// the context's pinned weights word serves one pending pass 1 at a time
+static huff::Status pending_guard(const huff_ctx* ctx, const huff_enc* e) {
+    if (ctx->hist_pending && ctx->hist_pending != e)
+        return huff::Status::err(HUFF_E_STATE, "another job's pass 1 is pending on this context (huff_enc_hist_launch): "
+                                               "compress or hist that job first");
+    return huff::Status::ok();
+}
+
+huff::Status huff_enc::hist_launch() {
+    HUFF_TRY(ctx->activate());
+    HUFF_TRY(pending_guard(ctx, this));
+    if (nchunks == 0 || ctx->hist_pending == this) return huff::Status::ok();
+    uint64_t tag = 0;
+    HUFF_TRY(launch_publish(&tag));
+    ctx->hist_pending = this;
+    ctx->hist_pending_tag = tag;
+    return huff::Status::ok();
+}
+
+huff::Status huff_enc::hist() {
+    HUFF_TRY(ctx->activate());
+    HUFF_TRY(pending_guard(ctx, this));
+    if (nchunks == 0) {
+        for (int b = 0; b < 256; ++b) w[b] = 0;
+        have_hist = true;
+        packed = false;
+        return huff::Status::ok();
+    }
+    uint64_t tag = 0;
+    if (ctx->hist_pending == this) {  // queued ahead: only the wait is left
+        tag = ctx->hist_pending_tag;
+        ctx->hist_pending = nullptr;
+    } else {
+        HUFF_TRY(launch_publish(&tag));
+    }
+    HUFF_TRY(wait_weights(tag));
     have_hist = true;
     packed = false;
     return huff::Status::ok();
@@ -573,6 +637,7 @@ huff::Status huff_enc::hist() {
 
 huff::Status huff_enc::hist_known(const uint64_t counts[256]) {
     HUFF_TRY(ctx->activate());
+    if (ctx->hist_pending == this) ctx->hist_pending = nullptr;  // its weights are not wanted now
     std::memcpy(w, counts, sizeof w);
     have_hist = true;
     packed = false;
@@ -585,6 +650,7 @@ huff::Status huff_enc::hist_known(const uint64_t counts[256]) {
 
 huff::Status huff_enc::hist_row(long long* d_row) {
     HUFF_TRY(ctx->activate());
+    if (ctx->hist_pending == this) ctx->hist_pending = nullptr;
     hipStream_t s = ctx->stream;
     have_hist = packed = sums_valid = false;
     if (nchunks == 0) {
@@ -811,7 +877,7 @@ huff::Status huff_enc::decode(const huff_tree* t, const uint8_t* d_comp, uint64_
         return huff::Status::err(HUFF_E_INVALID_ARG, "compressed stream must be 4-byte aligned");
     HUFF_TRY(ctx->activate());
     const huff::DecTables* dt = nullptr;
-    HUFF_TRY(ctx->upload_dec_tables(t, &dt));
+    HUFF_TRY(t->dec_tables(&dt));
     if (dt->all8 && (bit_base & 7) == 0 && !huff::fixed8_disabled()) {  // inverse byte substitution
         huff::dev::BytemapArgs m{};
         m.src = d_comp;
@@ -821,6 +887,7 @@ huff::Status huff_enc::decode(const huff_tree* t, const uint8_t* d_comp, uint64_
         HUFF_TRY(ctx->timed("decode", [&] { return huff::dev::launch_bytemap(m, ctx->stream); }));
         return check_sums(d_out);
     }
+    HUFF_TRY(ctx->upload_dec_tables(t, &dt));
     HUFF_TRY(ensure_index());
     huff::dev::DecodeArgs a{};
     if (dt->maxdepth > huff::dev::kLongMaxLen) {  // deep codes (deep.hip)
@@ -1224,14 +1291,13 @@ Status indexless_sync(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_bytes,
     }
     if (before_wait) HUFF_TRY(before_wait());
     const uint64_t* hw = static_cast<const uint64_t*>(ctx->pin_total.p);
-    for (uint64_t spin = 0;; ++spin) {
+    SpinWait sw;
+    for (;;) {
         const uint64_t v = __atomic_load_n(hw, __ATOMIC_ACQUIRE);
         if ((v >> 48) == done.tag) {
+            // (a fault in the kernels before the scan stops the stream before
+            // the scan publishes: the wait's liveness check reports it)
             st.total = v & ((1ull << 48) - 1);
-            // a fault in the speculative or fix-up kernels (launched before
-            // the scan) surfaces here, not only at the caller's next sync
-            const hipError_t q = hipStreamQuery(strm);
-            if (q != hipSuccess && q != hipErrorNotReady) HIP_TRY(q);
             if (std::getenv("HUFF_FIX_STATS")) {  // diagnostics: how much the fix-up did (a synchronising copy)
                 unsigned int f[8];
                 HIP_TRY(hipMemcpyAsync(f, st.flag.p, sizeof f, hipMemcpyDeviceToHost, strm));
@@ -1241,15 +1307,11 @@ Status indexless_sync(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_bytes,
             }
             return Status::ok();
         }
-        if ((spin & 1023) == 1023) {
+        if (sw.check_due()) {
             const hipError_t q = hipStreamQuery(strm);
             if (q == hipSuccess && (__atomic_load_n(hw, __ATOMIC_ACQUIRE) >> 48) != done.tag)
                 return Status::err(HUFF_E_HIP, "the index-free scan finished without publishing its total");
             if (q != hipSuccess && q != hipErrorNotReady) HIP_TRY(q);
-            // a long wait (a huge stream, or a stream queued behind other
-            // work): stop burning the core; the first ~4 K spins stay hot
-            // (the total normally lands within tens of microseconds)
-            if (spin >= 4095) std::this_thread::yield();
         }
     }
 }
@@ -1340,7 +1402,8 @@ static Status decode_sync(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_by
     HIP_TRY(dev::launch_sync_decode(a, ctx->stream));
     HIP_TRY(hipEventRecord(ctx->lut_free, ctx->stream));
     const uint64_t* hw = static_cast<const uint64_t*>(ctx->pin_total.p);
-    for (uint64_t spin = 0;; ++spin) {
+    SpinWait sw;
+    for (;;) {
         const uint64_t v = __atomic_load_n(hw, __ATOMIC_ACQUIRE);
         if ((v >> 48) == a.tag) {
             const uint64_t n = v & dev::kSyncBad;
@@ -1358,12 +1421,11 @@ static Status decode_sync(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_by
             *done = true;
             return Status::ok();
         }
-        if ((spin & 1023) == 1023) {
+        if (sw.check_due()) {
             const hipError_t q = hipStreamQuery(ctx->stream);
             if (q == hipSuccess && (__atomic_load_n(hw, __ATOMIC_ACQUIRE) >> 48) != a.tag)
                 return Status::err(HUFF_E_HIP, "the one-pass index-free decode finished without publishing its count");
             if (q != hipSuccess && q != hipErrorNotReady) HIP_TRY(q);
-            if (spin >= 4095) std::this_thread::yield();
         }
     }
 }

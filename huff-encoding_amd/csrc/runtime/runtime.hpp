@@ -144,6 +144,10 @@ struct huff_ctx {
     PinnedBuf pin_w;     // weights readback: 256 tagged totals written by pass 1
     void* pin_w_dev = nullptr;
     uint64_t hist_seq = 0;
+    // a pass 1 queued ahead by huff_enc_hist_launch, not yet waited for: its
+    // job and tag (one at a time, as pin_w is the context's)
+    const huff_enc* hist_pending = nullptr;
+    uint64_t hist_pending_tag = 0;
     PinnedBuf pin_total;  // the index-free decode's symbol count, tagged, written by its scan
     void* pin_total_dev = nullptr;
     uint64_t total_seq = 0;
@@ -181,7 +185,10 @@ struct huff_ctx {
     huff::Status collect_timing();
 
     huff::Status activate() const;
-    huff::Status upload_dec_tables(const huff_tree* t, const huff::DecTables** dt);
+    // the tree's decode tables, built on the host and queued for upload;
+    // for_decode: the upload is skipped when decode() will take the byte-map
+    // path, which carries its map in the kernel arguments
+    huff::Status upload_dec_tables(const huff_tree* t, const huff::DecTables** dt, bool for_decode = false);
     huff::Status sync();
 };
 
@@ -224,6 +231,11 @@ struct huff_enc {
 
     huff::Status init(huff_ctx* c, const uint8_t* d, uint64_t nbytes);
     huff::Status hist();
+    // pass 1 queued on the stream, its weights waited for by the next hist()
+    // (huff_enc_hist_launch)
+    huff::Status hist_launch();
+    huff::Status launch_publish(uint64_t* tag);
+    huff::Status wait_weights(uint64_t tag);
     // pass 1 when the counts are already known (the file path's second pass):
     // the per-chunk rows only, no host wait
     huff::Status hist_known(const uint64_t counts[256]);

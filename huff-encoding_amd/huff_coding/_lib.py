@@ -95,6 +95,7 @@ SIGNATURES = [
     ("huff_enc_free", None, [vp]),
     ("huff_enc_hist", i, [vp, vp]),
     ("huff_enc_hist_row", i, [vp, vp]),
+    ("huff_enc_hist_launch", i, [vp]),
     ("huff_enc_bits", i, [vp, vp, u64p]),
     ("huff_enc_pack", i, [vp, vp, C.c_uint64, vp, sz, vp, sz, u64p]),
     ("huff_enc_pack_shards", i, [vp, vp, C.c_uint32, C.c_uint32, vp, vp, vp, sz, C.POINTER(vp), u64p, u64p]),

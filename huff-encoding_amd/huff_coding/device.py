@@ -47,6 +47,13 @@ class EncodeJob:
         _check(load().huff_enc_hist(self.h, w.ctypes.data))
         return w
 
+    def hist_launch(self):
+        """pass 1 queued ahead, not waited for: the next hist()/compress() of
+        this job only waits for its weights (huff_enc_hist_launch). Queued
+        between a job's pack and its decode, the host tree build of the next
+        compress overlaps that decode."""
+        _check(load().huff_enc_hist_launch(self.h))
+
     def hist_row(self, d_row: int):
         """pass 1 enqueued without a host wait: 258 int64 at d_row (device) =
         [weights(256) | last <= 8 input bytes, little-endian | their count]"""

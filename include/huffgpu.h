@@ -196,6 +196,13 @@ int huff_enc_create(huff_ctx* ctx, const uint8_t* d_in, size_t n, huff_enc** out
 void huff_enc_free(huff_enc* e);
 /* pass 1: hist256 over the job (per-chunk + global); weights to host */
 int huff_enc_hist(huff_enc* e, uint64_t weights[256]);
+/* pass 1 queued ahead, without waiting for it: the next huff_enc_hist or
+ * huff_enc_compress of this job only waits for its weights. Queued between a
+ * job's pack and its decode, the next job's host tree build overlaps that
+ * decode (a streaming encoder's software pipeline; no reference counterpart).
+ * One pending pass 1 per context: another job's hist/compress/hist_launch on
+ * the same context fails with HUFF_E_STATE until this job's is waited for. */
+int huff_enc_hist_launch(huff_enc* e);
 /* pass 1 for a sharded job without a host round trip (replaces
  * the per-shard ByteWeights::threaded_from_bytes + merge, weights.rs:293-319):
  * enqueues hist256 on the context stream and writes one row of 258 int64 to

@@ -831,6 +831,68 @@ def test_enc_compress_one_call(H, O, ctx):
         assert torch.equal(dec[:n], x[:n])
 
 
+@pytest.mark.parametrize("kind", ["uniform", "zipf", "text"])
+def test_pipelined_steps(H, O, ctx, kind):
+    """bench.py's software pipeline: each step's pass 1 is queued between the
+    previous step's pack and decode (huff_enc_hist_launch). Every compress
+    and decode equals the serial one, bit for bit, and the oracle's bytes"""
+    import torch
+    from huff_coding import device as D
+
+    n = (1 << 22) + 77
+    x = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
+    D.generate(ctx, kind, 7 + n, x.data_ptr(), n, cdf=D.zipf_cdf(1.2) if kind == "zipf" else None)
+    host = x[:n].cpu().numpy()
+    ot = O.Tree.from_weights(O.weights_from_array(O.fast_hist(host, 8)))
+    code, ln = ot.code_table()
+    want, wbits = O.fast_encode(host, code, ln, threads=8)
+    job = H.EncodeJob(ctx, x.data_ptr(), n)
+    out = torch.zeros(n + 128, dtype=torch.uint8, device="cuda")
+    dec = torch.zeros(n + 64, dtype=torch.uint8, device="cuda")
+    steps = 4
+    for i in range(steps):
+        out.zero_()
+        dec.zero_()
+        tree, bits = job.compress(out.data_ptr(), out.numel())
+        if i + 1 < steps:
+            job.hist_launch()
+            job.hist_launch()  # a second launch while one is pending is a no-op
+        job.decode(tree, out.data_ptr(), dec.data_ptr())
+        torch.cuda.synchronize()
+        assert tree.as_bin() == ot.as_bin()
+        assert bits == wbits and (out[: (bits + 7) // 8].cpu().numpy() == want).all(), (kind, i)
+        assert torch.equal(dec[:n], x[:n]), (kind, i)
+
+
+HUFF_E_STATE = 18  # include/huffgpu.h
+
+
+def test_hist_launch_one_pending_per_context(H, ctx):
+    """the context's pinned weights word serves one pending pass 1: another
+    job's hist/compress/hist_launch fails with HUFF_E_STATE until it is
+    waited for; hist() consumes it; freeing the job releases it"""
+    import torch
+    from huff_coding import device as D
+
+    n = 1 << 20
+    x = torch.empty(2 * n + 64, dtype=torch.uint8, device="cuda")
+    D.generate(ctx, "text", 5, x.data_ptr(), 2 * n)
+    a = H.EncodeJob(ctx, x.data_ptr(), n)
+    b = H.EncodeJob(ctx, x.data_ptr() + n, n)
+    out = torch.zeros(n + 128, dtype=torch.uint8, device="cuda")
+    a.hist_launch()
+    for call in (lambda: b.hist(), lambda: b.hist_launch(), lambda: b.compress(out.data_ptr(), out.numel())):
+        with pytest.raises(H.HuffError) as e:
+            call()
+        assert e.value.code == HUFF_E_STATE and "pending" in str(e.value)
+    wa = a.hist()
+    assert wa.sum() == n
+    assert b.hist().sum() == n  # nothing pending any more
+    b.hist_launch()
+    b.close()  # huff_enc_free with its pass 1 pending
+    assert a.hist().sum() == n
+
+
 def test_bytemap_pack_then_bit_decoder(H, O, ctx, monkeypatch):
     """the byte-map pack leaves its arithmetic restart index unwritten; a
     decode through the bit decoders (fixed-8 disabled after the pack) must
