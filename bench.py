@@ -340,17 +340,23 @@ def run_workload(s: Setup, kind: str, n: int, with_cpu: bool, strong: bool = Fal
             state["out"] = torch.empty(state["cap"], dtype=torch.uint8, device="cuda")
             return encode()
 
-    # N=1 weak steps are software-pipelined: the next step's pass 1 is queued
+    # Weak steps are software-pipelined: at N=1 the next step's pass 1 is queued
     # between this step's pack and its decode (huff_enc_hist_launch), so the
     # host tree build overlaps the decode instead of idling the GPU (~27 us a
     # step, profiles/r06/pipeline). Every step still runs pass 1, tree, pass 2
     # and decode over the whole batch.
-    pipe = world == 1 and flush is None and not args.no_pipeline
+    # N>1 over the library's communicator the same: the next step's exchange
+    # (pass 1, row, all-gather, rows to the host) is queued ahead of the decode
+    # (huff_mgpu_exchange_launch), every rank at the same point.
+    pipe = (world == 1 or s.comm is not None) and flush is None and not args.no_pipeline
 
     def step(more=False):
         tree, bits = encode_grow()
         if pipe and more:
-            job.hist_launch()
+            if world == 1:
+                job.hist_launch()
+            else:
+                s.comm.exchange_launch(job)
         job.decode(tree, state["out"].data_ptr(), dec.data_ptr())
         return bits, tree
 

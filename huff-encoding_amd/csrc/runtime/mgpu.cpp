@@ -6,7 +6,8 @@
 // rank over any channel it has (MPI, TCP, a file), and each rank joins with
 // huff_comm_init. huff_mgpu_compress then runs the whole sharded encode of
 // the rank's job in one call (huff_mgpu_pack_rows is its host half, for
-// callers that exchange the rows over their own channel):
+// callers that exchange the rows over their own channel;
+// huff_mgpu_exchange_launch queues the exchange of the next call ahead):
 //
 //   pass 1 (hist256 + row kernel)  -> ncclAllGather of a 258 x int64 row per
 //   rank on the context stream     -> one device-to-host copy, ONE host wait
@@ -38,7 +39,11 @@ struct huff_comm {
     ncclComm_t comm = nullptr;
     int world = 0, rank = 0;
     DevBuf row, rows;    // this rank's row, the gathered rows (device)
-    PinnedBuf host_rows; // the gathered rows (host)
+    PinnedBuf host_rows; // the gathered rows (host); its event follows their copy
+    // an exchange queued ahead by huff_mgpu_exchange_launch for this job, not
+    // yet consumed by huff_mgpu_compress, and the job's own pass-1 status
+    const huff_enc* pending = nullptr;
+    huff::Status pending_local;
     ~huff_comm() {
         if (comm) ncclCommDestroy(comm);
     }
@@ -148,38 +153,75 @@ int huff_mgpu_pack_rows(huff_enc* e, const int64_t* rows, int world, int rank, u
     });
 }
 
+namespace {
+
+// pass 1 -> row -> all-gather -> rows to pinned host memory, all queued on
+// the context stream (the copy's completion recorded on host_rows.ev). A
+// rank that cannot run its pass 1 still takes part in the collective, with a
+// row that marks it failed (tail count -1): every rank then returns an error
+// instead of the others blocking in ncclAllGather. The local failure (its
+// own status code: argument, HIP, memory) is returned in *local.
+huff::Status queue_exchange(huff_comm* c, huff_enc* e, huff::Status* local) {
+    huff_ctx* ctx = c->ctx;
+    // a context that cannot be activated cannot post its row either: the
+    // other ranks would block in the collective, so say so loudly
+    HUFF_TRY(ctx->activate());
+    const size_t world = static_cast<size_t>(c->world);
+    if (!*local) *local = e->hist_row(static_cast<long long*>(c->row.p));
+    if (*local) {
+        static const std::vector<int64_t> bad = [] {
+            std::vector<int64_t> r(kRowWords, 0);
+            r[257] = -1;
+            return r;
+        }();
+        HIP_TRY_RT(hipMemcpyAsync(c->row.p, bad.data(), kRowWords * 8, hipMemcpyHostToDevice, ctx->stream));
+    }
+    NCCL_TRY(ncclAllGather(c->row.p, c->rows.p, kRowWords, ncclInt64, c->comm, ctx->stream));
+    HIP_TRY_RT(hipMemcpyAsync(c->host_rows.p, c->rows.p, kRowWords * 8 * world, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY_RT(hipEventRecord(c->host_rows.ev, ctx->stream));
+    return huff::Status::ok();
+}
+
+}  // namespace
+
+// The exchange of the job's next compress queued now (a streaming encoder's
+// software pipeline: queued between a pack and its decode, the wait and tree
+// of the next huff_mgpu_compress overlap that decode). Every rank must queue
+// it at the same point of its stream order, as for any collective.
+int huff_mgpu_exchange_launch(huff_comm* c, huff_enc* e) {
+    if (!c) return fail(HUFF_E_INVALID_ARG, "null communicator");
+    if (c->pending)  // no collective queued: every rank fails the same way
+        return fail(HUFF_E_STATE, "an exchange is already pending on this communicator");
+    huff::Status local;
+    if (!e) local = huff::Status::err(HUFF_E_INVALID_ARG, "null argument");
+    else if (e->ctx != c->ctx) local = huff::Status::err(HUFF_E_INVALID_ARG, "a job of another context");
+    return guarded([&]() -> huff::Status {
+        HUFF_TRY(queue_exchange(c, e, &local));
+        c->pending = e;
+        c->pending_local = local;
+        return huff::Status::ok();
+    });
+}
+
 int huff_mgpu_compress(huff_comm* c, huff_enc* e, uint8_t* d_out, size_t out_cap, huff_tree** tree_out,
                        uint64_t* bit_base_out, uint64_t* bits_out, uint64_t* owned_bytes_out) {
     if (!c) return fail(HUFF_E_INVALID_ARG, "null communicator");
     if (tree_out) *tree_out = nullptr;
-    // A rank that cannot run its pass 1 still takes part in the collective,
-    // with a row that marks it failed (tail count -1): every rank then
-    // returns an error instead of the others blocking in ncclAllGather. The
-    // local failure keeps its own status code (argument, HIP, memory).
+    if (c->pending && c->pending != e)
+        return fail(HUFF_E_STATE, "an exchange of another job is pending on this communicator");
     huff::Status local;
     if (!e || !d_out || !tree_out) local = huff::Status::err(HUFF_E_INVALID_ARG, "null argument");
     else if (e->ctx != c->ctx) local = huff::Status::err(HUFF_E_INVALID_ARG, "a job of another context");
     else if (reinterpret_cast<uintptr_t>(d_out) & 15)
         local = huff::Status::err(HUFF_E_INVALID_ARG, "d_out must be 16-byte aligned");
     return guarded([&]() -> huff::Status {
-        huff_ctx* ctx = c->ctx;
-        // a context that cannot be activated cannot post its row either: the
-        // other ranks would block in the collective, so say so loudly
-        HUFF_TRY(ctx->activate());
-        const size_t world = static_cast<size_t>(c->world);
-        if (!local) local = e->hist_row(static_cast<long long*>(c->row.p));
-        if (local) {
-            static const std::vector<int64_t> bad = [] {
-                std::vector<int64_t> r(kRowWords, 0);
-                r[257] = -1;
-                return r;
-            }();
-            HIP_TRY_RT(hipMemcpyAsync(c->row.p, bad.data(), kRowWords * 8, hipMemcpyHostToDevice, ctx->stream));
+        if (c->pending) {  // queued ahead: only the wait is left
+            c->pending = nullptr;
+            if (!local) local = c->pending_local;
+        } else {
+            HUFF_TRY(queue_exchange(c, e, &local));
         }
-        NCCL_TRY(ncclAllGather(c->row.p, c->rows.p, kRowWords, ncclInt64, c->comm, ctx->stream));
-        HIP_TRY_RT(hipMemcpyAsync(c->host_rows.p, c->rows.p, kRowWords * 8 * world, hipMemcpyDeviceToHost,
-                                  ctx->stream));
-        HUFF_TRY(ctx->sync());
+        HUFF_TRY(c->host_rows.wait());  // the rows' copy, not the work queued after it
         if (local) return local;
         const int rc = huff_mgpu_pack_rows(e, static_cast<const int64_t*>(c->host_rows.p), c->world, c->rank, d_out,
                                            out_cap, tree_out, bit_base_out, bits_out, owned_bytes_out);

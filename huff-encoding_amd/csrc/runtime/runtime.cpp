@@ -652,7 +652,10 @@ huff::Status huff_enc::hist_row(long long* d_row) {
     HUFF_TRY(ctx->activate());
     if (ctx->hist_pending == this) ctx->hist_pending = nullptr;
     hipStream_t s = ctx->stream;
-    have_hist = packed = sums_valid = false;
+    // the restart index (and the check build's sums) still describe the last
+    // packed stream until the next pack rewrites them: a decode of that
+    // stream may still be queued after this pass 1 (huff_mgpu_exchange_launch)
+    have_hist = false;
     if (nchunks == 0) {
         HIP_TRY(hipMemsetAsync(d_row, 0, 258 * 8, s));
         return huff::Status::ok();

@@ -109,6 +109,7 @@ SIGNATURES = [
     ("huff_comm_free", None, [vp]),
     ("huff_comm_world", i, [vp, C.POINTER(i), C.POINTER(i)]),
     ("huff_mgpu_compress", i, [vp, vp, vp, sz, C.POINTER(vp), u64p, u64p, u64p]),
+    ("huff_mgpu_exchange_launch", i, [vp, vp]),
     ("huff_mgpu_pack_rows", i, [vp, vp, i, i, vp, sz, C.POINTER(vp), u64p, u64p, u64p]),
     ("huff_dev_generate", i, [vp, i, C.c_uint64, C.c_uint64, u64p, vp, sz]),
     ("huff_dev_calibrate", i, [vp, vp, vp, sz, i, C.POINTER(C.c_double), C.POINTER(C.c_double)]),

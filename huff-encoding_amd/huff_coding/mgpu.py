@@ -208,6 +208,16 @@ class NativeComm:
         _check(load().huff_comm_world(self.h, C.byref(w), C.byref(r)))
         return w.value, r.value
 
+    def exchange_launch(self, job):
+        """huff_mgpu_exchange_launch: the exchange of the job's next compress
+        queued now (every rank at the same point); that compress then only
+        waits for the gathered rows"""
+        from ._lib import load
+
+        from . import _check
+
+        _check(load().huff_mgpu_exchange_launch(self.h, job.h))
+
     def compress(self, job, d_out: int, out_cap: int):
         """huff_mgpu_compress: (HuffTree, bit_base, bits, owned_bytes); a short
         buffer raises HuffError with .bits_needed / .bit_base"""

@@ -275,6 +275,14 @@ int huff_comm_world(const huff_comm* c, int* world, int* rank);
  * HUFF_E_BUFFER_TOO_SMALL *bits_out / *bit_base_out still hold the need. */
 int huff_mgpu_compress(huff_comm* c, huff_enc* e, uint8_t* d_out, size_t out_cap, huff_tree** tree_out,
                        uint64_t* bit_base_out, uint64_t* bits_out, uint64_t* owned_bytes_out);
+/* The exchange of the job's NEXT huff_mgpu_compress (pass 1, its row, the
+ * all-gather, the rows' copy to the host) queued now, without waiting: the
+ * next huff_mgpu_compress of this job only waits for the rows. Queued
+ * between a job's pack and its decode, that wait and the host tree overlap
+ * the decode (a streaming encoder's software pipeline; no reference
+ * counterpart). Every rank must call it at the same point, as any
+ * collective; one pending exchange per communicator (HUFF_E_STATE). */
+int huff_mgpu_exchange_launch(huff_comm* c, huff_enc* e);
 /* The host half of huff_mgpu_compress, for a caller that exchanges the rows
  * over its own channel: rows = world x 258 int64 in rank order, each what
  * huff_enc_hist_row wrote for that rank's shard (host memory, already

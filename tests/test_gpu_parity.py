@@ -961,4 +961,20 @@ def test_native_comm_world1_mgpu_compress(H, O, ctx, kind):
     with pytest.raises(H.HuffError) as ei:
         comm.compress(job, out.data_ptr() + 3, out.numel() - 3)
     assert "aligned" in str(ei.value)
+    # bench.py's pipeline: the next compress's exchange queued between a pack
+    # and its decode (huff_mgpu_exchange_launch); same bytes every step
+    for i in range(3):
+        out.zero_()
+        dec.zero_()
+        t2, b2, bits2, owned2 = comm.compress(job, out.data_ptr(), out.numel())
+        if i < 2:
+            comm.exchange_launch(job)
+            with pytest.raises(H.HuffError) as ei:  # one pending exchange per communicator
+                comm.exchange_launch(job)
+            assert ei.value.code == HUFF_E_STATE
+        job.decode(t2, out.data_ptr(), dec.data_ptr())
+        torch.cuda.synchronize()
+        assert t2.as_bin() == rtree.as_bin() and bits2 == bits and owned2 == owned
+        assert (out[:owned].cpu().numpy() == want).all(), i
+        assert torch.equal(dec[:n], x[:n]), i
     comm.close()
