@@ -502,8 +502,12 @@ int huff_enc_compress(huff_enc* e, uint8_t* d_out, size_t out_cap, huff_tree** t
                 return static_cast<long long>(
                     std::chrono::duration_cast<std::chrono::nanoseconds>(a.time_since_epoch()).count());
             };
-            std::fprintf(stderr, "huff_enc_compress host us: hist %.1f tree %.1f pack %.1f at %lld %lld %lld %lld %lld\n",
-                         us(t0, t1), us(t1, t2), us(t2, t3), ns(t0), ns(t1), ns(t2), ns(tl), ns(t3));
+            const auto& ps = huff::pack_stamps();  // inside pass 2's call: bit count, launch start, launch end
+            std::fprintf(stderr,
+                         "huff_enc_compress host us: hist %.1f tree %.1f pack %.1f (bits %.1f args %.1f launch %.1f) "
+                         "at %lld %lld %lld %lld %lld\n",
+                         us(t0, t1), us(t1, t2), us(t2, t3), us(t2, ps.bits), us(ps.bits, ps.launch),
+                         us(ps.launch, ps.launched), ns(t0), ns(t1), ns(t2), ns(tl), ns(t3));
         }
         if (bits_out) *bits_out = bits;
         HUFF_TRY(st);

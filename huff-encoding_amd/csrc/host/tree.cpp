@@ -89,6 +89,34 @@ Status HuffTree::from_leaves(const uint8_t* letters, const uint64_t* weights, si
         out.nodes_.push_back(leaf);
     }
     if (merge_untied(weights, n, out.nodes_, out.root_)) return Status::ok();
+    // a byte tree (<= 257 leaves, so < 1024 nodes) whose weights sum below
+    // 2^54: the packed-key heap, same pops
+    uint64_t sum = 0;
+    bool small = n <= 257;
+    for (size_t i = 0; small && i < n; ++i) {
+        sum += weights[i];
+        small = weights[i] < (1ull << 54) && sum < (1ull << 54);
+    }
+    if (small) {
+        out.nodes_.resize(n);  // the leaves stay; merge_untied's joints go
+        PackedMaxHeap heap;
+        for (size_t i = 0; i < n; ++i) heap.push(weights[i], static_cast<int32_t>(i));  // branch_heap.rs:52-58
+        while (heap.size() > 1) {  // tree_inner.rs:289-303
+            uint64_t wa, wb;
+            int32_t a, b;
+            heap.pop(wa, a);  // min       -> left  (code bit 0)
+            heap.pop(wb, b);  // next_min  -> right (code bit 1)
+            HuffNode joint;
+            joint.weight = wa + wb;
+            joint.left = a;
+            joint.right = b;
+            out.nodes_.push_back(joint);
+            heap.push(joint.weight, static_cast<int32_t>(out.nodes_.size() - 1));
+        }
+        uint64_t w;
+        heap.pop(w, out.root_);  // tree_inner.rs:306
+        return Status::ok();
+    }
     out.nodes_.clear();
     RustMaxHeap heap(n + 1);
     for (size_t i = 0; i < n; ++i) {  // branch_heap.rs:52-58

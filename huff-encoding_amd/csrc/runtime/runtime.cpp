@@ -717,10 +717,18 @@ huff::Status huff_enc::check_sums(const uint8_t* d_out) {
                                                  " task(s) of 4096 letters; first: task " + std::to_string(e[1]));
 }
 
+huff::PackStamps& huff::pack_stamps() {
+    static thread_local PackStamps p;
+    return p;
+}
+
 huff::Status huff_enc::pack(const huff_tree* t, uint64_t base, const uint8_t* prev_tail, size_t prev_tail_len,
                             uint8_t* d_out, size_t out_cap, uint64_t* total) {
+    auto& ps = huff::pack_stamps();
+    ps.bits = ps.launch = ps.launched = {};
     uint64_t tb = 0;
     HUFF_TRY(bits(t, &tb));
+    ps.bits = std::chrono::steady_clock::now();
     compact_index = false;  // set by the general pack below when it writes the compact index
     const uint64_t need = ((base & 7) + tb + 7) / 8;
     if (total) *total = tb;
@@ -748,7 +756,9 @@ huff::Status huff_enc::pack(const huff_tree* t, uint64_t base, const uint8_t* pr
             for (int b = 0; b < 256; ++b) m.map[b] = static_cast<uint8_t>(et.code[b]);
             m.nchunks = nchunks;
             m.base_bits = 0;
+            ps.launch = std::chrono::steady_clock::now();
             HUFF_TRY(ctx->timed("pack", [&] { return huff::dev::launch_bytemap(m, s); }));
+            ps.launched = std::chrono::steady_clock::now();
             packed = true;
             index_pending = true;  // arithmetic: written only if a consumer needs it
             packed_tree_id = t->id;

@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <chrono>
 #include <functional>
 #include <map>
 #include <memory>
@@ -73,6 +74,12 @@ struct DecTables {
 
 // HUFF_DISABLE_FIXED8=1 forces the general kernels even for all-8-bit codes
 bool fixed8_disabled();
+// HUFF_HOST_TRACE: when huff_enc::pack finished its bit count, started and
+// returned from the byte-map launch (this thread's last pack)
+struct PackStamps {
+    std::chrono::steady_clock::time_point bits, launch, launched;
+};
+PackStamps& pack_stamps();
 // HUFF_SMALL_STAGE=0 keeps the decoders' 4.5 KiB stage for every stream
 bool small_stage_enabled();
 // HUFF_DEC_VARIANT=11 -> k_decode_fixed's self-checking build (mode 1; else 0)

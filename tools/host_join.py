@@ -20,7 +20,7 @@ def main():
         if m:
             host.append([int(v) for v in m.groups()])
     rows = sorted(csv.DictReader(open(sys.argv[2])), key=lambda r: int(r["Start_Timestamp"]))
-    pub = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in rows if "k_hist_publish" in r["Kernel_Name"]]
+    pub = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in rows if "k_hist_publish" in r["Kernel_Name"] or "k_rows_publish" in r["Kernel_Name"]]
     h1 = [int(r["Start_Timestamp"]) for r in rows if "k_hist1x2" in r["Kernel_Name"]]
     bm = [int(r["Start_Timestamp"]) for r in rows if "k_bytemap" in r["Kernel_Name"]]
     out = []
