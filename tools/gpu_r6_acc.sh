@@ -1,0 +1,21 @@
+#!/usr/bin/env bash
+# Round 6: the pack's accumulator emit (HUFF_LIB_AB=acc, emit_codes_acc)
+# against the grouped two-word ORs: parity under the variant, then kbench
+# --phase pack on Zipf, text and uniform through the general kernels, and the
+# Zipf bench line, alternated.
+set -uo pipefail
+root=${GRAFT_REPO_ROOT:-$(pwd)}
+tag=${1:-r6acc}
+out=$root/gpurun_out/$tag; mkdir -p $out
+cd $root
+HUFF_LIB_AB=acc timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_wide.py -x -q --timeout 120 --timeout-method thread > $out/pytest.log 2>&1; tail -2 $out/pytest.log
+for r in 1 2; do
+  for v in default acc; do
+    if [ $v = default ]; then env=""; else env="HUFF_LIB_AB=$v"; fi
+    for wl in zipf text uniform; do
+      fx=""; [ $wl = uniform ] && fx="HUFF_DISABLE_FIXED8=1"
+      env $env $fx timeout -k 10 120 python -u tools/kbench.py --phase pack --workload $wl --iters 20 > $out/pack_${v}_${wl}_$r.json 2> $out/pack_${v}_${wl}_$r.err || { tail -5 $out/pack_${v}_${wl}_$r.err; exit 1; }
+    done
+  done
+done
+grep -H "pack" $out/pack_*.json | sed "s|$out/||" | cut -c1-200
