@@ -407,6 +407,9 @@ hipError_t launch_decode_deep_serial(const DeepSerialArgs& a, hipStream_t s);
 size_t pack_lds_bytes(bool long_codes, uint32_t max_len, uint32_t stage_words);
 uint32_t pack_round_bytes();  // input bytes per wave round of k_pack (its LDS stage holds one round's bits)
 uint32_t pack_waves_per_group(bool long_codes);
+// resident k_pack workgroups per CU for this launch (its registers and LDS
+// both limit; the persistent grid is this many per CU)
+uint32_t pack_groups_per_cu(bool long_codes, uint32_t max_len, size_t lds);
 size_t decode_lds_bytes(uint32_t lut_bits);
 // HUFF_DEC_VARIANT: 10 = k_decode_fixed (the default for codes <= 32 bits),
 // 11 = its self-checking build

@@ -263,18 +263,33 @@ uint32_t pack_round_bytes() { return kRoundB; }
 
 uint32_t pack_waves_per_group(bool long_codes) { return long_codes ? pack_waves<true>() : pack_waves<false>(); }
 
+namespace {
+using PackKern = void (*)(PackArgs);
+PackKern pack_kernel(bool long_codes, uint32_t max_len) {
+    if (long_codes) return k_pack<true>;
+    if (max_len <= 8) return k_pack<false, 4>;  // 4 codes per OR pair
+    if (max_len <= 16) return k_pack<false, 2>;
+    return k_pack<false, 1>;
+}
+}  // namespace
+
+uint32_t pack_groups_per_cu(bool long_codes, uint32_t max_len, size_t lds) {
+    int per = 0;
+    const int threads = (long_codes ? pack_waves<true>() : pack_waves<false>()) * 64;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, pack_kernel(long_codes, max_len), threads, lds) !=
+            hipSuccess ||
+        per < 1) {  // the LDS bound alone
+        const size_t by_lds = lds ? (160 * 1024) / lds : 8;
+        per = static_cast<int>(by_lds < 1 ? 1 : by_lds > 8 ? 8 : by_lds);
+    }
+    return static_cast<uint32_t>(per);
+}
+
 hipError_t launch_pack(bool long_codes, const PackArgs& a, hipStream_t s) {
     if (a.nchunks == 0) return hipSuccess;
     const size_t lds = pack_lds_bytes(long_codes, a.max_len, a.stage_words);
-    if (long_codes) {
-        launch_k(k_pack<true>, dim3(a.grid), dim3(pack_waves<true>() * 64), lds, s, a);
-    } else if (a.max_len <= 8) {  // 4 codes per OR pair
-        launch_k((k_pack<false, 4>), dim3(a.grid), dim3(pack_waves<false>() * 64), lds, s, a);
-    } else if (a.max_len <= 16) {
-        launch_k((k_pack<false, 2>), dim3(a.grid), dim3(pack_waves<false>() * 64), lds, s, a);
-    } else {
-        launch_k((k_pack<false, 1>), dim3(a.grid), dim3(pack_waves<false>() * 64), lds, s, a);
-    }
+    launch_k(pack_kernel(long_codes, a.max_len), dim3(a.grid),
+             dim3((long_codes ? pack_waves<true>() : pack_waves<false>()) * 64), lds, s, a);
     return hipGetLastError();
 }
 

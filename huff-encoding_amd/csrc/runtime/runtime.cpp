@@ -846,7 +846,7 @@ huff::Status huff_enc::pack(const huff_tree* t, uint64_t base, const uint8_t* pr
     a.stage_words = (huff::dev::pack_round_bytes() / 32 * std::max<uint32_t>(et.maxlen, 1) + 12 + 3) & ~3u;
     a.max_len = et.maxlen;
     const size_t lds = huff::dev::pack_lds_bytes(long_codes, et.maxlen, a.stage_words);
-    const uint32_t per_cu = std::max<uint32_t>(1, std::min<uint32_t>(8, static_cast<uint32_t>((160 * 1024) / lds)));
+    const uint32_t per_cu = huff::dev::pack_groups_per_cu(long_codes, et.maxlen, lds);
     const uint32_t wpg = huff::dev::pack_waves_per_group(long_codes);
     a.grid = std::max<uint32_t>(1, std::min<uint32_t>((nchunks + wpg - 1) / wpg, ctx->cu_count * per_cu));
     HUFF_TRY(ctx->timed("pack", [&] { return huff::dev::launch_pack(long_codes, a, s); }));
