@@ -66,59 +66,102 @@ struct Task {
     uint32_t skip;      // SKIP: codes to decode and drop before this lane's letters
 };
 
-// SKIP: the index-free path's k_mark_lite entries (boundary | skip << 48)
-template <bool SKIP = false>
-__device__ __forceinline__ Task task_info(const DecodeArgs& a, uint64_t t, uint32_t lane) {
+// A task's index entries in two steps: task_load issues the loads (nothing
+// in it reads a loaded value, so the compiler places no wait there) and
+// task_finish derives the task from them. k_decode_dma issues the loads of
+// the task after next before it decodes and finishes them a task later, so
+// their latency hides behind the decode and no wait drains its in-flight
+// LDS-DMA early (a vmcnt wait covers every older VMEM operation).
+// Every load is unconditional (indices clamped to the arrays) and lands in a
+// field of its own width: a select or a widening copy of a loaded value is a
+// use, and the compiler would wait for it right there.
+struct TaskLoad {
+    uint32_t m = 0, m1 = 0, s0 = 0, s1 = 0;  // u16/u32 entries (zero-extended by the load)
+    uint64_t q = 0, q1 = 0, q2 = 0;          // u64 entries
+};
+// SKIP: the index-free path's k_mark_lite entries (boundary | skip << 48).
+// MODE: which index the task reads, when known at compile time (k_decode_dma:
+// the branches over the index forms made the compiler join their registers
+// and wait for the loads at the join): kIdxAny (run time), kIdxMark32
+// (compact marks), kIdxSub16 (the compact restart index)
+constexpr int kIdxAny = 0, kIdxMark32 = 1, kIdxSub16 = 2;
+template <bool SKIP = false, int MODE = kIdxAny>
+__device__ __forceinline__ TaskLoad task_load(const DecodeArgs& a, uint64_t t, uint32_t lane) {
+    TaskLoad r;
+    // vz = 0 in every lane, but divergent to the compiler: the wave-uniform
+    // entries then load into VGPRs and stay there until task_finish (as
+    // uniform values they were moved to SGPRs by a readfirstlane right after
+    // the load, i.e. waited for at once)
+    const uint64_t vz = MODE == kIdxAny ? 0u : __builtin_amdgcn_mbcnt_lo(0u, 0u);
+    const uint64_t ntasks = (a.n + kTaskSym - 1) / kTaskSym;
+    const uint64_t last = (a.n - 1) / kIdx;  // the last mark / index entry
+    const uint64_t sym0 = t * kTaskSym;
+    const uint64_t next = sym0 + kTaskSym;
+    const uint64_t li = sym0 / kIdx + lane < last ? sym0 / kIdx + lane : last;  // the lane's entry (clamped)
+    const uint64_t ni = (next / kIdx < last ? next / kIdx : last) + vz;         // the next task's first
+    const uint64_t t1 = (t + 1 < ntasks ? t + 1 : ntasks - 1) + vz;
+    const uint64_t t0 = t + vz;
+    // the task's end (the next task's first bit) beside the lane's entry: a
+    // scalar load with no dependence on it, so both are in flight together
+    if (MODE == kIdxMark32 || (MODE == kIdxAny && SKIP && a.mark32)) {  // compact marks (k_mark_lite)
+        r.m1 = a.mark32[ni];
+        r.s1 = a.task_seg[t1];  // the next task's first mark's own segment
+        r.s0 = a.task_seg[t0];
+        r.m = a.mark32[li];
+    } else if (MODE == kIdxAny && a.sub_abs64) {  // index-free streams: absolute start bit of every 64th symbol
+        r.q1 = a.sub_abs64[ni];
+        r.q = a.sub_abs64[li];
+    } else if (MODE == kIdxSub16 || (MODE == kIdxAny && a.sub16)) {  // compact index: task base + u16 offset
+        r.q1 = a.task_base[t1];
+        r.q2 = a.chunk_start[a.nchunks + vz];
+        r.q = a.task_base[t0];
+        r.m = a.sub16[li];
+    } else {
+        r.q1 = a.chunk_start[(next < a.n ? next : sym0) / kChunk];
+        r.m1 = a.sub_bit[ni];
+        r.q2 = a.chunk_start[a.nchunks];
+        r.q = a.chunk_start[sym0 / kChunk];
+        r.m = a.sub_bit[li];
+    }
+    return r;
+}
+template <bool SKIP = false, int MODE = kIdxAny>
+__device__ __forceinline__ Task task_finish(const DecodeArgs& a, uint64_t t, uint32_t lane, const TaskLoad& r) {
     Task k;
     k.sym0 = t * kTaskSym;
     k.nsym = static_cast<uint32_t>(a.n - k.sym0 < kTaskSym ? a.n - k.sym0 : kTaskSym);
     const uint32_t ls = lane * kLaneSym;
     k.cnt = ls >= k.nsym ? 0u : (k.nsym - ls < kLaneSym ? k.nsym - ls : kLaneSym);
     k.skip = 0;
-    // the task's end (the next task's first bit) first: a scalar load with no
-    // dependence on the lane's entry, so both are in flight together (read
-    // after the lane's entry it cost a second memory latency per task)
     const uint64_t next = k.sym0 + kTaskSym;
+    const bool tail = next >= a.n;  // the stream's last task
     uint64_t end;
-    if (SKIP && a.mark32) {  // compact marks (k_mark_lite): segment + offset + skip
-        if (next < a.n) {
-            const uint32_t m = a.mark32[next / kIdx];
-            const uint64_t seg = a.task_seg[t + 1];  // the next task's first mark's own segment
-            end = seg * a.seg_bits + mark32_rel(m) + static_cast<uint64_t>(mark32_skip(m)) * a.max_len;
-        } else {
-            end = a.end_bit;
-        }
-        const uint32_t seg0 = a.task_seg[t];
-        const uint32_t m = k.cnt ? a.mark32[k.sym0 / kIdx + lane] : 0u;
-        k.lane_bit = k.cnt ? static_cast<uint64_t>(mark32_seg(m, seg0)) * a.seg_bits + mark32_rel(m) : 0;
-        k.skip = mark32_skip(m);
-    } else if (a.sub_abs64) {
-        end = next < a.n ? a.sub_abs64[next / kIdx] : a.end_bit;
-    } else if (next < a.n) {
-        end = a.sub16 ? a.task_base[t + 1] : a.chunk_start[next / kChunk] + a.sub_bit[next / kIdx];
-    } else {
-        end = a.chunk_start[a.nchunks];
-    }
-    if (SKIP && a.mark32) {
-        // (read above)
-    } else if (a.sub_abs64) {  // index-free streams: absolute start bit of every 64th symbol (k_mark_lds)
-        k.lane_bit = k.cnt ? a.sub_abs64[k.sym0 / kIdx + lane] : 0;
+    if (MODE == kIdxMark32 || (MODE == kIdxAny && SKIP && a.mark32)) {
+        end = !tail ? static_cast<uint64_t>(r.s1) * a.seg_bits + mark32_rel(r.m1) +
+                          static_cast<uint64_t>(mark32_skip(r.m1)) * a.max_len
+                    : a.end_bit;
+        k.lane_bit = k.cnt ? static_cast<uint64_t>(mark32_seg(r.m, r.s0)) * a.seg_bits + mark32_rel(r.m) : 0;
+        k.skip = k.cnt ? mark32_skip(r.m) : 0u;
+    } else if (MODE == kIdxAny && a.sub_abs64) {
+        end = !tail ? r.q1 : a.end_bit;
+        k.lane_bit = k.cnt ? r.q : 0;
         if constexpr (SKIP) {
             k.skip = static_cast<uint32_t>(k.lane_bit >> 48);
             k.lane_bit &= kSkipPosMask;
         }
-    } else if (a.sub16) {  // compact index: task base + u16 offset
-        k.lane_bit = k.cnt ? a.task_base[t] + a.sub16[k.sym0 / kIdx + lane] : 0;
+    } else if (MODE == kIdxSub16 || (MODE == kIdxAny && a.sub16)) {
+        end = !tail ? r.q1 : r.q2;
+        k.lane_bit = k.cnt ? r.q + r.m : 0;
     } else {
-        const uint32_t c = static_cast<uint32_t>(k.sym0 / kChunk);
-        k.lane_bit = k.cnt ? a.chunk_start[c] + a.sub_bit[k.sym0 / kIdx + lane] : 0;
+        end = !tail ? r.q1 + r.m1 : r.q2;
+        k.lane_bit = k.cnt ? r.q + r.m : 0;
     }
     // readfirstlane returns int: widen through uint32_t (no sign extension)
     const uint32_t f_lo = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(k.lane_bit)));
     const uint32_t f_hi = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(k.lane_bit >> 32)));
     const uint64_t first = (static_cast<uint64_t>(f_hi) << 32) | f_lo;
     if constexpr (SKIP)  // the next task's first bit lies within its skipped codes (used only now)
-        if (!a.mark32 && a.sub_abs64 && next < a.n) end = (end & kSkipPosMask) + (end >> 48) * a.max_len;
+        if (MODE == kIdxAny && !a.mark32 && a.sub_abs64 && !tail) end = (end & kSkipPosMask) + (end >> 48) * a.max_len;
     k.end = end;
     k.b0 = (first >> 3) & ~15ull;
     uint64_t b1 = ((end + 7) >> 3) + 32;  // lookahead: window + the dword read ahead
@@ -126,6 +169,10 @@ __device__ __forceinline__ Task task_info(const DecodeArgs& a, uint64_t t, uint3
     k.len = static_cast<uint32_t>(b1 - k.b0 < 0xFFFFFFFFull ? b1 - k.b0 : 0xFFFFFFFFull);
     k.len = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(k.len)));  // uniform (scalar)
     return k;
+}
+template <bool SKIP = false>
+__device__ __forceinline__ Task task_info(const DecodeArgs& a, uint64_t t, uint32_t lane) {
+    return task_finish<SKIP>(a, t, lane, task_load<SKIP>(a, t, lane));
 }
 
 // The task's staged pieces (np = len / 16 when the range fits the stage)
@@ -200,7 +247,7 @@ template <bool SLOW, bool SKIP, class Words>
 __device__ __forceinline__ void decode_fixed64(const Words& src, uint32_t rel, uint32_t (&o)[16],
                                                const uint16_t* __restrict__ stab, uint32_t K,
                                                const uint32_t* __restrict__ glut, uint32_t Ks, uint32_t* end_rel,
-                                               uint32_t skip, WaveStamps* ws) {
+                                               uint32_t skip, WaveStamps* ws, uint32_t* rp_out = nullptr) {
     uint32_t rp = rel >> 5;
     const uint32_t sh = rel & 31;
     uint64_t buf = static_cast<uint64_t>(src(rp) << sh) << 32;
@@ -286,6 +333,7 @@ __device__ __forceinline__ void decode_fixed64(const Words& src, uint32_t rel, u
         FX_LOOKUP(i + 1);
     }
     *end_rel = 32 * rp - (X & 63u);
+    if (rp_out) *rp_out = rp;  // dwords [0, rp) became valid bits; dword rp was read ahead
 #undef FX_STEP
 #undef FX_LOOKUP
 #undef FX_REFILL
@@ -528,6 +576,205 @@ __device__ __forceinline__ void decode_fixed_body(const DecodeArgs& a) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// k_decode_dma: the same tasks and lane decoder, PERSISTENT waves with the
+// next task's input in flight while the current one decodes. Where the time
+// goes in the one-shot decoder (round-5 stamps, 1 GiB Zipf): of a wave's
+// 16.6 K-cycle life, ~6 K wait for its table copy and first loads (HBM
+// latency), 1.8 K stage the input, 7.5 K decode the 64 letters per lane. A
+// register prefetch of the next task cost a wave per SIMD and lost (round 5,
+// decode_prefetch/); here the prefetch goes straight to LDS by LDS-DMA
+// (buffer_load_dwordx4 ... lds: no VGPR destination, no staging stores) into
+// the wave's second stage buffer, so the load latency hides behind the
+// decode. The stage holds the raw stream bytes (words are byte-swapped as
+// they are read); the swizzled (PAD) layout is made on the SOURCE side
+// (slot p receives piece padded_piece(p), an involution: the register path's
+// layout). Column-stage A/B of this round (each lane loading its own rows so
+// that refill reads are conflict-free): LDS cycles -16 %, time +1..8 %.
+// PMC (profiles/r06/lds/): the one-shot decoder's LDS array is 87 % busy,
+// 62 % of it bank conflicts, yet cutting those cycles did not pay: the wave's
+// serial latency (memory, then the lookup chain) bounds it.
+// ---------------------------------------------------------------------------
+struct LdsWordsBS {  // raw stream bytes in LDS: big-endian words
+    const uint32_t* w;
+    __device__ __forceinline__ uint32_t operator()(uint32_t i) const { return __builtin_bswap32(w[i]); }
+};
+struct PaddedLdsWordsBS {
+    const uint32_t* w;
+    __device__ __forceinline__ uint32_t operator()(uint32_t i) const { return __builtin_bswap32(w[i ^ ((i >> 3) & 28u)]); }
+};
+
+typedef __attribute__((address_space(3))) void* lds_void_p;
+
+// the task's pieces into the stage at `buf` (16 B per lane per instruction,
+// LDS address = buf + 16 lane + 1 KiB r); pieces past the task's range or the
+// stream read zero (the buffer range check), and a task longer than the
+// stage loads nothing (it decodes from global memory)
+template <uint32_t CAPB, bool PAD>
+__device__ __forceinline__ void issue_task_dma(const DecodeArgs& a, const Task& k, uint32_t lane, uint32_t* buf) {
+    constexpr uint32_t NPC = CAPB / 16;
+    constexpr uint32_t R = (NPC + 63) / 64;
+    const uint32_t np = k.len <= CAPB ? k.len / 16 : 0u;
+    const uint64_t end4 = (a.comp_bytes + 3) & ~3ull;
+    const uint64_t avail = end4 > k.b0 ? end4 - k.b0 : 0;
+    const uint32_t nb = static_cast<uint32_t>(avail < 16ull * np ? avail : 16ull * np);
+    const auto rs = buf_rsrc(nb ? a.comp + k.b0 : a.comp, nb);
+#pragma unroll
+    for (uint32_t r = 0; r < R; ++r) {
+        const uint32_t p = lane + 64 * r;
+        const uint32_t src = PAD ? padded_piece(p) : p;
+        if (NPC % 64 == 0 || r + 1 < R || p < NPC)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void_p)(buf + 256 * r), 16, src * 16, 0, 0, 0);
+    }
+}
+
+template <bool SKIP, bool PAD, uint32_t CAPB>
+__device__ __forceinline__ void decode_dma_body(const DecodeArgs& a) {
+    constexpr int MODE = SKIP ? kIdxMark32 : kIdxSub16;  // the index forms the launcher admits
+    // allocation floor of 80 VGPRs (the LDS of the small stages holds 5 waves
+    // per SIMD anyway): at the compiler's 72 the window shift took its
+    // amount from v71, the last register of the allocation — the gfx950
+    // 64-bit shift hazard (tools/check_shift64.py)
+    asm volatile("" ::: "v79");
+    constexpr int NT = kThreads;
+    constexpr int NW = NT / 64;
+    constexpr bool HALVES = CAPB < 64 * kRowBytes;  // the output rows leave in two halves
+    static_assert(CAPB % 16 == 0 && 32 * kRowBytes <= CAPB, "the output rows (or half) fit the stage");
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    const uint32_t K = a.stab_bits;
+    const uint32_t nent = 1u << K;
+    const uint32_t t = threadIdx.x, lane = t & 63, wave = wave_index();
+    const uint16_t* stab = reinterpret_cast<const uint16_t*>(lds);
+    const uint32_t tab_words = (nent + 1) / 2;
+    const uint32_t tab_rw = (tab_words + 3) & ~3u;
+    uint32_t* const st0 = lds + tab_rw + wave * (2 * CAPB / 4);
+    uint32_t* const st1 = st0 + CAPB / 4;
+    const uint64_t ntasks = (a.n + kTaskSym - 1) / kTaskSym;
+    const uint64_t step = static_cast<uint64_t>(gridDim.x) * NW;
+    uint64_t task = static_cast<uint64_t>(blockIdx.x) * NW + wave;
+    Task cur{};
+    TaskLoad nxt_raw{};
+    WaveStamps ws;
+    HUFF_STAMP(ws, 0);
+    {
+        // the table copy overlaps the first task's DMA and the second task's entries
+        const uint32_t tab_pieces = (tab_words + 3) / 4;
+        const auto rtab = buf_rsrc(a.stab, tab_words * 4);
+        constexpr int TP = (512 + NT - 1) / NT;
+        uint4 tp[TP];
+#pragma unroll
+        for (int i = 0; i < TP; ++i) tp[i] = buf_ld16(rtab, (t + NT * i) * 16);
+        if (task < ntasks) {
+            cur = task_finish<SKIP, MODE>(a, task, lane, task_load<SKIP, MODE>(a, task, lane));
+            issue_task_dma<CAPB, PAD>(a, cur, lane, st0);
+            nxt_raw = task_load<SKIP, MODE>(a, task + step < ntasks ? task + step : ntasks - 1, lane);
+        }
+#pragma unroll
+        for (int i = 0; i < TP; ++i)
+            if (t + NT * i < tab_pieces) st_stage16(lds + 4 * (t + NT * i), tp[i]);
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): table stores done; the DMA stays in flight
+        __builtin_amdgcn_s_barrier();
+        HUFF_STAMP(ws, 1);
+        if (task >= ntasks) return;
+        __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): the first stage has landed
+    }
+    bool odd = false;
+    while (true) {
+        // invariant: cur's bytes are in this wave's `stage` (its DMA retired by
+        // a vmcnt wait of this wave), nxt's entries are loaded
+        uint32_t* const stage = odd ? st1 : st0;
+        uint8_t* const sb = reinterpret_cast<uint8_t*>(stage);
+        const uint64_t ntask = task + step;
+        const bool more = ntask < ntasks;
+        Task nxt{};
+        if (more) {
+            nxt = task_finish<SKIP, MODE>(a, ntask, lane, nxt_raw);
+            issue_task_dma<CAPB, PAD>(a, nxt, lane, odd ? st0 : st1);
+        }
+        // (a clamped task index past the last: loaded, never finished)
+        const TaskLoad nn_raw = task_load<SKIP, MODE>(a, ntask + step < ntasks ? ntask + step : ntasks - 1, lane);
+        HUFF_STAMP(ws, 2);
+        const uint32_t rel = static_cast<uint32_t>(cur.lane_bit - cur.b0 * 8);
+        uint8_t* dst = a.out + cur.sym0 + lane * kLaneSym;
+        bool plain = false;  // the last VMEM ops of the task are its 4 row stores
+        if (cur.len > CAPB) {
+            if (cur.cnt)
+                decode_fixed_global(GlobalWords{a.comp, a.comp_bytes, cur.b0 / 4}, rel, cur.cnt, dst, a.lut,
+                                    a.lut_bits, SKIP ? cur.skip : 0u);
+        } else if (cur.nsym == kTaskSym) {
+            uint32_t o[16];
+            uint32_t e = 0;
+            if constexpr (PAD)
+                decode_fixed64<false, SKIP>(PaddedLdsWordsBS{stage}, rel, o, stab, K, a.lut, a.lut_bits, &e, cur.skip, &ws);
+            else
+                decode_fixed64<false, SKIP>(LdsWordsBS{stage}, rel, o, stab, K, a.lut, a.lut_bits, &e, cur.skip, &ws);
+            HUFF_STAMP(ws, 4);
+            wave_sync();  // the wave's stage reads are done
+            uint4* d4 = reinterpret_cast<uint4*>(a.out + cur.sym0) + lane;
+            if constexpr (!HALVES) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    st_stage16(sb + row_piece(lane, q), make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]));
+                wave_sync();
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    st_nt(d4 + 64 * q, ld_stage16(sb + row_piece(16 * q + (lane >> 2), lane & 3)));
+            } else {
+#pragma unroll
+                for (uint32_t h = 0; h < 2; ++h) {
+                    if ((lane >> 5) == h) {
+#pragma unroll
+                        for (int q = 0; q < 4; ++q)
+                            st_stage16(sb + row_piece(lane & 31, q),
+                                       make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]));
+                    }
+                    wave_sync();
+#pragma unroll
+                    for (int q = 0; q < 2; ++q)
+                        st_nt(d4 + 64 * (2 * h + q), ld_stage16(sb + row_piece(16 * q + (lane >> 2), lane & 3)));
+                    wave_sync();
+                }
+            }
+            plain = true;
+            HUFF_STAMP(ws, 5);
+        } else if (cur.cnt) {
+            uint32_t o[16];
+            uint32_t e = 0;
+            if constexpr (PAD)
+                decode_fixed64<false, SKIP>(PaddedLdsWordsBS{stage}, rel, o, stab, K, a.lut, a.lut_bits, &e, cur.skip, nullptr);
+            else
+                decode_fixed64<false, SKIP>(LdsWordsBS{stage}, rel, o, stab, K, a.lut, a.lut_bits, &e, cur.skip, nullptr);
+            if (cur.cnt == kLaneSym) {
+                uint4* d4 = reinterpret_cast<uint4*>(dst);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) d4[q] = make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
+            } else {
+#pragma unroll
+                for (uint32_t i = 0; i < kLaneSym; ++i)
+                    if (i < cur.cnt) dst[i] = static_cast<uint8_t>(o[i >> 2] >> (8 * (i & 3)));
+            }
+        }
+        HUFF_STAMP(ws, 6);
+        ws.flush(a.stamps, task);
+        if (!more) break;
+        // the next stage has landed (and nn's entries): all but the row stores
+        if (plain) __builtin_amdgcn_s_waitcnt(0x0f74);  // vmcnt(4)
+        else __builtin_amdgcn_s_waitcnt(0x0f70);
+        wave_sync();  // this stage's reads are done before a DMA rewrites it
+        task = ntask;
+        cur = nxt;
+        nxt_raw = nn_raw;
+        odd = !odd;
+    }
+}
+
+// the DMA build's stage per buffer: 3 KiB (two halves of output rows) for
+// streams of <= kSmallStageBits bits per symbol, else 4.5 KiB
+template <bool SKIP, bool PAD, uint32_t CAPB>
+__global__ __launch_bounds__(kThreads) void k_decode_dma(DecodeArgs a) {
+    decode_dma_body<SKIP, PAD, CAPB>(a);
+}
+
 // Production kernels. The register allocation is the compiler's, with one
 // floor for every swizzled-stage (PAD) body, the plain and the index-free skip
 // build alike (kPadWaves waves per SIMD); `make` rejects any build in which a
@@ -597,6 +844,21 @@ hipError_t launch_decode_fixed(const DecodeArgs& a, hipStream_t s) {
         return hipErrorInvalidValue;
     K kern = small ? small_kern
                    : (a.skip_packed ? skip_table[slow][pad] : table[a.check_mode][slow][pad]);
+    size_t lds_bytes = lds;
+    // (the index forms it reads: compact marks / the compact restart index)
+    const bool dma = a.dma_stage && !a.check_mode && !slow &&
+                     (a.skip_packed ? a.mark32 != nullptr : (a.sub16 != nullptr && !a.sub_abs64));
+    if (dma) {  // k_decode_dma: persistent waves, two stage buffers each
+        static const K dma_table[2][2][2] = {
+            {{k_decode_dma<false, false, kInCap>, k_decode_dma<false, false, kInCapSmall>},
+             {k_decode_dma<false, true, kInCap>, k_decode_dma<false, true, kInCapSmall>}},
+            {{k_decode_dma<true, false, kInCap>, k_decode_dma<true, false, kInCapSmall>},
+             {k_decode_dma<true, true, kInCap>, k_decode_dma<true, true, kInCapSmall>}}};
+        const bool sm = a.small_stage != 0;
+        kern = dma_table[a.skip_packed ? 1 : 0][pad][sm];
+        const size_t tab_words = ((size_t(1) << a.stab_bits) + 1) / 2;
+        lds_bytes = ((tab_words + 3) & ~size_t(3)) * 4 + size_t(kWaves) * 2 * (sm ? kInCapSmall : kInCap);
+    }
     const uint64_t want = (ntasks + kWaves - 1) / kWaves;
     // production: one task per wave (a one-shot grid, as the byte map's): the
     // dispatcher refills the CUs as waves finish — same-box A/B against the
@@ -610,14 +872,14 @@ hipError_t launch_decode_fixed(const DecodeArgs& a, hipStream_t s) {
     constexpr bool oneshot = true;
 #endif
     uint64_t cap = want;
-    if (a.check_mode || !oneshot) {  // persistent grid = resident workgroups (registers and LDS both limit)
+    if (a.check_mode || !oneshot || dma) {  // persistent grid = resident workgroups (registers and LDS both limit)
         int per_cu = 0;
-        const hipError_t err = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kThreads, lds);
+        const hipError_t err = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kThreads, lds_bytes);
         if (err != hipSuccess || per_cu < 1) per_cu = 1;
         cap = uint64_t(a.cu_count ? a.cu_count : 256) * per_cu;
     }
     const uint32_t grid = static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>(want, cap)));
-    launch_k(kern, dim3(grid), dim3(kThreads), lds, s, a);
+    launch_k(kern, dim3(grid), dim3(kThreads), lds_bytes, s, a);
     return hipGetLastError();
 }
 

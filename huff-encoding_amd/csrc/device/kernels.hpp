@@ -133,6 +133,9 @@ struct DecodeArgs {
     // k_decode_fixed: the 3 KiB per-wave stage (8 workgroups per CU instead of
     // 6) for streams of at most kSmallStageBits bits per symbol (fixed_decode_small)
     uint32_t small_stage;
+    // k_decode_fixed: 1 = the persistent LDS-DMA build (decode_wave.hip
+    // k_decode_dma: the next task's input in flight while a task decodes)
+    uint32_t dma_stage;
     // k_decode_fixed self-check build (0: production kernel; 1: checked).
     // err: u32[8] mismatch count + first (task, lane, want, got)
     uint32_t check_mode;

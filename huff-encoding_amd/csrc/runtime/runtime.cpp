@@ -69,6 +69,13 @@ bool small_stage_enabled() {
     return !(e && *e == '0');
 }
 
+// HUFF_DMA_DECODE=1: the persistent LDS-DMA decoder (k_decode_dma; measured
+// 8-15 % slower than the one-shot register-staged one, profiles/r06/decode_bound/)
+uint32_t dma_decode_enabled() {
+    const char* e = std::getenv("HUFF_DMA_DECODE");  // read per call: tests flip it
+    return (e && *e == '1') ? 1u : 0u;
+}
+
 uint32_t decode_check_mode() {
     const char* e = std::getenv("HUFF_DEC_VARIANT");  // read per call: tests flip it
     if (!e) return 0;
@@ -952,6 +959,7 @@ huff::Status huff_enc::decode(const huff_tree* t, const uint8_t* d_comp, uint64_
     a.cu_count = static_cast<uint32_t>(ctx->cu_count);
     a.pad_stage = huff::dev::fixed_decode_pad(total_bits, n);
     a.small_stage = huff::small_stage_enabled() && huff::dev::fixed_decode_small(total_bits, n);
+    a.dma_stage = huff::dma_decode_enabled();
     a.stab = reinterpret_cast<const uint16_t*>(static_cast<const uint32_t*>(ctx->d_lut.p) + dt->soff);
     a.stab_bits = dt->sbits;
     a.n = n;
@@ -1611,6 +1619,7 @@ Status decode_indexless_dev(huff_ctx* ctx, const uint8_t* d_comp, uint64_t comp_
         d.cu_count = static_cast<uint32_t>(ctx->cu_count);
         d.pad_stage = dev::fixed_decode_pad(valid_bits, total);
         d.small_stage = small_stage_enabled() && dev::fixed_decode_small(valid_bits, total);
+        d.dma_stage = dma_decode_enabled();
         d.n = total;
         d.out = bounce ? static_cast<uint8_t*>(ctx->d_align.p) : out_at();
         d.check_mode = check;

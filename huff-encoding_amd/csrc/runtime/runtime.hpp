@@ -82,6 +82,7 @@ struct PackStamps {
 PackStamps& pack_stamps();
 // HUFF_SMALL_STAGE=0 keeps the decoders' 4.5 KiB stage for every stream
 bool small_stage_enabled();
+uint32_t dma_decode_enabled();
 // HUFF_DEC_VARIANT=11 -> k_decode_fixed's self-checking build (mode 1; else 0)
 uint32_t decode_check_mode();
 
