@@ -96,8 +96,8 @@ def index_free_cases(O, rng):
 
 @pytest.fixture(params=["sync", "pipeline"])
 def decoder(request, monkeypatch):
-    """the one-pass decoder (syncdec.hip, the default where it applies) and
-    the pipeline (indexless.hip: HUFF_SYNC_DECODE=0) on the same cases"""
+    """the one-pass decoder (syncdec.hip, opt-in: HUFF_SYNC_DECODE=1) and the
+    pipeline (indexless.hip, the default: HUFF_SYNC_DECODE=0) on the same cases"""
     monkeypatch.setenv("HUFF_SYNC_DECODE", "1" if request.param == "sync" else "0")
     return request.param
 
@@ -302,3 +302,34 @@ def test_capacity_below_count(H, O, ctx, decoder):
     res = out.cpu().numpy()
     assert np.array_equal(res[:n], host)
     assert (res[n:] == 0xAB).all()
+
+
+@pytest.mark.parametrize("kind,seed", [("zipf", 0x5EED0002), ("text", 0x5EED0005), ("uniform", 0x5EED0001)])
+def test_dma_decoder(H, O, ctx, cases, kind, seed, monkeypatch):
+    """the opt-in persistent LDS-DMA decoder (decode_wave.hip k_decode_dma,
+    HUFF_DMA_DECODE=1; measured slower): the indexed decode of a
+    device job (16 MiB + a ragged tail; uniform through the general kernels)
+    and, for the first workload, every index-free case"""
+    import torch
+
+    monkeypatch.setenv("HUFF_DMA_DECODE", "1")
+    monkeypatch.setenv("HUFF_SYNC_DECODE", "0")
+    if kind == "uniform":
+        monkeypatch.setenv("HUFF_DISABLE_FIXED8", "1")
+    from huff_coding import device as D
+
+    n = (1 << 24) + 12345
+    x = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
+    D.generate(ctx, kind, seed, x.data_ptr(), n, cdf=D.zipf_cdf(1.2) if kind == "zipf" else None)
+    job = H.EncodeJob(ctx, x.data_ptr(), n)
+    tree = H.HuffTree.from_weights(H.ByteWeights.from_array(job.hist()))
+    bits = job.bits(tree)
+    out = torch.zeros((bits + 7) // 8 + 64, dtype=torch.uint8, device="cuda")
+    assert job.pack(tree, out.data_ptr(), out.numel()) == bits
+    dec = torch.empty(n + 64, dtype=torch.uint8, device="cuda")
+    job.decode(tree, out.data_ptr(), dec.data_ptr())
+    torch.cuda.synchronize()
+    assert torch.equal(dec[:n], x[:n])
+    if kind == "zipf":
+        for name, data in cases:
+            roundtrip(H, O, ctx, data)
