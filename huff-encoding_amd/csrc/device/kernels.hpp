@@ -322,7 +322,6 @@ struct WideDecArgs {
     uint32_t cu_count;
     uint32_t max_len;             // longest code (<= 32: wdecode.hip)
     uint32_t stage_bytes;         // wdecode.hip: LDS stage per wave (a multiple of 16)
-    uint32_t pair_stage_bytes;    // wdecode.hip k_wdec_pair: the same for two tasks (0: no pair decoder)
     uint64_t n;
     uint8_t* out;                 // n * width bytes
 };

@@ -19,7 +19,6 @@
 //
 // Roofline: HBM-bound in principle; ceil(bits/8) read + n W written + the
 // restart index (4 B per 64 letters).
-#include <cstdlib>
 #include <type_traits>
 
 #include "bitreader.hpp"
@@ -119,56 +118,51 @@ struct Lane {
 // | s, offset in bits 8..31) continues at level 2 with the next s bits. Both
 // reads are made by every lane (a lane with a level-1 leaf re-reads entry 0:
 // one broadcast address), so lanes never diverge.
-// letter i of a part (i a compile-time constant in the unrolled callers)
-template <uint32_t W, bool TWO, bool R1, uint32_t N, class Words>
-__device__ __forceinline__ void decode_step(Lane<W>& s, const Words& src, uint32_t (&o)[N], uint32_t i,
-                                            const EntryT<W>* __restrict__ tab, uint32_t K1,
-                                            const uint8_t* __restrict__ letters, bool leaf4) {
-    if (R1 || (i & 1) == 0) {  // refill
-        s.buf |= (static_cast<uint64_t>(s.nextw) << 32) >> (s.X & 63);
-        s.rp += (s.X & 32) ? 0u : 1u;
-        s.X |= 32;
-        s.nextw = src(s.rp);
-    }
-    const uint32_t top = static_cast<uint32_t>(s.buf >> 32);
-    EntryT<W> e = tab[top >> (32 - K1)];
-    if constexpr (TWO) {
-        const uint32_t lo = static_cast<uint32_t>(e);
-        const bool ptr = (lo & kSlowFlag) != 0;
-        const uint32_t sw = lo & 63u;
-        const uint32_t i2 = ptr ? (lo >> 8) + ((top << K1) >> (32 - sw)) : 0u;
-        const EntryT<W> e2 = tab[i2];
-        e = ptr ? e2 : e;
-    }
-    const uint32_t len = static_cast<uint32_t>(e) & 63u;
-    // (8- and 16-byte letters: the split shift keeps the build clear of
-    // the shift hazard since the skip loop was added; others unchanged)
-    if constexpr (W >= 8) s.buf = shl_window(s.buf, len);
-    else s.buf <<= len;
-    s.X -= len;
-    const uint32_t v = payload<W>(e);
-    if constexpr (W == 1) {
-        if ((i & 3) == 0) o[i >> 2] = v;
-        else o[i >> 2] |= v << (8 * (i & 3));
-    } else if constexpr (W == 2) {
-        if ((i & 1) == 0) o[i >> 1] = v;
-        else o[i >> 1] |= v << 16;
-    } else if constexpr (W == 4) {
-        o[i] = leaf4 ? reinterpret_cast<const uint32_t*>(letters)[v] : v;
-    } else {
-        uint32_t d[W / 4];
-        leaf_letter<W>(letters, v, d);
-#pragma unroll
-        for (uint32_t k = 0; k < W / 4; ++k) o[i * (W / 4) + k] = d[k];
-    }
-}
-
 template <uint32_t W, uint32_t PL, bool TWO, bool R1, class Words>
 __device__ __forceinline__ void decode_part(Lane<W>& s, const Words& src, uint32_t (&o)[PL * W / 4 > 0 ? PL * W / 4 : 1],
                                             const EntryT<W>* __restrict__ tab, uint32_t K1,
                                             const uint8_t* __restrict__ letters, bool leaf4) {
+    auto refill = [&]() {
+        s.buf |= (static_cast<uint64_t>(s.nextw) << 32) >> (s.X & 63);
+        s.rp += (s.X & 32) ? 0u : 1u;
+        s.X |= 32;
+        s.nextw = src(s.rp);
+    };
 #pragma unroll
-    for (uint32_t i = 0; i < PL; ++i) decode_step<W, TWO, R1>(s, src, o, i, tab, K1, letters, leaf4);
+    for (uint32_t i = 0; i < PL; ++i) {
+        if (R1 || (i & 1) == 0) refill();
+        const uint32_t top = static_cast<uint32_t>(s.buf >> 32);
+        EntryT<W> e = tab[top >> (32 - K1)];
+        if constexpr (TWO) {
+            const uint32_t lo = static_cast<uint32_t>(e);
+            const bool ptr = (lo & kSlowFlag) != 0;
+            const uint32_t sw = lo & 63u;
+            const uint32_t i2 = ptr ? (lo >> 8) + ((top << K1) >> (32 - sw)) : 0u;
+            const EntryT<W> e2 = tab[i2];
+            e = ptr ? e2 : e;
+        }
+        const uint32_t len = static_cast<uint32_t>(e) & 63u;
+        // (8- and 16-byte letters: the split shift keeps the build clear of
+        // the shift hazard since the skip loop was added; others unchanged)
+        if constexpr (W >= 8) s.buf = shl_window(s.buf, len);
+        else s.buf <<= len;
+        s.X -= len;
+        const uint32_t v = payload<W>(e);
+        if constexpr (W == 1) {
+            if ((i & 3) == 0) o[i >> 2] = v;
+            else o[i >> 2] |= v << (8 * (i & 3));
+        } else if constexpr (W == 2) {
+            if ((i & 1) == 0) o[i >> 1] = v;
+            else o[i >> 1] |= v << 16;
+        } else if constexpr (W == 4) {
+            o[i] = leaf4 ? reinterpret_cast<const uint32_t*>(letters)[v] : v;
+        } else {
+            uint32_t d[W / 4];
+            leaf_letter<W>(letters, v, d);
+#pragma unroll
+            for (uint32_t k = 0; k < W / 4; ++k) o[i * (W / 4) + k] = d[k];
+        }
+    }
 }
 
 template <uint32_t W, class Words>
@@ -213,37 +207,6 @@ constexpr uint32_t part_letters() { return 64u / W; }
 // pieces XOR-swizzled by row: conflict-free ds_write_b128, as decode_wave.hip)
 __device__ __forceinline__ uint32_t row_piece(uint32_t r, uint32_t q) { return r * 64 + 16 * (q ^ ((r >> 1) & 3)); }
 
-// part p (64 B per lane) of a whole task's lanes to its output through the
-// wave's transpose rows (letters of <= 4 bytes: two halves of 32 rows), stored
-// through a buffer resource over the task's output: 32-bit offsets (64-bit
-// addresses per store held ~8 more registers)
-template <uint32_t W>
-__device__ __forceinline__ void part_rows(const uint32_t (&o)[16], uint8_t* rows, uint8_t* task_out, uint32_t lane,
-                                          uint32_t p) {
-    const auto ro = buf_rsrc(task_out, kTaskLetters * W);
-    constexpr uint32_t H = row_halves<W>(), RH = 64 / H;  // halves, rows per half
-#pragma unroll
-    for (uint32_t h = 0; h < H; ++h) {  // lanes [RH h, RH h + RH)
-        wave_order();  // the previous rows were read first
-        if (H == 1 || lane / RH == h) {
-#pragma unroll
-            for (uint32_t q = 0; q < 4; ++q)
-                *reinterpret_cast<uint4*>(rows + row_piece(lane % RH, q)) =
-                    make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
-        }
-        wave_order();
-#pragma unroll
-        for (uint32_t j = 0; j < RH / 16; ++j) {
-            const uint32_t r = 16 * j + (lane >> 2), q = lane & 3;
-            const uint4 v = *reinterpret_cast<const uint4*>(rows + row_piece(r, q));
-            u32x4_t w = {v.x, v.y, v.z, v.w};
-            __builtin_amdgcn_raw_buffer_store_b128(w, ro,
-                                                   static_cast<int>((RH * h + r) * (kWideRun * W) + p * 64 + 16 * q), 0,
-                                                   0);
-        }
-    }
-}
-
 // a full lane: 64 letters in parts of 64 B. ROWS (every lane of the wave
 // full, 16-B aligned output): each part goes through the wave's transpose
 // buffer, so a store instruction writes 16 lanes' parts as whole 64-B
@@ -279,7 +242,29 @@ __device__ __forceinline__ void lane_full(const Words& src, uint32_t rel, uint8_
                 }
                 continue;
             }
-            part_rows<W>(o, rows, task_out, lane, p);
+            // through a buffer resource over the task's output: 32-bit
+            // offsets (64-bit addresses per store held ~8 more registers)
+            const auto ro = buf_rsrc(task_out, kTaskLetters * W);
+            constexpr uint32_t H = row_halves<W>(), RH = 64 / H;  // halves, rows per half
+#pragma unroll
+            for (uint32_t h = 0; h < H; ++h) {  // lanes [RH h, RH h + RH)
+                wave_order();  // the previous rows were read first
+                if (H == 1 || lane / RH == h) {
+#pragma unroll
+                    for (uint32_t q = 0; q < 4; ++q)
+                        *reinterpret_cast<uint4*>(rows + row_piece(lane % RH, q)) =
+                            make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
+                }
+                wave_order();
+#pragma unroll
+                for (uint32_t j = 0; j < RH / 16; ++j) {
+                    const uint32_t r = 16 * j + (lane >> 2), q = lane & 3;
+                    const uint4 v = *reinterpret_cast<const uint4*>(rows + row_piece(r, q));
+                    u32x4_t w = {v.x, v.y, v.z, v.w};
+                    __builtin_amdgcn_raw_buffer_store_b128(
+                        w, ro, static_cast<int>((RH * h + r) * (kWideRun * W) + p * 64 + 16 * q), 0, 0);
+                }
+            }
             continue;
         }
         uint8_t* d = dst + p * PL * W;
@@ -314,18 +299,11 @@ __device__ __forceinline__ void lane_tail(const Words& src, uint32_t rel, uint32
     }
 }
 
-// The LDS a decoder workgroup shares: the table and the wide letters (when
-// LDS), then per wave its stage and transpose rows
-template <uint32_t W, bool LDS>
-struct WdecShared {
-    const EntryT<W>* tab;
-    const uint8_t* letters;
-    uint32_t* stage;
-    uint8_t* rows;
-};
-template <uint32_t W, bool LDS>
-__device__ __forceinline__ WdecShared<W, LDS> wdec_shared(const WideDecArgs& a, uint8_t* lds, uint32_t wave) {
-    const uint32_t t = threadIdx.x;
+template <uint32_t W, bool TWO, bool R1, bool LDS>
+__global__ __launch_bounds__((LDS ? max_waves<W>() : 4) * 64) void k_wdec_task(WideDecArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const uint32_t K1 = a.stab_bits;
+    const uint32_t t = threadIdx.x, lane = t & 63, wave = wave_index();
     // LDS: [the table][leaf letters (W >= 8, 4-byte leaves)] when LDS, then the waves' stages
     const uint32_t tab_bytes = LDS ? a.stab_bytes : 0u;
     const uint32_t let_bytes = LDS && leaf_letters<W>(a) ? (a.nleaves * W + 15) & ~15u : 0u;
@@ -336,200 +314,75 @@ __device__ __forceinline__ WdecShared<W, LDS> wdec_shared(const WideDecArgs& a, 
             reinterpret_cast<uint4*>(lds + tab_bytes)[i] = reinterpret_cast<const uint4*>(a.letters)[i];
     }
     __syncthreads();
-    WdecShared<W, LDS> s;
     // one pointer origin per instantiation (ds_read or global_load, never flat)
-    s.tab = LDS ? reinterpret_cast<const EntryT<W>*>(lds) : static_cast<const EntryT<W>*>(a.stab);
-    s.letters = LDS && leaf_letters<W>(a) ? lds + tab_bytes : a.letters;
-    uint8_t* wave_lds = lds + tab_bytes + let_bytes + wave * (a.stage_bytes + row_bytes<W>());
-    s.stage = reinterpret_cast<uint32_t*>(wave_lds);
-    s.rows = wave_lds + a.stage_bytes;
-    return s;
-}
-
-// A run's restart entry (its first bit; skip_packed: a boundary at or before
-// it and the codes to skip from there)
-__device__ __forceinline__ uint64_t run_entry(const WideDecArgs& a, uint64_t run) {
-    return a.sub_abs ? a.sub_abs[run] : a.chunk_start[run >> 8] + a.sub_bit[run];
-}
-// the staged range of tasks [t0, t1) of a wave: lane 0's start (lane_bit of
-// lane 0, skips removed) to the next task's start plus its skipped codes,
-// in 16-B pieces from byte b0; 0 pieces when it exceeds the stage
-__device__ __forceinline__ uint32_t wdec_range(const WideDecArgs& a, uint64_t lane_bit, uint64_t t1, uint64_t nruns,
-                                               uint32_t np_max, uint64_t* b0_out) {
-    const uint32_t f_lo = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(lane_bit)));
-    const uint32_t f_hi = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(lane_bit >> 32)));
-    const uint64_t first = (static_cast<uint64_t>(f_hi) << 32) | f_lo;
-    const uint64_t nrun = t1 * 64;
-    uint64_t end = nrun < nruns ? run_entry(a, nrun) : a.end_bit;
-    if (a.skip_packed && nrun < nruns)  // the next task's first letter lies within its skipped codes
-        end = (end & kSkipPosMask) + (end >> 48) * a.max_len;
-    const uint64_t b0 = (first >> 3) & ~15ull;
-    const uint64_t b1 = ((((end + 7) >> 3) + 32) + 15) & ~15ull;  // + the window's lookahead
-    *b0_out = b0;
-    return static_cast<uint32_t>(
-        __builtin_amdgcn_readfirstlane(static_cast<int>(b1 - b0 <= 16ull * np_max ? (b1 - b0) / 16 : 0)));
-}
-// np 16-B pieces from byte b0 into the wave's stage (byte-swapped words):
-// coalesced loads through a buffer resource clamped to the stream's last
-// dword (pieces past it read zero)
-__device__ __forceinline__ void wdec_stage(const WideDecArgs& a, uint64_t b0, uint32_t np, uint32_t* stage,
-                                           uint32_t lane) {
-    const uint64_t end4 = (a.comp_bytes + 3) & ~3ull;
-    const uint64_t avail = end4 > b0 ? end4 - b0 : 0;
-    const uint32_t nb = static_cast<uint32_t>(avail < 16ull * np ? avail : 16ull * np);
-    const auto rs = buf_rsrc(nb ? a.comp + b0 : a.comp, nb);
-    for (uint32_t p = lane; p < np; p += 64) {
-        const uint4 v = buf_ld16(rs, p * 16);
-        reinterpret_cast<uint4*>(stage)[p] = make_uint4(__builtin_bswap32(v.x), __builtin_bswap32(v.y),
-                                                        __builtin_bswap32(v.z), __builtin_bswap32(v.w));
-    }
-    wave_sync();
-}
-
-// one task of 4,096 letters by one wave
-template <uint32_t W, bool TWO, bool R1, bool LDS>
-__device__ __forceinline__ void wdec_one_task(const WideDecArgs& a, const WdecShared<W, LDS>& sh, uint64_t task,
-                                              uint32_t lane, uint64_t nruns, uint32_t np_max, bool aligned) {
-    const uint32_t K1 = a.stab_bits;
+    const EntryT<W>* tab = LDS ? reinterpret_cast<const EntryT<W>*>(lds) : static_cast<const EntryT<W>*>(a.stab);
+    const uint8_t* letters = LDS && leaf_letters<W>(a) ? lds + tab_bytes : a.letters;
     const bool leaf4 = W == 4 && a.w4_leaf;
-    const uint64_t run = task * 64 + lane;
-    const uint64_t l0 = run * kWideRun;
-    const uint32_t cnt = l0 >= a.n ? 0u : static_cast<uint32_t>(a.n - l0 < kWideRun ? a.n - l0 : kWideRun);
-    uint64_t lane_bit = !cnt ? 0 : run_entry(a, run);
-    uint32_t skip = 0;
-    if (a.skip_packed) {
-        skip = static_cast<uint32_t>(lane_bit >> 48);
-        lane_bit &= kSkipPosMask;
-    }
-    uint64_t b0;
-    const uint32_t np = wdec_range(a, lane_bit, task + 1, nruns, np_max, &b0);
-    uint8_t* dst = a.out + l0 * W;
-    // the transpose needs every lane of the task (wave-uniform)
-    const bool whole = (task + 1) * kTaskLetters <= a.n && aligned;
-    uint8_t* trows = whole ? sh.rows : nullptr;
-    uint8_t* task_out = a.out + task * kTaskLetters * W;
-    if (np) {
-        wdec_stage(a, b0, np, sh.stage, lane);
-        const StageWords src{sh.stage};
-        const uint32_t rel = static_cast<uint32_t>(lane_bit - b0 * 8);
-        if (cnt == kWideRun)
-            lane_full<W, TWO, R1>(src, rel, dst, sh.tab, K1, sh.letters, aligned, trows, task_out, lane, skip, leaf4);
-        else if (cnt)
-            lane_tail<W, TWO, R1>(src, rel, cnt, dst, sh.tab, K1, sh.letters, skip, leaf4);
-        wave_sync();  // the stage is reused by the next task
-    } else {  // longer than the stage: straight from global memory
-        const GlobalWords src{a.comp, a.comp_bytes, (lane_bit >> 5)};
-        const uint32_t grel = static_cast<uint32_t>(lane_bit & 31);
-        if (cnt == kWideRun)
-            lane_full<W, TWO, R1>(src, grel, dst, sh.tab, K1, sh.letters, aligned, trows, task_out, lane, skip, leaf4);
-        else if (cnt)
-            lane_tail<W, TWO, R1>(src, grel, cnt, dst, sh.tab, K1, sh.letters, skip, leaf4);
-    }
-}
-
-template <uint32_t W, bool TWO, bool R1, bool LDS>
-__global__ __launch_bounds__((LDS ? max_waves<W>() : 4) * 64) void k_wdec_task(WideDecArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    const uint32_t lane = threadIdx.x & 63, wave = wave_index();
-    const WdecShared<W, LDS> sh = wdec_shared<W, LDS>(a, lds, wave);
+    uint8_t* wave_lds = lds + tab_bytes + let_bytes + wave * (a.stage_bytes + row_bytes<W>());
+    uint32_t* stage = reinterpret_cast<uint32_t*>(wave_lds);
+    uint8_t* rows = wave_lds + a.stage_bytes;
     const bool aligned = (reinterpret_cast<uintptr_t>(a.out) & 15) == 0;
     const uint64_t nruns = (a.n + kWideRun - 1) / kWideRun;
     const uint64_t ntasks = (a.n + kTaskLetters - 1) / kTaskLetters;
     const uint32_t np_max = a.stage_bytes / 16;
     const uint32_t waves = blockDim.x / 64;
     for (uint64_t task = static_cast<uint64_t>(blockIdx.x) * waves + wave; task < ntasks;
-         task += static_cast<uint64_t>(gridDim.x) * waves)
-        wdec_one_task<W, TWO, R1, LDS>(a, sh, task, lane, nruns, np_max, aligned);
-}
-
-// ---------------------------------------------------------------------------
-// k_wdec_pair (letters of <= 4 bytes, table in LDS): TWO tasks per wave, lane
-// l decoding run l of both, its two letter chains interleaved letter by
-// letter. A letter is a chain of dependent LDS reads (the level-1 entry, the
-// level-2 entry, the window's refill), and at the 4 waves per SIMD the
-// one-task decoder's registers allow, its SIMDs wait on that chain (PMC, round
-// 5: 66 % of wave cycles waiting, VALU ~36 % and LDS ~40 % busy); two
-// independent chains per lane at 3 waves per SIMD keep 1.5x as many lookups
-// in flight. The pair's compressed range (task 2j's first bit to task 2j+2's)
-// is one contiguous stage; a pair that is not whole, or whose range exceeds
-// the stage, runs as two single tasks.
-// ---------------------------------------------------------------------------
-#ifndef HUFF_WPAIR_WAVES
-#define HUFF_WPAIR_WAVES 12
-#endif
-constexpr int kPairWaves = HUFF_WPAIR_WAVES;
-#ifndef HUFF_WPAIR_SCHED
-#define HUFF_WPAIR_SCHED 0
-#endif
-constexpr uint32_t kPairSched = HUFF_WPAIR_SCHED;
-
-template <uint32_t W, bool TWO, bool R1>
-__device__ __forceinline__ void lane_pair(const StageWords& src, uint32_t relA, uint32_t relB, const EntryT<W>* tab,
-                                          uint32_t K1, const uint8_t* letters, uint8_t* rows, uint8_t* outA,
-                                          uint8_t* outB, uint32_t lane, uint32_t skipA, uint32_t skipB, bool leaf4) {
-    constexpr uint32_t PL = part_letters<W>();
-    static_assert(PL * W / 4 == 16, "64-B parts");
-    Lane<W> sA, sB;
-    lane_init<W>(sA, src, relA);
-    lane_init<W>(sB, src, relB);
-    lane_skip<W, TWO>(sA, src, tab, K1, skipA);
-    lane_skip<W, TWO>(sB, src, tab, K1, skipB);
-    for (uint32_t p = 0; p < kWideRun / PL; ++p) {
-        uint32_t oA[16], oB[16];
-#pragma unroll
-        for (uint32_t i = 0; i < PL; ++i) {
-            decode_step<W, TWO, R1>(sA, src, oA, i, tab, K1, letters, leaf4);
-            decode_step<W, TWO, R1>(sB, src, oB, i, tab, K1, letters, leaf4);
-            // HUFF_WPAIR_SCHED=k (A/B builds): a scheduling barrier every k letters
-            if (kPairSched && (i % (kPairSched ? kPairSched : 1u)) == kPairSched - 1) __builtin_amdgcn_sched_barrier(0);
+         task += static_cast<uint64_t>(gridDim.x) * waves) {
+        const uint64_t run = task * 64 + lane;
+        const uint64_t l0 = run * kWideRun;
+        const uint32_t cnt = l0 >= a.n ? 0u : static_cast<uint32_t>(a.n - l0 < kWideRun ? a.n - l0 : kWideRun);
+        uint64_t lane_bit = !cnt ? 0 : (a.sub_abs ? a.sub_abs[run] : a.chunk_start[run >> 8] + a.sub_bit[run]);
+        uint32_t skip = 0;
+        if (a.skip_packed) {
+            skip = static_cast<uint32_t>(lane_bit >> 48);
+            lane_bit &= kSkipPosMask;
         }
-        part_rows<W>(oA, rows, outA, lane, p);
-        part_rows<W>(oB, rows, outB, lane, p);
-    }
-}
-
-template <uint32_t W, bool TWO, bool R1>
-__global__ __launch_bounds__(kPairWaves * 64) void k_wdec_pair(WideDecArgs a) {
-    static_assert(W <= 4, "two 64-B parts per step fit the registers of <= 4-byte letters");
-    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    const uint32_t lane = threadIdx.x & 63, wave = wave_index();
-    const WdecShared<W, true> sh = wdec_shared<W, true>(a, lds, wave);
-    const uint32_t K1 = a.stab_bits;
-    const bool leaf4 = W == 4 && a.w4_leaf;
-    const bool aligned = (reinterpret_cast<uintptr_t>(a.out) & 15) == 0;
-    const uint64_t nruns = (a.n + kWideRun - 1) / kWideRun;
-    const uint64_t ntasks = (a.n + kTaskLetters - 1) / kTaskLetters;
-    const uint64_t npairs = (ntasks + 1) / 2;
-    const uint32_t np_max = a.stage_bytes / 16;
-    // the pair index and its stride in SGPRs (from VGPRs, the stride spilled)
-    const uint32_t waves = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(blockDim.x / 64)));
-    const uint64_t stride = static_cast<uint64_t>(gridDim.x) * waves;
-    for (uint64_t pair = static_cast<uint64_t>(blockIdx.x) * waves + wave; pair < npairs; pair += stride) {
-        const uint64_t tA = 2 * pair, tB = tA + 1;
-        // whole pair (wave-uniform): every lane of both tasks has 64 letters
-        if ((tB + 1) * kTaskLetters <= a.n && aligned) {
-            uint64_t bitA = run_entry(a, tA * 64 + lane), bitB = run_entry(a, tB * 64 + lane);
-            uint32_t skipA = 0, skipB = 0;
-            if (a.skip_packed) {
-                skipA = static_cast<uint32_t>(bitA >> 48);
-                skipB = static_cast<uint32_t>(bitB >> 48);
-                bitA &= kSkipPosMask;
-                bitB &= kSkipPosMask;
+        // the task's range: lane 0's start to the next task's start
+        const uint32_t f_lo = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(lane_bit)));
+        const uint32_t f_hi = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(lane_bit >> 32)));
+        const uint64_t first = (static_cast<uint64_t>(f_hi) << 32) | f_lo;
+        const uint64_t nrun = (task + 1) * 64;
+        uint64_t end = nrun < nruns ? (a.sub_abs ? a.sub_abs[nrun] : a.chunk_start[nrun >> 8] + a.sub_bit[nrun])
+                                    : a.end_bit;
+        if (a.skip_packed && nrun < nruns)  // the next task's first letter lies within its skipped codes
+            end = (end & kSkipPosMask) + (end >> 48) * a.max_len;
+        const uint64_t b0 = (first >> 3) & ~15ull;
+        const uint64_t b1 = ((((end + 7) >> 3) + 32) + 15) & ~15ull;  // + the window's lookahead
+        const uint32_t np = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(
+            static_cast<int>(b1 - b0 <= 16ull * np_max ? (b1 - b0) / 16 : 0)));
+        uint8_t* dst = a.out + l0 * W;
+        // the transpose needs every lane of the task (wave-uniform)
+        const bool whole = (task + 1) * kTaskLetters <= a.n && aligned;
+        uint8_t* trows = whole ? rows : nullptr;
+        uint8_t* task_out = a.out + task * kTaskLetters * W;
+        if (np) {
+            // stage: coalesced 16-B pieces through a buffer resource clamped to
+            // the stream's last dword (pieces past it read zero)
+            const uint64_t end4 = (a.comp_bytes + 3) & ~3ull;
+            const uint64_t avail = end4 > b0 ? end4 - b0 : 0;
+            const uint32_t nb = static_cast<uint32_t>(avail < 16ull * np ? avail : 16ull * np);
+            const auto rs = buf_rsrc(nb ? a.comp + b0 : a.comp, nb);
+            for (uint32_t p = lane; p < np; p += 64) {
+                const uint4 v = buf_ld16(rs, p * 16);
+                reinterpret_cast<uint4*>(stage)[p] = make_uint4(__builtin_bswap32(v.x), __builtin_bswap32(v.y),
+                                                                __builtin_bswap32(v.z), __builtin_bswap32(v.w));
             }
-            uint64_t b0;
-            const uint32_t np = wdec_range(a, bitA, tB + 1, nruns, np_max, &b0);
-            if (np) {
-                wdec_stage(a, b0, np, sh.stage, lane);
-                lane_pair<W, TWO, R1>(StageWords{sh.stage}, static_cast<uint32_t>(bitA - b0 * 8),
-                                      static_cast<uint32_t>(bitB - b0 * 8), sh.tab, K1, sh.letters, sh.rows,
-                                      a.out + tA * kTaskLetters * W, a.out + tB * kTaskLetters * W, lane, skipA,
-                                      skipB, leaf4);
-                wave_sync();  // the stage is reused by the next pair
-                continue;
-            }
+            wave_sync();
+            const StageWords src{stage};
+            const uint32_t rel = static_cast<uint32_t>(lane_bit - b0 * 8);
+            if (cnt == kWideRun)
+                lane_full<W, TWO, R1>(src, rel, dst, tab, K1, letters, aligned, trows, task_out, lane, skip, leaf4);
+            else if (cnt)
+                lane_tail<W, TWO, R1>(src, rel, cnt, dst, tab, K1, letters, skip, leaf4);
+            wave_sync();  // the stage is reused by the next task
+        } else {  // longer than the stage: straight from global memory
+            const GlobalWords src{a.comp, a.comp_bytes, (lane_bit >> 5)};
+            const uint32_t grel = static_cast<uint32_t>(lane_bit & 31);
+            if (cnt == kWideRun)
+                lane_full<W, TWO, R1>(src, grel, dst, tab, K1, letters, aligned, trows, task_out, lane, skip, leaf4);
+            else if (cnt)
+                lane_tail<W, TWO, R1>(src, grel, cnt, dst, tab, K1, letters, skip, leaf4);
         }
-        for (uint64_t t = tA; t <= tB && t < ntasks; ++t)
-            wdec_one_task<W, TWO, R1, true>(a, sh, t, lane, nruns, np_max, aligned);
     }
 }
 
@@ -557,41 +410,6 @@ hipError_t launch_as(const WideDecArgs& a, size_t shared, uint32_t waves, hipStr
     return hipGetLastError();
 }
 
-// the pair decoder: pair_stage_bytes per wave, kPairWaves waves beside the
-// table (fewer when the LDS holds fewer, at least 8)
-template <uint32_t W>
-hipError_t launch_pair(WideDecArgs a, size_t shared, hipStream_t s) {
-    using Kern = void (*)(WideDecArgs);
-    const bool two = a.max_len > a.stab_bits;
-    const bool r1 = a.max_len > 16;
-    const Kern k = !two ? k_wdec_pair<W, false, false> : (r1 ? k_wdec_pair<W, true, true> : k_wdec_pair<W, true, false>);
-    a.stage_bytes = a.pair_stage_bytes;
-    const size_t per_wave = a.stage_bytes + row_bytes<W>();
-    size_t waves = (160 * 1024 - shared) / per_wave;
-    waves = waves > size_t(kPairWaves) ? size_t(kPairWaves) : waves;
-    const size_t lds = shared + waves * per_wave;
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    if (e != hipSuccess) return e;
-    int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, static_cast<int>(waves) * 64, lds) != hipSuccess ||
-        per_cu < 1)
-        per_cu = 1;
-    const uint64_t npairs = ((a.n + kTaskLetters - 1) / kTaskLetters + 1) / 2;
-    const uint64_t want = (npairs + waves - 1) / waves;
-    const uint64_t cap = uint64_t(a.cu_count ? a.cu_count : 256) * per_cu;
-    const uint32_t grid = static_cast<uint32_t>(want < cap ? want : cap);
-    launch_k(k, dim3(grid), dim3(static_cast<uint32_t>(waves) * 64), lds, s, a);
-    return hipGetLastError();
-}
-
-// HUFF_WIDE_PAIR (read per call): 0 = the one-task decoder for every width
-// (A/B), 2 = the pair decoder at any size (tests), else by size
-int pair_mode() {
-    const char* e = std::getenv("HUFF_WIDE_PAIR");
-    return !e || !e[0] ? 1 : e[0] == '0' ? 0 : e[0] == '2' ? 2 : 1;
-}
-
 // the table (and wide letters) in LDS when they fit: one copy per workgroup,
 // with as many waves beside it as the LDS holds (4..16)
 template <uint32_t W>
@@ -599,15 +417,6 @@ hipError_t by_place(const WideDecArgs& a, hipStream_t s) {
     constexpr size_t kLds = 160 * 1024;
     const size_t tab = a.stab_bytes;
     const size_t let = leaf_letters<W>(a) ? (static_cast<size_t>(a.nleaves) * W + 15) & ~size_t(15) : 0;
-    if constexpr (W <= 4) {
-        // at least 8 waves beside the table, and enough pairs to fill the chip (4,096 tasks)
-        const size_t pair_wave = a.pair_stage_bytes + row_bytes<W>();
-        const uint64_t ntasks = (a.n + kTaskLetters - 1) / kTaskLetters;
-        const int mode = pair_mode();
-        if (a.pair_stage_bytes && mode && tab + let <= 96 * 1024 && tab + let + 8 * pair_wave <= kLds &&
-            (ntasks >= 4096 || mode == 2))
-            return launch_pair<W>(a, tab + let, s);
-    }
     const size_t per_wave = a.stage_bytes + row_bytes<W>();
     if (tab + let <= 96 * 1024 && tab + let + 4 * per_wave <= kLds) {
         size_t waves = (kLds - tab - let) / per_wave;

@@ -191,11 +191,6 @@ Status huff_wenc::decode(const huff_wtree* t, const uint8_t* d_comp, uint64_t co
         const double want = 1.25 * bits_per * huff::dev::kWideRun * 64 / 8 + 96;
         uint32_t sb = static_cast<uint32_t>(want < 2048 ? 2048 : (want > 16384 ? 16384 : want));
         a.stage_bytes = (sb + 15) & ~15u;
-        // two tasks per wave (k_wdec_pair): a pair's range varies less, a
-        // tenth of headroom
-        const double want2 = 1.1 * bits_per * huff::dev::kWideRun * 128 / 8 + 96;
-        const uint32_t sb2 = static_cast<uint32_t>(want2 < 4096 ? 4096 : (want2 > 24576 ? 24576 : want2));
-        a.pair_stage_bytes = (sb2 + 15) & ~15u;
         return ctx->timed("wdecode", [&] { return huff::dev::launch_wide_decode_task(a, s); });
     }
     if (skip_packed) return Status::err(HUFF_E_INVALID_ARG, "skip marks need the task decoder (codes <= 32 bits)");

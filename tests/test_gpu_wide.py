@@ -410,50 +410,3 @@ def test_index_free_capacity_below_count(W, O, ctx):
     res = out.cpu().numpy()
     assert np.array_equal(res[:n], letters)
     assert (res[n:] == 0x5A5A).all()
-
-
-PAIR_LENGTHS = [1, 4095, 4096, 8191, 8192, 8193, 3 * 4096, 3 * 4096 + 5, 5 * 8192 + 64 * 7 + 3, 400_003]
-
-
-@pytest.mark.parametrize("pair", ["auto", "forced", "off"])
-@pytest.mark.parametrize("dtype", [np.uint8, np.int16, np.uint32])
-def test_pair_decoder(W, O, ctx, dtype, pair, monkeypatch):
-    """k_wdec_pair (two tasks per wave, two letter chains per lane) against the
-    one-task decoder and the input: HUFF_WIDE_PAIR=2 runs it at every size
-    (whole pairs, a partial last pair and an odd last task take the one-task
-    path inside it), =0 never; restart-index and index-free containers, Zipf
-    codes and 17-24-bit codes (a refill before every code, level-2 entries)"""
-    if pair == "forced":
-        monkeypatch.setenv("HUFF_WIDE_PAIR", "2")
-    elif pair == "off":
-        monkeypatch.setenv("HUFF_WIDE_PAIR", "0")
-    rng = np.random.default_rng(np.dtype(dtype).itemsize * 31 + len(pair))
-    fib = [1, 1]
-    while len(fib) < 25:
-        fib.append(fib[-1] + fib[-2])
-    pf = np.array(fib, np.float64) ** 0.5  # flatter than the weights: long codes are frequent
-    tfib = W.WideTree.from_weights([(3 + 5 * i, f) for i, f in enumerate(fib)], dtype)
-    for n in PAIR_LENGTHS:
-        zipf = zipf_letters(rng, n, dtype, k=50 if dtype == np.uint8 else 3000)
-        deep = (3 + 5 * rng.choice(25, n, p=pf / pf.sum())).astype(dtype)
-        for letters, t in ((zipf, None), (deep, tfib)):
-            cd = W.compress(letters, ctx) if t is None else W.compress_with_tree(letters, t, ctx)
-            assert np.array_equal(W.decompress(cd, ctx), letters), (dtype, n)
-            back_cd = W.WideCompressData.try_from_bytes(cd.to_bytes(), dtype)
-            assert not back_cd.has_index()
-            assert np.array_equal(W.decompress(back_cd, ctx), letters), (dtype, n)
-
-
-@pytest.mark.parametrize("dtype", [np.uint32])
-def test_pair_decoder_leaf_entries(W, O, ctx, dtype, monkeypatch):
-    """4-byte letters above 2^24: the pair decoder reads letters by leaf index
-    from LDS; forced at a size that is not a whole number of pairs"""
-    monkeypatch.setenv("HUFF_WIDE_PAIR", "2")
-    rng = np.random.default_rng(5)
-    alphabet = np.unique(rng.integers(1 << 25, 1 << 31, 3000, dtype=np.uint32))
-    p = 1.0 / np.arange(1, alphabet.size + 1) ** 1.1
-    letters = alphabet[rng.choice(alphabet.size, 5 * 8192 + 4096 + 17, p=p / p.sum())]
-    cd = W.compress(letters, ctx)
-    assert np.array_equal(W.decompress(cd, ctx), letters)
-    back_cd = W.WideCompressData.try_from_bytes(cd.to_bytes(), dtype)
-    assert np.array_equal(W.decompress(back_cd, ctx), letters)
