@@ -72,19 +72,6 @@ __device__ __forceinline__ uint32_t wave_scan_incl(uint32_t x) {
     return x;
 }
 
-// the largest value over the wave's 64 lanes, wave-uniform (in an SGPR):
-// DPP row shifts within the 16-lane rows, row broadcasts across them, then
-// lane 63 holds the maximum
-__device__ __forceinline__ uint32_t wave_max_u32(uint32_t x) {
-    x = max(x, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x111, 0xf, 0xf, false)));
-    x = max(x, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x112, 0xf, 0xf, false)));
-    x = max(x, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x114, 0xf, 0xf, false)));
-    x = max(x, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x118, 0xf, 0xf, false)));
-    x = max(x, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x142, 0xa, 0xf, false)));
-    x = max(x, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(x), 0x143, 0xc, 0xf, false)));
-    return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(x), 63));
-}
-
 // 16-byte streaming store
 __device__ __forceinline__ void st_nt(uint4* p, uint4 v) {
     u32x4_t w = {v.x, v.y, v.z, v.w};

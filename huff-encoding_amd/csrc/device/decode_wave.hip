@@ -53,12 +53,6 @@ static_assert(kChunk % kTaskSym == 0, "a task never straddles a chunk");
 #define HUFF_DEC_PAD_WAVES 5
 #endif
 constexpr bool kEarlyLoads = HUFF_DEC_EARLY_LOADS != 0;
-// the index-free skip codes in one wave-uniform predicated loop
-// (HUFF_SKIP_UNIFORM=0 for the A/B build with the per-lane loop)
-#ifndef HUFF_SKIP_UNIFORM
-#define HUFF_SKIP_UNIFORM 1
-#endif
-constexpr bool kSkipUniform = HUFF_SKIP_UNIFORM != 0;
 constexpr int kPadWaves = HUFF_DEC_PAD_WAVES;
 
 struct Task {
@@ -249,10 +243,7 @@ struct GlobalWords {
 // don't-care (X -= entry borrows only from them)
 // Invariant: the window's valid bits end at stream bit 32 rp, so the lane's
 // position after its 64 letters is 32 rp - nb (*end_rel, for the self-check).
-// UNI: every lane of the wave is active here (a whole task): the skip codes
-// may run as one wave-uniform loop (its trip count is a DPP maximum over
-// the 64 lanes, which would read stale registers of inactive lanes)
-template <bool SLOW, bool SKIP, bool UNI = false, class Words>
+template <bool SLOW, bool SKIP, class Words>
 __device__ __forceinline__ void decode_fixed64(const Words& src, uint32_t rel, uint32_t (&o)[16],
                                                const uint16_t* __restrict__ stab, uint32_t K,
                                                const uint32_t* __restrict__ glut, uint32_t Ks, uint32_t* end_rel,
@@ -323,46 +314,7 @@ __device__ __forceinline__ void decode_fixed64(const Words& src, uint32_t rel, u
 #ifdef HUFF_SKIP_EXPERIMENT  // timing only (wrong letters): 1 = no skip codes, 2 = the wave's max for all lanes
     if constexpr (SKIP) skip = HUFF_SKIP_EXPERIMENT == 1 ? 0u : __reduce_max_sync(~0ull, skip);
 #endif
-// one code consumed when k < skip, none past it (a select: the wave-uniform skip loop)
-#define FX_STEPM(k)                                                                           \
-    do {                                                                                      \
-        uint32_t e = stab[static_cast<uint32_t>(buf >> 32) >> (32 - K)];                      \
-        e = (k) < skip ? e : 0u;                                                              \
-        buf <<= (e & 63u);                                                                    \
-        X -= e;                                                                               \
-    } while (0)
-
-    if constexpr (SKIP && !SLOW && UNI && kSkipUniform) {
-        // codes before this lane's first letter, decoded and not kept, in a
-        // loop as long as the wave's largest skip: every lane runs it (its
-        // steps past its own skip consume nothing), four steps per trip with
-        // no exec-mask branch (the per-lane loop cost ~1.6x a letter per code:
-        // round-6 stamps, profiles/r06/budget/)
-        const uint32_t mx = wave_max_u32(skip);
-        if constexpr (HUFF_SKIP_UNIFORM == 2) {  // (A/B) exec-masked steps: finished lanes make no LDS reads
-            for (uint32_t j = 0; j < mx; j += 4) {
-                if (j < skip) {
-                    FX_REFILL();
-                    FX_STEP();
-                }
-                if (j + 1 < skip) FX_STEP();
-                if (j + 2 < skip) {
-                    FX_REFILL();
-                    FX_STEP();
-                }
-                if (j + 3 < skip) FX_STEP();
-            }
-        } else {
-            for (uint32_t j = 0; j < mx; j += 4) {
-                FX_REFILL();
-                FX_STEPM(j);
-                FX_STEPM(j + 1);
-                FX_REFILL();
-                FX_STEPM(j + 2);
-                FX_STEPM(j + 3);
-            }
-        }
-    } else if constexpr (SKIP) {  // codes before this lane's first letter: decoded, not kept
+    if constexpr (SKIP) {  // codes before this lane's first letter: decoded, not kept
         for (uint32_t j = skip; j >= 2; j -= 2) {
             FX_REFILL();
             FX_STEP();
@@ -382,22 +334,21 @@ __device__ __forceinline__ void decode_fixed64(const Words& src, uint32_t rel, u
     }
     *end_rel = 32 * rp - (X & 63u);
     if (rp_out) *rp_out = rp;  // dwords [0, rp) became valid bits; dword rp was read ahead
-#undef FX_STEPM
 #undef FX_STEP
 #undef FX_LOOKUP
 #undef FX_REFILL
 }
 
-template <bool SLOW, bool PAD, bool SKIP = false, bool UNI = false>
+template <bool SLOW, bool PAD, bool SKIP = false>
 __device__ __forceinline__ void decode_fixed64_stage(const uint32_t* stage, uint32_t rel, uint32_t (&o)[16],
                                                      const uint16_t* __restrict__ stab, uint32_t K,
                                                      const uint32_t* __restrict__ glut, uint32_t Ks,
                                                      uint32_t* end_rel, uint32_t skip = 0,
                                                      WaveStamps* ws = nullptr) {
     if constexpr (PAD)
-        decode_fixed64<SLOW, SKIP, UNI>(PaddedLdsWords{stage}, rel, o, stab, K, glut, Ks, end_rel, skip, ws);
+        decode_fixed64<SLOW, SKIP>(PaddedLdsWords{stage}, rel, o, stab, K, glut, Ks, end_rel, skip, ws);
     else
-        decode_fixed64<SLOW, SKIP, UNI>(LdsWords{stage}, rel, o, stab, K, glut, Ks, end_rel, skip, ws);
+        decode_fixed64<SLOW, SKIP>(LdsWords{stage}, rel, o, stab, K, glut, Ks, end_rel, skip, ws);
 }
 
 // fallback for a task whose compressed range exceeds the stage: a compact
@@ -561,7 +512,7 @@ __device__ __forceinline__ void decode_fixed_body(const DecodeArgs& a) {
         } else if (cur.nsym == kTaskSym) {  // wave-uniform: every lane has 64 letters
             uint32_t o[16];
             uint32_t e = 0;
-            decode_fixed64_stage<SLOW, PAD, SKIP, true>(stage, rel, o, stab, K, a.lut, a.lut_bits, &e, cur.skip, &ws);
+            decode_fixed64_stage<SLOW, PAD, SKIP>(stage, rel, o, stab, K, a.lut, a.lut_bits, &e, cur.skip, &ws);
             fx_check<CHECK>(a, cur, task, lane, cur.b0 * 8 + e, true);
             HUFF_STAMP(ws, 4);
             // transpose through the stage so every store instruction writes
@@ -754,10 +705,9 @@ __device__ __forceinline__ void decode_dma_body(const DecodeArgs& a) {
             uint32_t o[16];
             uint32_t e = 0;
             if constexpr (PAD)
-                decode_fixed64<false, SKIP, true>(PaddedLdsWordsBS{stage}, rel, o, stab, K, a.lut, a.lut_bits, &e, cur.skip,
-                                                  &ws);
+                decode_fixed64<false, SKIP>(PaddedLdsWordsBS{stage}, rel, o, stab, K, a.lut, a.lut_bits, &e, cur.skip, &ws);
             else
-                decode_fixed64<false, SKIP, true>(LdsWordsBS{stage}, rel, o, stab, K, a.lut, a.lut_bits, &e, cur.skip, &ws);
+                decode_fixed64<false, SKIP>(LdsWordsBS{stage}, rel, o, stab, K, a.lut, a.lut_bits, &e, cur.skip, &ws);
             HUFF_STAMP(ws, 4);
             wave_sync();  // the wave's stage reads are done
             uint4* d4 = reinterpret_cast<uint4*>(a.out + cur.sym0) + lane;
