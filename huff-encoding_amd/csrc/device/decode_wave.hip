@@ -243,7 +243,10 @@ struct GlobalWords {
 // don't-care (X -= entry borrows only from them)
 // Invariant: the window's valid bits end at stream bit 32 rp, so the lane's
 // position after its 64 letters is 32 rp - nb (*end_rel, for the self-check).
-template <bool SLOW, bool SKIP, class Words>
+// R: lookups per refill. After a refill the window holds >= 32 valid bits,
+// so R codes of <= 32 / R bits fit: 2 for codes of <= 16 bits, 3 for <= 10,
+// 4 for <= 8 (fewer stage reads per letter for shallow trees)
+template <bool SLOW, bool SKIP, int R = 2, class Words>
 __device__ __forceinline__ void decode_fixed64(const Words& src, uint32_t rel, uint32_t (&o)[16],
                                                const uint16_t* __restrict__ stab, uint32_t K,
                                                const uint32_t* __restrict__ glut, uint32_t Ks, uint32_t* end_rel,
@@ -326,11 +329,11 @@ __device__ __forceinline__ void decode_fixed64(const Words& src, uint32_t rel, u
         }
     }
     if (ws) HUFF_STAMP(*ws, 3);
+    static_assert(R >= 2 && R <= 4 && (!SLOW || R == 2), "2-4 lookups per refill (slow codes: 2)");
 #pragma unroll
-    for (int i = 0; i < 64; i += 2) {
-        FX_REFILL();
+    for (int i = 0; i < 64; ++i) {
+        if (i % R == 0) FX_REFILL();
         FX_LOOKUP(i);
-        FX_LOOKUP(i + 1);
     }
     *end_rel = 32 * rp - (X & 63u);
     if (rp_out) *rp_out = rp;  // dwords [0, rp) became valid bits; dword rp was read ahead
@@ -339,16 +342,16 @@ __device__ __forceinline__ void decode_fixed64(const Words& src, uint32_t rel, u
 #undef FX_REFILL
 }
 
-template <bool SLOW, bool PAD, bool SKIP = false>
+template <bool SLOW, bool PAD, bool SKIP = false, int R = 2>
 __device__ __forceinline__ void decode_fixed64_stage(const uint32_t* stage, uint32_t rel, uint32_t (&o)[16],
                                                      const uint16_t* __restrict__ stab, uint32_t K,
                                                      const uint32_t* __restrict__ glut, uint32_t Ks,
                                                      uint32_t* end_rel, uint32_t skip = 0,
                                                      WaveStamps* ws = nullptr) {
     if constexpr (PAD)
-        decode_fixed64<SLOW, SKIP>(PaddedLdsWords{stage}, rel, o, stab, K, glut, Ks, end_rel, skip, ws);
+        decode_fixed64<SLOW, SKIP, R>(PaddedLdsWords{stage}, rel, o, stab, K, glut, Ks, end_rel, skip, ws);
     else
-        decode_fixed64<SLOW, SKIP>(LdsWords{stage}, rel, o, stab, K, glut, Ks, end_rel, skip, ws);
+        decode_fixed64<SLOW, SKIP, R>(LdsWords{stage}, rel, o, stab, K, glut, Ks, end_rel, skip, ws);
 }
 
 // fallback for a task whose compressed range exceeds the stage: a compact
@@ -422,7 +425,7 @@ __device__ __forceinline__ void fx_check(const DecodeArgs& a, const Task& k, uin
     }
 }
 
-template <bool SLOW, bool PAD, bool CHECK, bool SKIP = false, bool SMALL = false>
+template <bool SLOW, bool PAD, bool CHECK, bool SKIP = false, bool SMALL = false, int R = 2>
 __device__ __forceinline__ void decode_fixed_body(const DecodeArgs& a) {
     constexpr uint32_t CAP = fx_stage_bytes<SMALL>();
     constexpr uint32_t kLoadRounds = load_rounds<SMALL>();
@@ -512,7 +515,7 @@ __device__ __forceinline__ void decode_fixed_body(const DecodeArgs& a) {
         } else if (cur.nsym == kTaskSym) {  // wave-uniform: every lane has 64 letters
             uint32_t o[16];
             uint32_t e = 0;
-            decode_fixed64_stage<SLOW, PAD, SKIP>(stage, rel, o, stab, K, a.lut, a.lut_bits, &e, cur.skip, &ws);
+            decode_fixed64_stage<SLOW, PAD, SKIP, R>(stage, rel, o, stab, K, a.lut, a.lut_bits, &e, cur.skip, &ws);
             fx_check<CHECK>(a, cur, task, lane, cur.b0 * 8 + e, true);
             HUFF_STAMP(ws, 4);
             // transpose through the stage so every store instruction writes
@@ -552,7 +555,7 @@ __device__ __forceinline__ void decode_fixed_body(const DecodeArgs& a) {
         } else if (cur.cnt) {
             uint32_t o[16];
             uint32_t e = 0;
-            decode_fixed64_stage<SLOW, PAD, SKIP>(stage, rel, o, stab, K, a.lut, a.lut_bits, &e, cur.skip);
+            decode_fixed64_stage<SLOW, PAD, SKIP, R>(stage, rel, o, stab, K, a.lut, a.lut_bits, &e, cur.skip);
             // a lane with fewer than 64 letters decodes past its end: only full lanes are checked
             fx_check<CHECK>(a, cur, task, lane, cur.b0 * 8 + e, cur.cnt == kLaneSym);
             if (cur.cnt == kLaneSym) {
@@ -781,9 +784,12 @@ __global__ __launch_bounds__(kThreads) void k_decode_dma(DecodeArgs a) {
 // 64-bit shift takes its amount from the last allocated VGPR
 // (tools/check_shift64.py, DESIGN.md §3 "The 64-bit shift hazard"), the
 // hardware hazard behind every wrong-letter build of rounds 1-2.
-template <bool PAD>
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(PAD ? kPadWaves : 1, 8))) void k_decode_fixed(DecodeArgs a) {
-    decode_fixed_body<false, PAD, false>(a);
+// (R > 2 bodies unfloored took 90-113 VGPRs, the scheduler hoisting the
+// lookups that the refills no longer separate: floored at the R = 2 body's
+// occupancy)
+template <bool PAD, int R = 2>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(PAD ? kPadWaves : (R > 2 ? 6 : 1), 8))) void k_decode_fixed(DecodeArgs a) {
+    decode_fixed_body<false, PAD, false, false, false, R>(a);
 }
 template <bool PAD>
 __global__ __launch_bounds__(kThreads) void k_decode_fixed_slow(DecodeArgs a) { decode_fixed_body<true, PAD, false>(a); }
@@ -797,9 +803,9 @@ __global__ __launch_bounds__(kThreads) void k_decode_fixed_chk(DecodeArgs a) { d
 // drops its skip codes
 // (forcing 7 or 8 waves per SIMD on the small-stage body spills 20 bytes
 // per lane: not built)
-template <bool SLOW, bool PAD, bool SMALL>
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(PAD && !SLOW ? kPadWaves : 1, 8))) void k_decode_fixed_skip(DecodeArgs a) {
-    decode_fixed_body<SLOW, PAD, false, true, SMALL>(a);
+template <bool SLOW, bool PAD, bool SMALL, int R = 2>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(PAD && !SLOW ? kPadWaves : (R > 2 ? (SMALL ? 7 : 6) : 1), 8))) void k_decode_fixed_skip(DecodeArgs a) {
+    decode_fixed_body<SLOW, PAD, false, true, SMALL, R>(a);
 }
 
 }  // namespace
@@ -812,6 +818,14 @@ size_t decode_fixed_lds_bytes(uint32_t stab_bits, bool small) {
     const size_t tab_words = ((1u << stab_bits) + 1) / 2;
     return ((tab_words + 3) & ~size_t(3)) * 4 +
            static_cast<size_t>(kWaves) * (small ? fx_stage_bytes<true>() : fx_stage_bytes<false>());
+}
+
+// lookups per refill for codes of at most max_len bits (decode_fixed64's R)
+static int lookups_per_refill(uint32_t max_len) {
+    const char* e = std::getenv("HUFF_DEC_REFILL");  // read per call: tests flip it
+    const int cap = e && e[0] >= '2' && e[0] <= '4' ? e[0] - '0' : 4;
+    const int r = max_len <= 8 ? 4 : max_len <= 10 ? 3 : 2;
+    return r < cap ? r : cap;
 }
 
 hipError_t launch_decode_fixed(const DecodeArgs& a, hipStream_t s) {
@@ -844,6 +858,17 @@ hipError_t launch_decode_fixed(const DecodeArgs& a, hipStream_t s) {
         return hipErrorInvalidValue;
     K kern = small ? small_kern
                    : (a.skip_packed ? skip_table[slow][pad] : table[a.check_mode][slow][pad]);
+    // shallow trees: 3 or 4 lookups per refill (the production builds;
+    // HUFF_DEC_REFILL=2 keeps two, for A/B)
+    const int r = lookups_per_refill(a.max_len);
+    if (!slow && !a.check_mode && r > 2) {
+        static const K fx_r[2][2] = {{k_decode_fixed<false, 3>, k_decode_fixed<true, 3>},
+                                     {k_decode_fixed<false, 4>, k_decode_fixed<true, 4>}};
+        static const K skip_r[2][2] = {{k_decode_fixed_skip<false, false, false, 3>, k_decode_fixed_skip<false, true, false, 3>},
+                                       {k_decode_fixed_skip<false, false, false, 4>, k_decode_fixed_skip<false, true, false, 4>}};
+        static const K small_r[2] = {k_decode_fixed_skip<false, false, true, 3>, k_decode_fixed_skip<false, false, true, 4>};
+        kern = small ? small_r[r - 3] : (a.skip_packed ? skip_r[r - 3][pad] : fx_r[r - 3][pad]);
+    }
     size_t lds_bytes = lds;
     // (the index forms it reads: compact marks / the compact restart index)
     const bool dma = a.dma_stage && !a.check_mode && !slow &&

@@ -978,3 +978,60 @@ def test_native_comm_world1_mgpu_compress(H, O, ctx, kind):
         assert (out[:owned].cpu().numpy() == want).all(), i
         assert torch.equal(dec[:n], x[:n]), i
     comm.close()
+
+
+def _shallow_letters(kind, n, rng):
+    if kind == "u100":  # codes of 6-7 bits
+        return rng.integers(0, 100, n).astype(np.uint8)
+    if kind == "u256":  # all 8 bits (the padded stage)
+        return rng.integers(0, 256, n).astype(np.uint8)
+    if kind == "zipf64":  # 1-8 bits
+        return (rng.zipf(1.3, n) % 64).astype(np.uint8)
+    if kind == "dyadic":  # 1-10 bits
+        p = 2.0 ** -np.arange(1, 12)
+        p[-1] = p[-2]
+        return rng.choice(11, n, p=p / p.sum()).astype(np.uint8)
+    return (rng.integers(0, 64, n) + rng.integers(0, 64, n)).astype(np.uint8)  # "tri": up to 12 bits
+
+
+@pytest.mark.parametrize("refill", ["auto", "2"])
+@pytest.mark.parametrize("kind", ["u100", "u256", "zipf64", "dyadic", "tri"])
+def test_shallow_trees_lookups_per_refill(H, O, ctx, kind, refill, monkeypatch):
+    """trees of <= 8 / <= 10 bits decode with 4 / 3 lookups per window refill
+    (decode_wave.hip decode_fixed64's R; HUFF_DEC_REFILL=2 forces two): the
+    general pack matches the oracle's stream, and the restart-index decode and
+    the index-free decode (its skip build) return the input, at a ragged
+    size and at one with a partial task"""
+    import torch
+    from huff_coding import device as D
+
+    monkeypatch.setenv("HUFF_DISABLE_FIXED8", "1")
+    if refill != "auto":
+        monkeypatch.setenv("HUFF_DEC_REFILL", refill)
+    rng = np.random.default_rng(len(kind) * 7 + 1)
+    for n in ((1 << 22) + 77, 5000):
+        host = _shallow_letters(kind, n, rng)
+        w = O.fast_hist(host, 8)
+        ot = O.Tree.from_weights(O.weights_from_array(w))
+        code, ln = ot.code_table()
+        depth = int(ln[w > 0].max())
+        assert depth <= {"u100": 8, "u256": 9, "zipf64": 9, "dyadic": 10, "tri": 16}[kind]
+        if kind == "dyadic":
+            assert depth > 8
+        x = torch.from_numpy(np.concatenate([host, np.zeros(64, np.uint8)])).cuda()
+        job = H.EncodeJob(ctx, x.data_ptr(), n)
+        tree = H.HuffTree.from_weights(H.ByteWeights.from_array(job.hist()))
+        bits = job.bits(tree)
+        out = torch.zeros((bits + 7) // 8 + 64, dtype=torch.uint8, device="cuda")
+        assert job.pack(tree, out.data_ptr(), out.numel()) == bits
+        want, wbits = O.fast_encode(host, code, ln, threads=8)
+        torch.cuda.synchronize()
+        assert wbits == bits and (out[: (bits + 7) // 8].cpu().numpy() == want).all(), (kind, n)
+        dec = torch.full((n + 64,), 0xEE, dtype=torch.uint8, device="cuda")
+        job.decode(tree, out.data_ptr(), dec.data_ptr())
+        torch.cuda.synchronize()
+        assert torch.equal(dec[:n], x[:n]), (kind, n)
+        dec.fill_(0xEE)
+        got = D.decompress_dev(ctx, tree, out.data_ptr(), (bits + 7) // 8, (8 - bits % 8) % 8, dec.data_ptr(), n + 64)
+        torch.cuda.synchronize()
+        assert got == n and torch.equal(dec[:n], x[:n]), (kind, n)
