@@ -19,7 +19,6 @@
 //
 // Roofline: HBM-bound in principle; ceil(bits/8) read + n W written + the
 // restart index (4 B per 64 letters).
-#include <cstdlib>
 #include <type_traits>
 
 #include "bitreader.hpp"
@@ -107,9 +106,8 @@ __device__ __forceinline__ uint64_t shl_window(uint64_t buf, uint32_t len) {
 // One lane's letters [from, from + PL) of its 64, decoded into o (PL * W
 // bytes, PL * W / 4 dwords), window state carried between parts. Window:
 // 64-bit buf, valid-bit count in the low 6 bits of X (the rest don't-care),
-// refilled unconditionally (decode_wave.hip FX_REFILL) every RF codes: a
-// refill leaves >= 32 valid bits, so RF = 1 for codes of 17-32 bits, 2 for
-// <= 16, 3 for <= 10, 4 for <= 8 (a part starts with a refill).
+// refilled unconditionally (decode_wave.hip FX_REFILL): every two codes when
+// codes have <= 16 bits, before every code otherwise (R1).
 template <uint32_t W>
 struct Lane {
     uint64_t buf;
@@ -120,7 +118,7 @@ struct Lane {
 // | s, offset in bits 8..31) continues at level 2 with the next s bits. Both
 // reads are made by every lane (a lane with a level-1 leaf re-reads entry 0:
 // one broadcast address), so lanes never diverge.
-template <uint32_t W, uint32_t PL, bool TWO, int RF, class Words>
+template <uint32_t W, uint32_t PL, bool TWO, bool R1, class Words>
 __device__ __forceinline__ void decode_part(Lane<W>& s, const Words& src, uint32_t (&o)[PL * W / 4 > 0 ? PL * W / 4 : 1],
                                             const EntryT<W>* __restrict__ tab, uint32_t K1,
                                             const uint8_t* __restrict__ letters, bool leaf4) {
@@ -132,7 +130,7 @@ __device__ __forceinline__ void decode_part(Lane<W>& s, const Words& src, uint32
     };
 #pragma unroll
     for (uint32_t i = 0; i < PL; ++i) {
-        if (i % RF == 0) refill();
+        if (R1 || (i & 1) == 0) refill();
         const uint32_t top = static_cast<uint32_t>(s.buf >> 32);
         EntryT<W> e = tab[top >> (32 - K1)];
         if constexpr (TWO) {
@@ -146,9 +144,7 @@ __device__ __forceinline__ void decode_part(Lane<W>& s, const Words& src, uint32
         const uint32_t len = static_cast<uint32_t>(e) & 63u;
         // (8- and 16-byte letters: the split shift keeps the build clear of
         // the shift hazard since the skip loop was added; others unchanged)
-        // (3 or 4 codes per refill: the same, after a 1-byte build put the
-        // amount of a 64-bit shift in its last VGPR)
-        if constexpr (W >= 8 || RF > 2) s.buf = shl_window(s.buf, len);
+        if constexpr (W >= 8) s.buf = shl_window(s.buf, len);
         else s.buf <<= len;
         s.X -= len;
         const uint32_t v = payload<W>(e);
@@ -217,7 +213,7 @@ __device__ __forceinline__ uint32_t row_piece(uint32_t r, uint32_t q) { return r
 // segments (4 lanes each) — lane-strided 16-B stores wrote 2.6x the output
 // bytes to HBM and kept the TA busy (PMC). Else 16-B stores per lane, or
 // bytes when unaligned.
-template <uint32_t W, bool TWO, int RF, class Words>
+template <uint32_t W, bool TWO, bool R1, class Words>
 __device__ __forceinline__ void lane_full(const Words& src, uint32_t rel, uint8_t* dst, const EntryT<W>* tab,
                                           uint32_t K1, const uint8_t* letters, bool aligned, uint8_t* rows,
                                           uint8_t* task_out, uint32_t lane, uint32_t skip, bool leaf4) {
@@ -229,7 +225,7 @@ __device__ __forceinline__ void lane_full(const Words& src, uint32_t rel, uint8_
     lane_skip<W, TWO>(s, src, tab, K1, skip);
     for (uint32_t p = 0; p < kWideRun / PL; ++p) {
         uint32_t o[ND];
-        decode_part<W, PL, TWO, RF>(s, src, o, tab, K1, letters, leaf4);
+        decode_part<W, PL, TWO, R1>(s, src, o, tab, K1, letters, leaf4);
         if (rows) {
             if constexpr (W >= 8) {
                 wave_order();  // the previous part's row reads were issued first
@@ -286,7 +282,7 @@ __device__ __forceinline__ void lane_full(const Words& src, uint32_t rel, uint8_
 }
 
 // the stream's last lane (fewer than 64 letters): one letter at a time
-template <uint32_t W, bool TWO, int RF, class Words>
+template <uint32_t W, bool TWO, bool R1, class Words>
 __device__ __forceinline__ void lane_tail(const Words& src, uint32_t rel, uint32_t cnt, uint8_t* dst,
                                           const EntryT<W>* tab, uint32_t K1, const uint8_t* letters, uint32_t skip,
                                           bool leaf4) {
@@ -295,7 +291,7 @@ __device__ __forceinline__ void lane_tail(const Words& src, uint32_t rel, uint32
     lane_skip<W, TWO>(s, src, tab, K1, skip);
     for (uint32_t j = 0; j < cnt; j += 2) {
         uint32_t o[2 * W / 4 > 0 ? 2 * W / 4 : 1];
-        decode_part<W, 2, TWO, RF>(s, src, o, tab, K1, letters, leaf4);
+        decode_part<W, 2, TWO, R1>(s, src, o, tab, K1, letters, leaf4);
         // bytes [0, 2 W) of o: the pair's letters (the second one past cnt is dropped)
 #pragma unroll
         for (uint32_t b = 0; b < 2 * W; ++b)
@@ -303,7 +299,7 @@ __device__ __forceinline__ void lane_tail(const Words& src, uint32_t rel, uint32
     }
 }
 
-template <uint32_t W, bool TWO, int RF, bool LDS>
+template <uint32_t W, bool TWO, bool R1, bool LDS>
 __global__ __launch_bounds__((LDS ? max_waves<W>() : 4) * 64) void k_wdec_task(WideDecArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const uint32_t K1 = a.stab_bits;
@@ -375,17 +371,17 @@ __global__ __launch_bounds__((LDS ? max_waves<W>() : 4) * 64) void k_wdec_task(W
             const StageWords src{stage};
             const uint32_t rel = static_cast<uint32_t>(lane_bit - b0 * 8);
             if (cnt == kWideRun)
-                lane_full<W, TWO, RF>(src, rel, dst, tab, K1, letters, aligned, trows, task_out, lane, skip, leaf4);
+                lane_full<W, TWO, R1>(src, rel, dst, tab, K1, letters, aligned, trows, task_out, lane, skip, leaf4);
             else if (cnt)
-                lane_tail<W, TWO, RF>(src, rel, cnt, dst, tab, K1, letters, skip, leaf4);
+                lane_tail<W, TWO, R1>(src, rel, cnt, dst, tab, K1, letters, skip, leaf4);
             wave_sync();  // the stage is reused by the next task
         } else {  // longer than the stage: straight from global memory
             const GlobalWords src{a.comp, a.comp_bytes, (lane_bit >> 5)};
             const uint32_t grel = static_cast<uint32_t>(lane_bit & 31);
             if (cnt == kWideRun)
-                lane_full<W, TWO, RF>(src, grel, dst, tab, K1, letters, aligned, trows, task_out, lane, skip, leaf4);
+                lane_full<W, TWO, R1>(src, grel, dst, tab, K1, letters, aligned, trows, task_out, lane, skip, leaf4);
             else if (cnt)
-                lane_tail<W, TWO, RF>(src, grel, cnt, dst, tab, K1, letters, skip, leaf4);
+                lane_tail<W, TWO, R1>(src, grel, cnt, dst, tab, K1, letters, skip, leaf4);
         }
     }
 }
@@ -394,12 +390,9 @@ template <uint32_t W, bool LDS>
 hipError_t launch_as(const WideDecArgs& a, size_t shared, uint32_t waves, hipStream_t s) {
     using Kern = void (*)(WideDecArgs);
     const bool two = a.max_len > a.stab_bits;
-    int rf = a.max_len > 16 ? 1 : (two || a.max_len > 10) ? 2 : a.max_len > 8 ? 3 : 4;
-    if (const char* e = std::getenv("HUFF_DEC_REFILL"); e && e[0] >= '2' && e[0] <= '4' && rf > e[0] - '0')
-        rf = e[0] - '0';  // (A/B and tests: a lower cap, read per call)
-    const Kern k = two ? (rf == 1 ? k_wdec_task<W, true, 1, LDS> : k_wdec_task<W, true, 2, LDS>)
-                       : (rf == 4 ? k_wdec_task<W, false, 4, LDS>
-                                  : rf == 3 ? k_wdec_task<W, false, 3, LDS> : k_wdec_task<W, false, 2, LDS>);
+    const bool r1 = a.max_len > 16;
+    const Kern k = !two ? k_wdec_task<W, false, false, LDS>
+                        : (r1 ? k_wdec_task<W, true, true, LDS> : k_wdec_task<W, true, false, LDS>);
     const size_t lds = shared + size_t(waves) * (a.stage_bytes + row_bytes<W>());
     if (lds > 64 * 1024) {
         const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k),

@@ -410,27 +410,3 @@ def test_index_free_capacity_below_count(W, O, ctx):
     res = out.cpu().numpy()
     assert np.array_equal(res[:n], letters)
     assert (res[n:] == 0x5A5A).all()
-
-
-@pytest.mark.parametrize("refill", ["auto", "2"])
-@pytest.mark.parametrize("dtype,k", [(np.int16, 30), (np.uint16, 70), (np.uint32, 60), (np.int64, 70)])
-def test_shallow_alphabets_codes_per_refill(W, O, ctx, dtype, k, refill, monkeypatch):
-    """alphabets whose codes fit 8 or 10 bits: the task decoder takes 4 or 3
-    codes per window refill (wdecode.hip RF; HUFF_DEC_REFILL=2 caps it at
-    two); restart-index and index-free decode return the letters, and the
-    stream equals the oracle's"""
-    if refill != "auto":
-        monkeypatch.setenv("HUFF_DEC_REFILL", refill)
-    rng = np.random.default_rng(k * 13 + len(refill))
-    for n in (1, 4095, 65537, 400_003):
-        letters = zipf_letters(rng, n, dtype, k=k)
-        items = list(W.build_weights_map(letters, ctx).items())
-        t = W.WideTree.from_weights(items, dtype)
-        if n > 1000:  # (ties may deepen a tree by a level: 11 bits decode two codes per refill)
-            assert max(len(c) for c in t.read_codes().values()) <= 11
-        cd = W.compress_with_tree(letters, t, ctx)
-        (ocomp, opad), _ = oracle_stream(O, letters, items, 8 * np.dtype(dtype).itemsize)
-        assert cd.comp_bytes() == ocomp and cd.padding_bits() == opad
-        assert np.array_equal(W.decompress(cd, ctx), letters), (dtype, n)
-        back_cd = W.WideCompressData.try_from_bytes(cd.to_bytes(), dtype)
-        assert np.array_equal(W.decompress(back_cd, ctx), letters), (dtype, n)
