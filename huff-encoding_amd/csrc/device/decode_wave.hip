@@ -53,6 +53,12 @@ static_assert(kChunk % kTaskSym == 0, "a task never straddles a chunk");
 #define HUFF_DEC_PAD_WAVES 5
 #endif
 constexpr bool kEarlyLoads = HUFF_DEC_EARLY_LOADS != 0;
+// the index-free skip codes at 4 per refill too when the letters take 4
+// (HUFF_SKIP_R=0: two, for the A/B build)
+#ifndef HUFF_SKIP_R
+#define HUFF_SKIP_R 1
+#endif
+constexpr bool kSkipR = HUFF_SKIP_R != 0;
 constexpr int kPadWaves = HUFF_DEC_PAD_WAVES;
 
 struct Task {
@@ -317,7 +323,24 @@ __device__ __forceinline__ void decode_fixed64(const Words& src, uint32_t rel, u
 #ifdef HUFF_SKIP_EXPERIMENT  // timing only (wrong letters): 1 = no skip codes, 2 = the wave's max for all lanes
     if constexpr (SKIP) skip = HUFF_SKIP_EXPERIMENT == 1 ? 0u : __reduce_max_sync(~0ull, skip);
 #endif
-    if constexpr (SKIP) {  // codes before this lane's first letter: decoded, not kept
+    if constexpr (SKIP && R == 4 && kSkipR) {  // the same at 4 codes per refill (codes of <= 8 bits)
+        for (uint32_t j = skip; j >= 4; j -= 4) {
+            FX_REFILL();
+            FX_STEP();
+            FX_STEP();
+            FX_STEP();
+            FX_STEP();
+        }
+        if (skip & 2u) {
+            FX_REFILL();
+            FX_STEP();
+            FX_STEP();
+        }
+        if (skip & 1u) {
+            FX_REFILL();
+            FX_STEP();
+        }
+    } else if constexpr (SKIP) {  // codes before this lane's first letter: decoded, not kept
         for (uint32_t j = skip; j >= 2; j -= 2) {
             FX_REFILL();
             FX_STEP();
