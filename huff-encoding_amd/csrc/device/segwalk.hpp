@@ -79,6 +79,12 @@ __device__ __forceinline__ Staged stage_block(const A& a, uint32_t* w, uint32_t 
 // path per lookup) cost ~40 VALU and ~40 SALU per step in the multi-symbol
 // form this replaces (PMC: 344 K VALU per SIMD per GiB).
 constexpr int kChunkSteps = 8;
+// refills every 3rd / 4th step for tables of <= 10 / <= 8 bits
+// (HUFF_WALK_R=0: every 2nd, for the A/B build)
+#ifndef HUFF_WALK_R
+#define HUFF_WALK_R 1
+#endif
+constexpr bool kWalkR = HUFF_WALK_R != 0;
 
 // lane cursor over the staged range: 64-bit window, valid bits in the low 6
 // bits of X (X -= entry borrows only above them), refilled unconditionally
@@ -181,12 +187,20 @@ struct Cursor {
         X -= e;
         return e & 63u;
     }
+    // the steps of a chunk that refill first: a refill leaves >= 32 valid
+    // bits and a step consumes <= K bits when no code is longer than the
+    // K-bit table (K = min(depth, 12)), so every 4th step for K <= 8, every
+    // 3rd for K <= 10, else every 2nd (K is wave-uniform: a scalar branch)
+    __device__ __forceinline__ static uint32_t refill_steps(uint32_t K) {
+        return !kWalkR || K > 10 ? 0x55u : K > 8 ? 0x49u : 0x11u;
+    }
     template <bool SLOW>
     __device__ __forceinline__ void chunk(uint32_t (&L)[kChunkSteps], const uint16_t* stab, uint32_t K,
                                           const uint32_t* glut, uint32_t Kg) {
+        const uint32_t rs = SLOW ? 0x55u : refill_steps(K);
 #pragma unroll
         for (int k = 0; k < kChunkSteps; ++k) {
-            if ((k & 1) == 0) refill();
+            if ((rs >> k) & 1u) refill();
             L[k] = step<SLOW>(stab, K, glut, Kg);
         }
     }
@@ -198,9 +212,10 @@ struct Cursor {
                                                 uint32_t K, const uint32_t* glut, uint32_t Kg) {
         U = 0;
         N = 0;
+        const uint32_t rs = SLOW ? 0x55u : refill_steps(K);
 #pragma unroll
         for (int k = 0; k < kChunkSteps; ++k) {
-            if ((k & 1) == 0) refill();
+            if ((rs >> k) & 1u) refill();
             const uint32_t e = wtab[static_cast<uint32_t>(buf >> 32) >> (32 - K)];
             if (SLOW && dense) {
                 const uint32_t l1 = dense_len(e, K);
@@ -228,9 +243,10 @@ struct Cursor {
                                                 const uint16_t* wtab, const uint16_t* stab, uint32_t K,
                                                 const uint32_t* glut, uint32_t Kg) {
         uint32_t Q = 0;
+        const uint32_t rs = SLOW ? 0x55u : refill_steps(K);
 #pragma unroll
         for (int k = 0; k < kChunkSteps; ++k) {
-            if ((k & 1) == 0) refill();
+            if ((rs >> k) & 1u) refill();
             const uint32_t e = wtab[static_cast<uint32_t>(buf >> 32) >> (32 - K)];
             if (SLOW && (e & kSsSlow)) {
                 Q += step_entry<SLOW>(e, K, glut, Kg) + (1u << 16);
